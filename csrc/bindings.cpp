@@ -1,0 +1,187 @@
+// Python bindings (pybind11) for the native MI355X runtime.  Tensors cross the boundary as raw
+// device pointers (tensor.data_ptr()) and HIP streams as integer handles
+// (torch.cuda.Stream.cuda_stream): the runtime never includes libtorch headers, so it is immune
+// to torch C++ ABI details and compiles in seconds.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+
+#include "include/kernels.h"
+#include "runtime/engine.h"
+#include "runtime/rccl_comm.h"
+
+namespace py = pybind11;
+using namespace mnist;
+
+namespace {
+template <typename T>
+T* P(uintptr_t x) { return reinterpret_cast<T*>(x); }
+hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(x); }
+
+void check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
+}
+
+EngineBuffers buffers_from_dict(const py::dict& d) {
+  EngineBuffers b;
+  auto get = [&](const char* k) -> uintptr_t {
+    if (!d.contains(k)) return 0;
+    return d[k].cast<uintptr_t>();
+  };
+  b.param = P<float>(get("param"));
+  b.grad = P<float>(get("grad"));
+  b.square_avg = P<float>(get("square_avg"));
+  b.acc_delta = P<float>(get("acc_delta"));
+  b.lr = P<float>(get("lr"));
+  b.w2f = P<uint16_t>(get("w2f"));
+  b.w2d = P<uint16_t>(get("w2d"));
+  b.w1 = P<uint16_t>(get("w1"));
+  b.w1t = P<uint16_t>(get("w1t"));
+  b.state = P<StepState>(get("state"));
+  b.loss_log = P<float>(get("loss_log"));
+  b.train_u8 = P<const uint8_t>(get("train_u8"));
+  b.train_labels = P<const int32_t>(get("train_labels"));
+  b.train_idx = P<const int32_t>(get("train_idx"));
+  b.test_u8 = P<const uint8_t>(get("test_u8"));
+  b.test_labels = P<const int32_t>(get("test_labels"));
+  b.test_idx = P<const int32_t>(get("test_idx"));
+  b.test_loss_rows = P<float>(get("test_loss_rows"));
+  b.test_correct = P<int32_t>(get("test_correct"));
+  if (!b.param || !b.grad || !b.square_avg || !b.acc_delta || !b.lr || !b.w2f || !b.w2d || !b.w1 ||
+      !b.w1t || !b.state)
+    throw std::runtime_error("engine buffers: missing model/optimizer pointer");
+  return b;
+}
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X (gfx950) native kernels + runtime for the MNIST DDP framework";
+
+  m.attr("PARAM_TOTAL") = PARAM_TOTAL;
+  m.attr("FC1_KSPLIT") = FC1_KSPLIT;
+  py::dict offs;
+  offs["fc1.weight"] = OFF_FC1_W; offs["fc1.bias"] = OFF_FC1_B;
+  offs["fc2.weight"] = OFF_FC2_W; offs["fc2.bias"] = OFF_FC2_B;
+  offs["conv1.weight"] = OFF_CONV1_W; offs["conv1.bias"] = OFF_CONV1_B;
+  offs["conv2.weight"] = OFF_CONV2_W; offs["conv2.bias"] = OFF_CONV2_B;
+  m.attr("PARAM_OFFSETS") = offs;
+  m.attr("BUCKET_SPLIT") = OFF_CONV1_W;
+  m.def("conv_wgrad_groups", &conv_wgrad_groups);
+
+  // ---------------- per-kernel entry points ----------------
+  m.def("trunk_fwd", [](uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t w1c,
+                        uintptr_t b1c, uintptr_t w2f, uintptr_t b2c, uintptr_t a1_out, uintptr_t p_out,
+                        uintptr_t pmask_out, int B, bool train, uintptr_t stream) {
+    TrunkFwdArgs a{P<const uint8_t>(data_u8), P<const int32_t>(idx), idx_stride, P<const StepState>(state),
+                   P<const float>(w1c), P<const float>(b1c), P<const uint16_t>(w2f), P<const float>(b2c),
+                   P<uint16_t>(a1_out), P<uint16_t>(p_out), P<uint8_t>(pmask_out)};
+    launch_trunk_fwd(a, B, train, S(stream));
+    check_launch();
+  });
+  m.def("fc1_fwd", [](uintptr_t p, uintptr_t w1, uintptr_t z1part, int B, uintptr_t stream) {
+    launch_fc1_fwd(P<const uint16_t>(p), P<const uint16_t>(w1), P<float>(z1part), B, S(stream));
+    check_launch();
+  });
+  m.def("head_train", [](uintptr_t z1part, uintptr_t b_fc1, uintptr_t w_fc2, uintptr_t b_fc2, uintptr_t labels,
+                         uintptr_t idx, int64_t idx_stride, uintptr_t state, float inv_batch, uintptr_t loss_rows,
+                         uintptr_t dz1, uintptr_t h_bf, uintptr_t dl_bf, int B, int Bp, uintptr_t stream) {
+    HeadArgs a{};
+    a.z1part = P<const float>(z1part); a.b_fc1 = P<const float>(b_fc1); a.w_fc2 = P<const float>(w_fc2);
+    a.b_fc2 = P<const float>(b_fc2); a.labels = P<const int32_t>(labels); a.idx = P<const int32_t>(idx);
+    a.idx_step_stride = idx_stride; a.state = P<const StepState>(state); a.inv_batch = inv_batch;
+    a.loss_rows = P<float>(loss_rows); a.dz1 = P<uint16_t>(dz1); a.h_bf = P<uint16_t>(h_bf);
+    a.dl_bf = P<uint16_t>(dl_bf);
+    launch_head_train(a, B, Bp, S(stream));
+    check_launch();
+  });
+  m.def("head_eval", [](uintptr_t z1part, uintptr_t b_fc1, uintptr_t w_fc2, uintptr_t b_fc2, uintptr_t labels,
+                        uintptr_t idx, uintptr_t loss_rows, uintptr_t correct, uintptr_t logp, int B,
+                        uintptr_t stream) {
+    HeadArgs a{};
+    a.z1part = P<const float>(z1part); a.b_fc1 = P<const float>(b_fc1); a.w_fc2 = P<const float>(w_fc2);
+    a.b_fc2 = P<const float>(b_fc2); a.labels = P<const int32_t>(labels); a.idx = P<const int32_t>(idx);
+    a.loss_rows = P<float>(loss_rows); a.correct_out = P<int32_t>(correct); a.logp_out = P<float>(logp);
+    launch_head_eval(a, B, S(stream));
+    check_launch();
+  });
+  m.def("fc_bwd", [](uintptr_t dz1, uintptr_t p, uintptr_t pmask, uintptr_t w1t, uintptr_t h_bf, uintptr_t dl_bf,
+                     uintptr_t loss_rows, uintptr_t state, uintptr_t grad, uintptr_t g, uintptr_t loss_log,
+                     float grad_scale, float inv_batch, int B, int Bp, uintptr_t stream) {
+    FcBwdArgs a{P<const uint16_t>(dz1), P<const uint16_t>(p), P<const uint8_t>(pmask), P<const uint16_t>(w1t),
+                P<const uint16_t>(h_bf), P<const uint16_t>(dl_bf), P<const float>(loss_rows),
+                P<const StepState>(state), P<float>(grad), P<uint16_t>(g), P<float>(loss_log), grad_scale,
+                inv_batch};
+    launch_fc_bwd(a, B, Bp, S(stream));
+    check_launch();
+  });
+  m.def("conv_bwd", [](uintptr_t g, uintptr_t pmask, uintptr_t a1, uintptr_t w2d, uintptr_t w1c, uintptr_t b1c,
+                       uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t c1part,
+                       uintptr_t w2part, uintptr_t grad, float grad_scale, int B, uintptr_t stream) {
+    ConvBwdArgs a{P<const uint16_t>(g), P<const uint8_t>(pmask), P<const uint16_t>(a1), P<const uint16_t>(w2d),
+                  P<const float>(w1c), P<const float>(b1c), P<const uint8_t>(data_u8), P<const int32_t>(idx),
+                  idx_stride, P<const StepState>(state), P<float>(c1part), P<float>(w2part), P<float>(grad),
+                  grad_scale, conv_wgrad_groups(B)};
+    launch_conv_bwd(a, B, S(stream));
+    launch_conv_grad_reduce(a, B, S(stream));
+    check_launch();
+  });
+  m.def("adadelta", [](uintptr_t param, uintptr_t grad, uintptr_t sq, uintptr_t acc, uintptr_t lr, float rho,
+                       float eps, float wd, uintptr_t w2f, uintptr_t w2d, uintptr_t w1, uintptr_t w1t,
+                       uintptr_t state_inc, int region, bool update, uintptr_t stream) {
+    AdadeltaArgs a{P<float>(param), P<const float>(grad), P<float>(sq), P<float>(acc), P<const float>(lr), rho,
+                   eps, wd, P<uint16_t>(w2f), P<uint16_t>(w2d), P<uint16_t>(w1), P<uint16_t>(w1t),
+                   P<StepState>(state_inc)};
+    if (update) launch_adadelta(a, region, S(stream));
+    else launch_refresh_shadows(a, S(stream));
+    check_launch();
+  });
+
+  // ---------------- communicator ----------------
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int world, int rank, int device) {
+             std::string s = uid;
+             return std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device);
+           }),
+           py::arg("unique_id"), py::arg("world_size"), py::arg("rank"), py::arg("device"))
+      .def_static("available", &RcclComm::available)
+      .def_static("version", &RcclComm::version)
+      .def_static("unique_id", []() {
+        auto v = RcclComm::unique_id();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("allreduce_sum", [](RcclComm& c, uintptr_t buf, int64_t count, int dtype, uintptr_t stream) {
+        c.allreduce_sum(P<void>(buf), count, dtype, S(stream));
+      })
+      .def("broadcast", [](RcclComm& c, uintptr_t buf, int64_t count, int dtype, int root, uintptr_t stream) {
+        c.broadcast(P<void>(buf), count, dtype, root, S(stream));
+      })
+      .def_property_readonly("world_size", &RcclComm::world_size)
+      .def_property_readonly("rank", &RcclComm::rank);
+
+  // ---------------- engine ----------------
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](py::dict bufs, int max_batch, int max_test_batch, uintptr_t compute, uintptr_t comm,
+                       int world, float rho, float eps, float wd) {
+             return new Engine(buffers_from_dict(bufs), max_batch, max_test_batch, S(compute), S(comm), world, rho,
+                               eps, wd);
+           }),
+           py::arg("buffers"), py::arg("max_batch"), py::arg("max_test_batch"), py::arg("compute_stream"),
+           py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
+      .def("attach_comm", &Engine::attach_comm)
+      .def("set_bucket_split", &Engine::set_bucket_split)
+      .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
+      .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
+      .def("capture_train", &Engine::capture_train)
+      .def("replay", &Engine::replay, py::call_guard<py::gil_scoped_release>())
+      .def("eval", &Engine::eval)
+      .def("capture_eval", &Engine::capture_eval)
+      .def("refresh_shadows", &Engine::refresh_shadows)
+      .def("broadcast_params", &Engine::broadcast_params)
+      .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("workspace_bytes", &Engine::workspace_bytes);
+
+  m.def("roctx_push", [](const std::string& s) { roctx_push(s.c_str()); });
+  m.def("roctx_pop", []() { roctx_pop(); });
+}

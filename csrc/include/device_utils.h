@@ -1,0 +1,93 @@
+// Device-side helpers (MFMA fragment types, bf16 conversion, LDS transpose reads, Philox RNG).
+// Included only by the .hip kernel translation units.
+#pragma once
+#include "mnist_common.h"
+
+namespace mnist {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(4))) float floatx4;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ floatx4 mfma16x16x32(const bf16x8& a, const bf16x8& b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16-byte LDS / global fragment loads (8 bf16)
+__device__ __forceinline__ bf16x8 ld16(const uint16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+__device__ __forceinline__ bf16x8 zero_frag() {
+  u32x4 z = {0u, 0u, 0u, 0u};
+  return __builtin_bit_cast(bf16x8, z);
+}
+
+// gfx950 ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p passes the address of row q,
+// columns 4p..4p+3; lane i receives column i of the 4 rows.  Two of them give an 8-deep k slice.
+__device__ __forceinline__ short4_t lds_tr16(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
+}
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* row_lo, const uint16_t* row_hi) {
+  short4_t a = lds_tr16(row_lo), b = lds_tr16(row_hi);
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  short8_t v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Philox-4x32-10 (Salmon et al. 2011), the counter-based generator family torch uses for dropout.
+__device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  u32x4 r = {c0, c1, c2, c3};
+  return r;
+}
+// Random words for elements [4*quad, 4*quad+4) of one dropout invocation (counter = offset).
+__device__ __forceinline__ u32x4 dropout_words(uint64_t seed, uint64_t offset, uint64_t quad) {
+  return philox4x32((uint32_t)quad, (uint32_t)(quad >> 32), (uint32_t)offset,
+                    (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// conv1 pre-activation at one output pixel/channel from an fp32 input tile with row stride 28.
+// Shared by the forward kernel and the backward relu-mask recompute so both see identical bits.
+__device__ __forceinline__ float conv1_preact(const float* x, int stride, const float* w9, float b) {
+  float acc = b;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) acc = __builtin_fmaf(x[ky * stride + kx], w9[ky * 3 + kx], acc);
+  return acc;
+}
+
+__device__ __forceinline__ float normalize_u8(uint8_t v) {
+  return ((float)v / 255.0f - MNIST_MEAN) / MNIST_STD;
+}
+
+}  // namespace mnist

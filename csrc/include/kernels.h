@@ -1,0 +1,114 @@
+// Host-visible launch interface of the hand-written gfx950 kernels.  Every launcher only
+// enqueues on the given stream (no allocation, no sync) so the sequences are graph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mnist_common.h"
+
+namespace mnist {
+
+// ---------------- forward ----------------
+struct TrunkFwdArgs {
+  const uint8_t* data_u8;     // [N][784] raw dataset, HBM resident
+  const int32_t* idx;         // epoch index vector; row b of step s = idx[s*idx_step_stride + b]
+  int64_t idx_step_stride;    // = batch size for the training stream, 0 for a fixed batch
+  const StepState* state;     // step counter + dropout RNG (may be null in eval)
+  const float* w1c;           // conv1.weight fp32 [32][9]
+  const float* b1c;           // conv1.bias   fp32 [32]
+  const uint16_t* w2f;        // conv2 weight bf16 [64][9][32]
+  const float* b2c;           // conv2.bias   fp32 [64]
+  uint16_t* a1_out;           // bf16 [B][26][26][32]  (train only)
+  uint16_t* p_out;            // bf16 [B][9216]
+  uint8_t* pmask_out;         // u8   [B][9216]        (train only)
+};
+void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
+
+// fc1 split-K partial GEMM: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
+constexpr int FC1_KSPLIT = 16;
+void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s);
+
+// Head: reduce fc1 partials + bias -> ReLU -> dropout(0.5) -> fc2 -> log_softmax (+ NLL + backward)
+struct HeadArgs {
+  const float* z1part;        // [FC1_KSPLIT][B][128]
+  const float* b_fc1;         // [128]
+  const float* w_fc2;         // [10][128] fp32
+  const float* b_fc2;         // [10]
+  const int32_t* labels;      // train: dataset labels [N] gathered through idx; eval: same
+  const int32_t* idx;
+  int64_t idx_step_stride;
+  const StepState* state;
+  float inv_batch;            // 1/B (nll mean)
+  // outputs (train)
+  float* loss_rows;           // [B] per-row NLL
+  uint16_t* dz1;              // bf16 [Bp][128] grad wrt fc1 pre-activation (rows >= B zeroed)
+  uint16_t* h_bf;             // bf16 [Bp][128] fc1 activations after ReLU+dropout (rows >= B zeroed)
+  uint16_t* dl_bf;            // bf16 [Bp][16]  d loss / d logits (cols >= 10, rows >= B zeroed)
+  // outputs (eval)
+  float* logp_out;            // optional [B][10]
+  int32_t* correct_out;       // [B] 1 if argmax == label
+};
+void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s);
+void launch_head_eval(const HeadArgs& a, int B, hipStream_t s);
+
+// ---------------- backward ----------------
+struct FcBwdArgs {
+  const uint16_t* dz1;        // bf16 [Bp][128]
+  const uint16_t* p;          // bf16 [Bp][9216] (rows >= B are masked)
+  const uint8_t* pmask;       // [B][9216]
+  const uint16_t* w1t;        // bf16 [9216][128]
+  const uint16_t* h_bf;       // bf16 [Bp][128]
+  const uint16_t* dl_bf;      // bf16 [Bp][16]
+  const float* loss_rows;     // [B]
+  const StepState* state;
+  float* grad;                // flat fp32 grad buffer (writes fc1.w, fc1.b, fc2.w, fc2.b)
+  uint16_t* g;                // bf16 [B][9216] grad wrt conv2 pooled output (pre-dropout, masked)
+  float* loss_log;            // [steps] mean loss per step (indexed by state->step)
+  float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
+  float inv_batch;
+};
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
+
+struct ConvBwdArgs {
+  const uint16_t* g;          // bf16 [B][9216]
+  const uint8_t* pmask;       // [B][9216]
+  const uint16_t* a1;         // bf16 [B][26][26][32]
+  const uint16_t* w2d;        // bf16 [9][32][64]
+  const float* w1c;           // conv1 fp32 [32][9]
+  const float* b1c;           // [32]
+  const uint8_t* data_u8;
+  const int32_t* idx;
+  int64_t idx_step_stride;
+  const StepState* state;
+  float* c1part;              // [4*B][320] conv1 wgrad(288)+bias(32) partials (dgrad kernel)
+  float* w2part;              // [G][18432 + 64] conv2 wgrad + bias partials
+  float* grad;                // flat fp32 grad buffer (conv params written by the reduce kernel)
+  float grad_scale;
+  int wgrad_groups;           // G
+};
+int conv_wgrad_groups(int B);
+void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad
+void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s);
+
+// ---------------- optimizer ----------------
+struct AdadeltaArgs {
+  float* param;               // flat fp32
+  const float* grad;
+  float* square_avg;
+  float* acc_delta;
+  const float* lr;            // device scalar (StepLR writes it once per epoch)
+  float rho, eps, weight_decay;
+  uint16_t* w2f;              // bf16 shadows refreshed in the same pass
+  uint16_t* w2d;
+  uint16_t* w1;
+  uint16_t* w1t;
+  StepState* state_inc;       // if non-null, block 0 advances state->step (end-of-step marker)
+};
+enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
+void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
+// Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
+void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
+
+// misc
+void launch_set_step(StepState* st, int step, hipStream_t s);
+
+}  // namespace mnist

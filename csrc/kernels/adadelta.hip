@@ -1,0 +1,158 @@
+// Fused multi-tensor Adadelta over the flat fp32 parameter buffer + bf16 shadow-weight refresh.
+//
+// Replaces optim.Adadelta(model.parameters(), lr) .step() (reference mnist_ddp.py:176, :73), which on
+// the GPU is a chain of ~11 torch._foreach_* kernels (torch/optim/adadelta.py _multi_tensor_adadelta),
+// and the weight casts the forward would otherwise need.  Per element, in torch's foreach order:
+//     sq  = sq*rho + (1-rho)*g*g
+//     d   = sqrt(acc+eps) / sqrt(sq+eps) * g
+//     acc = acc*rho + (1-rho)*d*d
+//     p  += -lr * d
+// One read of g, read-modify-write of sq/acc/p, and in the same pass the bf16 copies the next
+// forward/backward consume are written in the layouts their MFMA fragments want:
+//   fc1.weight -> w1 [128][9216] and w1t [9216][128] (64x64 tiles transposed through LDS),
+//   conv2.weight -> w2f [64][9][32] and w2d [9][32][64].
+// lr is read from device memory so a captured graph picks up StepLR changes.
+#include "../include/device_utils.h"
+#include "../include/kernels.h"
+
+namespace mnist {
+
+namespace {
+constexpr int FC1_TILES = 2 * (NFLAT / 64);                       // 288 64x64 tiles of fc1.weight
+constexpr int64_t FC_TAIL_N = OFF_CONV1_W - OFF_FC1_B;            // 1472 (fc1.b, fc2.w, fc2.b + pad)
+constexpr int64_t CONV_N = PARAM_TOTAL - OFF_CONV1_W;             // 18880
+constexpr int CONV_WGS = (int)((CONV_N / 4 + 255) / 256);         // 19
+
+struct Ada {
+  float rho, eps, wd, lr;
+  __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {
+    if (wd != 0.0f) g = g + wd * p;
+    sq = sq * rho;
+    sq = sq + (1.0f - rho) * g * g;
+    const float sd = sqrtf(sq + eps);
+    float d = sqrtf(acc + eps);
+    d = d / sd;
+    d = d * g;
+    acc = acc * rho;
+    acc = acc + (1.0f - rho) * d * d;
+    p = p + (-lr) * d;
+    return p;
+  }
+};
+
+__device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, float v) {
+  const int rel = (int)(e - OFF_CONV2_W);
+  if (rel < 0 || rel >= C2 * C1 * 9) return;
+  const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
+  const uint16_t h = f2bf(v);
+  a.w2f[(co * 9 + t) * C1 + ci] = h;
+  a.w2d[(t * C1 + ci) * C2 + co] = h;
+}
+
+template <bool UPDATE>
+__device__ __forceinline__ void elementwise(const AdadeltaArgs& a, const Ada& ad, int64_t begin, int64_t n,
+                                            int wg, int nwg) {
+  for (int64_t v = (int64_t)wg * 256 + threadIdx.x; v < n / 4; v += (int64_t)nwg * 256) {
+    const int64_t e = begin + 4 * v;
+    float4 p = *reinterpret_cast<float4*>(a.param + e);
+    if (UPDATE) {
+      const float4 g = *reinterpret_cast<const float4*>(a.grad + e);
+      float4 sq = *reinterpret_cast<float4*>(a.square_avg + e);
+      float4 ac = *reinterpret_cast<float4*>(a.acc_delta + e);
+      ad.step(p.x, g.x, sq.x, ac.x);
+      ad.step(p.y, g.y, sq.y, ac.y);
+      ad.step(p.z, g.z, sq.z, ac.z);
+      ad.step(p.w, g.w, sq.w, ac.w);
+      *reinterpret_cast<float4*>(a.param + e) = p;
+      *reinterpret_cast<float4*>(a.square_avg + e) = sq;
+      *reinterpret_cast<float4*>(a.acc_delta + e) = ac;
+    }
+    if (e + 3 >= OFF_CONV2_W && e < OFF_CONV2_W + C2 * C1 * 9) {
+      conv2_shadow(a, e, p.x);
+      conv2_shadow(a, e + 1, p.y);
+      conv2_shadow(a, e + 2, p.z);
+      conv2_shadow(a, e + 3, p.w);
+    }
+  }
+}
+
+template <bool UPDATE>
+__device__ __forceinline__ void fc1_tile(const AdadeltaArgs& a, const Ada& ad, int tile, uint16_t* ts) {
+  constexpr int TS = 72;  // padded LDS row (bf16 elements)
+  const int ot = tile / (NFLAT / 64), it = tile - ot * (NFLAT / 64);
+  const int t = threadIdx.x;
+  const int ol = t >> 2, ic = (t & 3) * 16;
+  const int o = 64 * ot + ol, i0 = 64 * it;
+  const int64_t e0 = OFF_FC1_W + (int64_t)o * NFLAT + i0 + ic;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float4 p = *reinterpret_cast<float4*>(a.param + e0 + 4 * j);
+    if (UPDATE) {
+      const float4 g = *reinterpret_cast<const float4*>(a.grad + e0 + 4 * j);
+      float4 sq = *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j);
+      float4 ac = *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j);
+      ad.step(p.x, g.x, sq.x, ac.x);
+      ad.step(p.y, g.y, sq.y, ac.y);
+      ad.step(p.z, g.z, sq.z, ac.z);
+      ad.step(p.w, g.w, sq.w, ac.w);
+      *reinterpret_cast<float4*>(a.param + e0 + 4 * j) = p;
+      *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j) = sq;
+      *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j) = ac;
+    }
+    v[4 * j] = p.x; v[4 * j + 1] = p.y; v[4 * j + 2] = p.z; v[4 * j + 3] = p.w;
+  }
+  uint4 lo, hi;
+  lo.x = pack2bf(v[0], v[1]); lo.y = pack2bf(v[2], v[3]); lo.z = pack2bf(v[4], v[5]); lo.w = pack2bf(v[6], v[7]);
+  hi.x = pack2bf(v[8], v[9]); hi.y = pack2bf(v[10], v[11]); hi.z = pack2bf(v[12], v[13]); hi.w = pack2bf(v[14], v[15]);
+  uint4* w1p = reinterpret_cast<uint4*>(a.w1 + (int64_t)o * NFLAT + i0 + ic);
+  w1p[0] = lo;
+  w1p[1] = hi;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) ts[(ic + j) * TS + ol] = f2bf(v[j]);
+  __syncthreads();
+  const int il = t >> 2, oc = (t & 3) * 16;
+  const uint4* src = reinterpret_cast<const uint4*>(ts + il * TS + oc);
+  uint4* dst = reinterpret_cast<uint4*>(a.w1t + (int64_t)(i0 + il) * NH + 64 * ot + oc);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+}  // namespace
+
+template <bool UPDATE>
+__global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int region) {
+  __shared__ __attribute__((aligned(16))) uint16_t ts[64 * 72];
+  Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
+  int bid = blockIdx.x;
+  if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (region != ADA_CONV) {
+    if (bid < FC1_TILES) { fc1_tile<UPDATE>(a, ad, bid, ts); return; }
+    bid -= FC1_TILES;
+    if (bid == 0) { elementwise<UPDATE>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
+    bid -= 1;
+  }
+  elementwise<UPDATE>(a, ad, OFF_CONV1_W, CONV_N, bid, CONV_WGS);
+}
+
+static int adadelta_grid(int region) {
+  if (region == ADA_FC) return FC1_TILES + 1;
+  if (region == ADA_CONV) return CONV_WGS;
+  return FC1_TILES + 1 + CONV_WGS;
+}
+
+void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s) {
+  hipLaunchKernelGGL(adadelta_kernel<true>, dim3(adadelta_grid(region)), dim3(256), 0, s, a, region);
+}
+
+void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s) {
+  AdadeltaArgs b = a;
+  b.state_inc = nullptr;
+  hipLaunchKernelGGL(adadelta_kernel<false>, dim3(adadelta_grid(ADA_ALL)), dim3(256), 0, s, b, (int)ADA_ALL);
+}
+
+__global__ void set_step_kernel(StepState* st, int step) { st->step = step; }
+void launch_set_step(StepState* st, int step, hipStream_t s) {
+  hipLaunchKernelGGL(set_step_kernel, dim3(1), dim3(1), 0, s, st, step);
+}
+
+}  // namespace mnist

@@ -1,0 +1,393 @@
+// fc1 forward (split-K MFMA GEMM), the fused head (bias+ReLU+dropout(0.5)+fc2+log_softmax+NLL and
+// its backward), and the fused fc backward (dW_fc1, db_fc1, dW_fc2, db_fc2, dgrad to the conv trunk).
+//
+// Reference ops replaced: mnist_ddp.py:57-61 (fc1, relu, dropout2, fc2, log_softmax), :71 (nll_loss)
+// and their autograd backward at :72.
+#include "../include/device_utils.h"
+#include "../include/kernels.h"
+
+namespace mnist {
+
+// ============================================================================================
+// fc1 forward: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
+// M = B rows, N = 128, K = 9216 split 16 ways (576 each).  One wave = 16 rows x 128 cols x one
+// K-chunk; fragments stream straight from L2 (w1 is 2.4 MB bf16, L2/MALL resident) into VGPRs.
+// ============================================================================================
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
+                                                      const uint16_t* __restrict__ w1,
+                                                      float* __restrict__ z1part, int B) {
+  constexpr int KC = NFLAT / FC1_KSPLIT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = lane & 15, kg = lane >> 4;
+  const int chunk = blockIdx.y * 4 + wave;
+  const int row = blockIdx.x * 16 + m;
+  const bool valid = row < B;
+  const uint16_t* pa = p + (int64_t)(valid ? row : 0) * NFLAT + chunk * KC + 8 * kg;
+  const uint16_t* pb = w1 + (int64_t)m * NFLAT + chunk * KC + 8 * kg;
+  floatx4 acc[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int ks = 0; ks < KC / 32; ++ks) {
+    bf16x8 A = ld16(pa + ks * 32);
+    if (!valid) A = zero_frag();
+    bf16x8 Bf[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) Bf[nt] = ld16(pb + (int64_t)nt * 16 * NFLAT + ks * 32);
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) acc[nt] = mfma16x16x32(A, Bf[nt], acc[nt]);
+  }
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = blockIdx.x * 16 + 4 * kg + r;
+      if (b < B) z1part[((int64_t)chunk * B + b) * NH + nt * 16 + m] = acc[nt][r];
+    }
+}
+
+void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s) {
+  dim3 grid((B + 15) / 16, FC1_KSPLIT / 4);
+  hipLaunchKernelGGL(fc1_fwd_kernel, grid, dim3(256), 0, s, p, w1, z1part, B);
+}
+
+// ============================================================================================
+// Head (one wave per batch row; lane owns hidden units o = lane and lane + 64)
+// ============================================================================================
+namespace {
+struct HeadRow {
+  float z[2], h[2];
+  bool keep[2];
+  float logit[NCLS];
+};
+
+__device__ __forceinline__ void head_forward_row(const HeadArgs& a, int B, int b, int lane, bool train,
+                                                 bool no_dropout, uint64_t seed, uint64_t off, HeadRow& r) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = lane + 64 * j;
+    float z = a.b_fc1[o];
+    // torch adds the bias after the GEMM; the partial sums are accumulated in fixed chunk order
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < FC1_KSPLIT; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
+    z += s;
+    r.z[j] = z;
+    float h = fmaxf(z, 0.0f);
+    bool keep = true;
+    if (train) {
+      if (!no_dropout) {
+        const u32x4 w = dropout_words(seed, off, ((uint64_t)b * NH + o) >> 2);
+        keep = w[o & 3] < KEEP2_THR;
+      }
+      h = keep ? (no_dropout ? h : h * (1.0f / KEEP2)) : 0.0f;
+    }
+    r.keep[j] = keep;
+    r.h[j] = h;
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float v = r.h[0] * a.w_fc2[c * NH + lane] + r.h[1] * a.w_fc2[c * NH + lane + 64];
+    r.logit[c] = wave_sum(v) + a.b_fc2[c];
+  }
+}
+
+// torch log_softmax: (x - max) - log(sum(exp(x - max)))
+__device__ __forceinline__ void log_softmax10(const float* x, float* lp) {
+  float mx = x[0];
+#pragma unroll
+  for (int c = 1; c < NCLS; ++c) mx = fmaxf(mx, x[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) se += expf(x[c] - mx);
+  const float lse = logf(se);
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lp[c] = (x[c] - mx) - lse;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= B) {  // padding rows of the bf16 operands consumed by the backward GEMMs
+    a.dz1[(int64_t)b * NH + lane] = 0;
+    a.dz1[(int64_t)b * NH + lane + 64] = 0;
+    a.h_bf[(int64_t)b * NH + lane] = 0;
+    a.h_bf[(int64_t)b * NH + lane + 64] = 0;
+    if (lane < 16) a.dl_bf[(int64_t)b * 16 + lane] = 0;
+    return;
+  }
+  const int step = a.state->step;
+  const uint64_t seed = a.state->seed;
+  const uint64_t off = a.state->rng_base + 2ull * (uint64_t)step + 1ull;
+  const bool no_drop = (a.state->flags & STEP_FLAG_NO_DROPOUT) != 0;
+  HeadRow r;
+  head_forward_row(a, B, b, lane, true, no_drop, seed, off, r);
+  float lp[NCLS];
+  log_softmax10(r.logit, lp);
+  const int y = a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
+  if (lane == 0) a.loss_rows[b] = -lp[y];
+  // nll(mean) backward: go[c] = -[c==y]/B; log_softmax backward: go - exp(lp) * sum(go)
+  float dl[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float go = (c == y) ? -a.inv_batch : 0.0f;
+    dl[c] = go - expf(lp[c]) * (-a.inv_batch);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = lane + 64 * j;
+    float dh = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) dh = __builtin_fmaf(dl[c], a.w_fc2[c * NH + o], dh);
+    const float dz = (r.keep[j] && r.z[j] > 0.0f) ? (no_drop ? dh : dh * (1.0f / KEEP2)) : 0.0f;
+    a.dz1[(int64_t)b * NH + o] = f2bf(dz);
+    a.h_bf[(int64_t)b * NH + o] = f2bf(r.h[j]);
+  }
+  if (lane < 16) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) v = (lane == c) ? dl[c] : v;
+    a.dl_bf[(int64_t)b * 16 + lane] = f2bf(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  HeadRow r;
+  head_forward_row(a, B, b, lane, false, true, 0, 0, r);
+  float lp[NCLS];
+  log_softmax10(r.logit, lp);
+  if (lane == 0) {
+    const int y = a.labels ? a.labels[a.idx ? a.idx[b] : b] : -1;
+    int am = 0;
+#pragma unroll
+    for (int c = 1; c < NCLS; ++c) am = (lp[c] > lp[am]) ? c : am;
+    if (a.loss_rows) a.loss_rows[b] = (y >= 0) ? -lp[y] : 0.0f;
+    if (a.correct_out) a.correct_out[b] = (am == y) ? 1 : 0;
+  }
+  if (a.logp_out && lane < NCLS) {
+    float v = lp[0];
+#pragma unroll
+    for (int c = 1; c < NCLS; ++c) v = (lane == c) ? lp[c] : v;
+    a.logp_out[(int64_t)b * NCLS + lane] = v;
+  }
+}
+
+void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {
+  hipLaunchKernelGGL(head_train_kernel, dim3(Bp / 4), dim3(256), 0, s, a, B);
+}
+void launch_head_eval(const HeadArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(head_eval_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B);
+}
+
+// ============================================================================================
+// fc backward, three workgroup roles in one launch:
+//   A (145 WGs): dW_fc1[o][i] = sum_b dz1[b][o] p[b][i]  (M=128, N=64 per WG, K=B); WG 144 computes
+//                db_fc1 = dz1^T * ones.  Both operands are k(=batch)-major in memory, so each
+//                32-row k-slab is staged in LDS and read with ds_read_b64_tr_b16 (hardware transpose).
+//   B (ceil(B/64)*144 WGs): g[b][i] = (dz1 . w1)[b][i] * dropout1/relu/pool mask  (M=B, N=9216, K=128)
+//   C (1 WG): dW_fc2 = dl^T h, db_fc2 = dl^T 1 (MFMA, 4 waves split K, LDS reduce) + mean loss.
+// ============================================================================================
+namespace {
+constexpr int ROLE_A_WGS = NFLAT / 64 + 1;   // 145
+
+__device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, unsigned char* smem) {
+  uint16_t* dzs = reinterpret_cast<uint16_t*>(smem);           // [32][128]
+  uint16_t* ps = reinterpret_cast<uint16_t*>(smem + 8192);     // [32][64]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const bool ones = (ib == NFLAT / 64);
+  const int i0 = ones ? 0 : ib * 64;
+  const int ntiles = ones ? 1 : 4;
+  floatx4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 onesfrag;
+  {
+    const uint16_t one = ((lane & 15) == 0) ? 0x3F80 : 0;
+    typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+    us8 v = {one, one, one, one, one, one, one, one};
+    onesfrag = __builtin_bit_cast(bf16x8, v);
+  }
+  for (int kb = 0; kb < Bp / 32; ++kb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j, row = c >> 4, c16 = c & 15;
+      *reinterpret_cast<uint4*>(dzs + row * 128 + c16 * 8) =
+          *reinterpret_cast<const uint4*>(a.dz1 + (int64_t)(kb * 32 + row) * NH + c16 * 8);
+    }
+    if (!ones) {
+      const int row = tid >> 3, c8 = tid & 7, b = kb * 32 + row;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (b < B) v = *reinterpret_cast<const uint4*>(a.p + (int64_t)b * NFLAT + i0 + c8 * 8);
+      *reinterpret_cast<uint4*>(ps + row * 64 + c8 * 8) = v;
+    }
+    __syncthreads();
+    const int rlo = 8 * g + q, rhi = rlo + 4;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int ob = 32 * wave + 16 * mt + 4 * pp;
+      const bf16x8 A = tr_frag(dzs + rlo * 128 + ob, dzs + rhi * 128 + ob);
+      if (ones) {
+        acc[mt][0] = mfma16x16x32(A, onesfrag, acc[mt][0]);
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int nb = 16 * nt + 4 * pp;
+          const bf16x8 Bf = tr_frag(ps + rlo * 64 + nb, ps + rhi * 64 + nb);
+          acc[mt][nt] = mfma16x16x32(A, Bf, acc[mt][nt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  (void)ntiles;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 32 * wave + 16 * mt + 4 * g + r;
+      if (ones) {
+        if ((lane & 15) == 0) a.grad[OFF_FC1_B + o] = acc[mt][0][r] * a.grad_scale;
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          a.grad[OFF_FC1_W + (int64_t)o * NFLAT + i0 + 16 * nt + (lane & 15)] = acc[mt][nt][r] * a.grad_scale;
+      }
+    }
+}
+
+__device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m = lane & 15, kg = lane >> 4;
+  const int bm = rb / (NFLAT / 64), ib = rb - bm * (NFLAT / 64);
+  const int i0 = ib * 64;
+  const int row = bm * 64 + 16 * wave + m;
+  const bool rvalid = row < Bp;
+  const float dscale = (a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT)) ? 1.0f : (1.0f / KEEP1);
+  floatx4 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NH / 32; ++ks) {
+    bf16x8 A = ld16(a.dz1 + (int64_t)(rvalid ? row : 0) * NH + ks * 32 + 8 * kg);
+    if (!rvalid) A = zero_frag();
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16x8 Bf = ld16(a.w1t + (int64_t)(i0 + 16 * nt + m) * NH + ks * 32 + 8 * kg);
+      acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = bm * 64 + 16 * wave + 4 * kg + r;
+      const int i = i0 + 16 * nt + m;
+      if (b < B) {
+        const uint8_t mk = a.pmask[(int64_t)b * NFLAT + i];
+        const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;
+        a.g[(int64_t)b * NFLAT + i] = f2bf(v);
+      }
+    }
+}
+
+__device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp, unsigned char* smem) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  uint16_t* hs = reinterpret_cast<uint16_t*>(smem + wave * 9216);          // [32][128]
+  uint16_t* dls = reinterpret_cast<uint16_t*>(smem + wave * 9216 + 8192);  // [32][16]
+  floatx4 acc[9];
+#pragma unroll
+  for (int nt = 0; nt < 9; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 onesfrag;
+  {
+    const uint16_t one = ((lane & 15) == 0) ? 0x3F80 : 0;
+    typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+    us8 v = {one, one, one, one, one, one, one, one};
+    onesfrag = __builtin_bit_cast(bf16x8, v);
+  }
+  const int nkb = Bp / 32;
+  const int iters = (nkb + 3) / 4;
+  for (int it = 0; it < iters; ++it) {
+    const int kb = it * 4 + wave;
+    const bool active = kb < nkb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = lane + 64 * j, row = c >> 4, c16 = c & 15;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (active) v = *reinterpret_cast<const uint4*>(a.h_bf + (int64_t)(kb * 32 + row) * NH + c16 * 8);
+      *reinterpret_cast<uint4*>(hs + row * 128 + c16 * 8) = v;
+    }
+    {
+      const int row = lane >> 1, c8 = lane & 1;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (active) v = *reinterpret_cast<const uint4*>(a.dl_bf + (int64_t)(kb * 32 + row) * 16 + c8 * 8);
+      *reinterpret_cast<uint4*>(dls + row * 16 + c8 * 8) = v;
+    }
+    __syncthreads();
+    const int rlo = 8 * g + q, rhi = rlo + 4;
+    const bf16x8 A = tr_frag(dls + rlo * 16 + 4 * pp, dls + rhi * 16 + 4 * pp);
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      const int nb = 16 * nt + 4 * pp;
+      const bf16x8 Bf = tr_frag(hs + rlo * 128 + nb, hs + rhi * 128 + nb);
+      acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
+    }
+    acc[8] = mfma16x16x32(A, onesfrag, acc[8]);
+    __syncthreads();
+  }
+  // cross-wave reduction through LDS: red[wave][nt][r][lane]
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int nt = 0; nt < 9; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((wave * 9 + nt) * 4 + r) * 64 + lane] = acc[nt][r];
+  __syncthreads();
+  for (int e = tid; e < 9 * 4 * 64; e += 256) {
+    const float s = red[e] + red[e + 2304] + red[e + 2 * 2304] + red[e + 3 * 2304];
+    const int ln = e & 63, r = (e >> 6) & 3, nt = e >> 8;
+    const int c = 4 * (ln >> 4) + r;        // row of the 16x16 output = class
+    const int col = ln & 15;
+    if (c < NCLS) {
+      if (nt < 8) a.grad[OFF_FC2_W + c * NH + 16 * nt + col] = s * a.grad_scale;
+      else if (col == 0) a.grad[OFF_FC2_B + c] = s * a.grad_scale;
+    }
+  }
+  if (wave == 0) {
+    float s = 0.f;
+    for (int b = lane; b < B; b += 64) s += a.loss_rows[b];
+    s = wave_sum(s);
+    if (lane == 0 && a.loss_log) a.loss_log[a.state->step] = s / (float)B;
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 9216];
+  const int bid = blockIdx.x;
+  const int nbm = (B + 63) / 64;
+  const int nb_roles = nbm * (NFLAT / 64);
+  // role C (one long-running WG) first so it is dispatched before the short role-B tiles
+  if (bid == 0) {
+    fc_bwd_role_c(a, B, Bp, smem);
+  } else if (bid <= ROLE_A_WGS) {
+    fc_bwd_role_a(a, B, Bp, bid - 1, smem);
+  } else {
+    fc_bwd_role_b(a, B, Bp, bid - 1 - ROLE_A_WGS);
+  }
+  (void)nb_roles;
+}
+
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
+  const int nbm = (B + 63) / 64;
+  const int grid = ROLE_A_WGS + nbm * (NFLAT / 64) + 1;
+  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp);
+}
+
+}  // namespace mnist

@@ -1,0 +1,226 @@
+#include "engine.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace mnist {
+
+#define HIP_OK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+namespace {
+inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+}  // namespace
+
+Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipStream_t compute,
+               hipStream_t comm, int world_size, float rho, float eps, float weight_decay)
+    : buf_(buf), max_batch_(max_batch), max_test_batch_(max_test_batch), compute_(compute),
+      comm_stream_(comm), world_(world_size), rho_(rho), eps_(eps), wd_(weight_decay) {
+  if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
+  HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_conv_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  alloc_workspace();
+}
+
+Engine::~Engine() {
+  for (auto g : graphs_) hipGraphExecDestroy(g);
+  for (auto g : graph_defs_) hipGraphDestroy(g);
+  if (ev_fc_) hipEventDestroy(ev_fc_);
+  if (ev_conv_) hipEventDestroy(ev_conv_);
+  if (ev_done_) hipEventDestroy(ev_done_);
+  if (ws_) hipFree(ws_);
+}
+
+void Engine::alloc_workspace() {
+  const int M = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
+  const int Mp = round_up(M, 64);
+  const int G = conv_wgrad_groups(max_batch_);
+  int64_t off = 0;
+  auto carve = [&](int64_t bytes) { int64_t o = off; off += align256(bytes); return o; };
+  const int64_t o_a1 = carve((int64_t)M * H1 * H1 * C1 * 2);
+  const int64_t o_p = carve((int64_t)Mp * NFLAT * 2);
+  const int64_t o_pm = carve((int64_t)M * NFLAT);
+  const int64_t o_z1 = carve((int64_t)FC1_KSPLIT * M * NH * 4);
+  const int64_t o_lr = carve((int64_t)M * 4);
+  const int64_t o_dz = carve((int64_t)Mp * NH * 2);
+  const int64_t o_h = carve((int64_t)Mp * NH * 2);
+  const int64_t o_dl = carve((int64_t)Mp * 16 * 2);
+  const int64_t o_g = carve((int64_t)M * NFLAT * 2);
+  const int64_t o_c1 = carve((int64_t)4 * M * 320 * 4);
+  const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
+  ws_bytes_ = off;
+  HIP_OK(hipMalloc(&ws_, ws_bytes_));
+  HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
+  char* base = static_cast<char*>(ws_);
+  a1_ = reinterpret_cast<uint16_t*>(base + o_a1);
+  p_ = reinterpret_cast<uint16_t*>(base + o_p);
+  pmask_ = reinterpret_cast<uint8_t*>(base + o_pm);
+  z1part_ = reinterpret_cast<float*>(base + o_z1);
+  loss_rows_ = reinterpret_cast<float*>(base + o_lr);
+  dz1_ = reinterpret_cast<uint16_t*>(base + o_dz);
+  h_bf_ = reinterpret_cast<uint16_t*>(base + o_h);
+  dl_bf_ = reinterpret_cast<uint16_t*>(base + o_dl);
+  g_ = reinterpret_cast<uint16_t*>(base + o_g);
+  c1part_ = reinterpret_cast<float*>(base + o_c1);
+  w2part_ = reinterpret_cast<float*>(base + o_w2);
+}
+
+void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
+  if (comm && comm->world_size() != world_) throw std::runtime_error("comm world size mismatch");
+  comm_ = std::move(comm);
+}
+
+void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags) {
+  StepState host{step0, flags, seed, rng_base};
+  // tiny H2D of 24 bytes, ordered on the compute stream (never inside a captured graph)
+  HIP_OK(hipMemcpyAsync(buf_.state, &host, sizeof(StepState), hipMemcpyHostToDevice, compute_));
+  HIP_OK(hipStreamSynchronize(compute_));   // `host` lives on this stack frame
+}
+
+void Engine::enqueue_step(int batch) {
+  const int B = batch, Bp = round_up(B, 32);
+  const int stride = idx_stride_;
+  float* P = buf_.param;
+  const float gscale = 1.0f / (float)world_;
+
+  TrunkFwdArgs tf{buf_.train_u8, buf_.train_idx, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
+                  buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_};
+  launch_trunk_fwd(tf, B, true, compute_);
+  launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
+  HeadArgs ha{};
+  ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
+  ha.labels = buf_.train_labels; ha.idx = buf_.train_idx; ha.idx_step_stride = stride;
+  ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
+  ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
+  launch_head_train(ha, B, Bp, compute_);
+  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, g_,
+               buf_.loss_log, gscale, 1.0f / (float)B};
+  launch_fc_bwd(fb, B, Bp, compute_);
+
+  AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
+                  buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+  const bool dist = comm_ && world_ > 1;
+  if (dist && two_buckets_) {
+    // bucket 0 (fc params, 98.4% of the bytes) is complete here: reduce it under the conv backward
+    HIP_OK(hipEventRecord(ev_fc_, compute_));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+  }
+  ConvBwdArgs cb{g_, pmask_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
+                 buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
+                 conv_wgrad_groups(B)};
+  launch_conv_bwd(cb, B, compute_);
+  launch_conv_grad_reduce(cb, B, compute_);
+  if (dist) {
+    HIP_OK(hipEventRecord(ev_conv_, compute_));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_conv_, 0));
+    AdadeltaArgs adc = ad;
+    adc.state_inc = buf_.state;
+    if (two_buckets_) {
+      comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, comm_stream_);
+      launch_adadelta(adc, ADA_CONV, comm_stream_);
+    } else {
+      comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, comm_stream_);
+      launch_adadelta(adc, ADA_ALL, comm_stream_);
+    }
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+  } else {
+    ad.state_inc = buf_.state;
+    launch_adadelta(ad, ADA_ALL, compute_);
+  }
+}
+
+void Engine::train_steps(int n, int batch, int stride) {
+  if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
+  idx_stride_ = stride;
+  for (int i = 0; i < n; ++i) enqueue_step(batch);
+  HIP_OK(hipGetLastError());
+}
+
+int Engine::capture_train(int n, int batch, int stride) {
+  if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
+  idx_stride_ = stride;
+  hipGraph_t g = nullptr;
+  HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
+  try {
+    for (int i = 0; i < n; ++i) enqueue_step(batch);
+  } catch (...) {
+    hipStreamEndCapture(compute_, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  HIP_OK(hipStreamEndCapture(compute_, &g));
+  hipGraphExec_t ex = nullptr;
+  HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  graph_defs_.push_back(g);
+  graphs_.push_back(ex);
+  return (int)graphs_.size() - 1;
+}
+
+void Engine::replay(int id) {
+  if (id < 0 || id >= (int)graphs_.size()) throw std::runtime_error("bad graph id");
+  HIP_OK(hipGraphLaunch(graphs_[id], compute_));
+}
+
+void Engine::enqueue_eval(int n_total, int batch) {
+  const float* P = buf_.param;
+  for (int s = 0; s < n_total; s += batch) {
+    const int B = (n_total - s) < batch ? (n_total - s) : batch;
+    TrunkFwdArgs tf{buf_.test_u8, buf_.test_idx + s, 0, nullptr, P + OFF_CONV1_W, P + OFF_CONV1_B,
+                    buf_.w2f, P + OFF_CONV2_B, nullptr, p_, nullptr};
+    launch_trunk_fwd(tf, B, false, compute_);
+    launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
+    HeadArgs ha{};
+    ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
+    ha.labels = buf_.test_labels; ha.idx = buf_.test_idx + s; ha.idx_step_stride = 0;
+    ha.loss_rows = buf_.test_loss_rows + s; ha.correct_out = buf_.test_correct + s;
+    launch_head_eval(ha, B, compute_);
+  }
+}
+
+void Engine::eval(int n_total, int batch) {
+  if (batch < 1 || batch > max_test_batch_) throw std::runtime_error("test batch exceeds engine capacity");
+  enqueue_eval(n_total, batch);
+  HIP_OK(hipGetLastError());
+}
+
+int Engine::capture_eval(int n_total, int batch) {
+  if (batch < 1 || batch > max_test_batch_) throw std::runtime_error("test batch exceeds engine capacity");
+  hipGraph_t g = nullptr;
+  HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
+  enqueue_eval(n_total, batch);
+  HIP_OK(hipStreamEndCapture(compute_, &g));
+  hipGraphExec_t ex = nullptr;
+  HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  graph_defs_.push_back(g);
+  graphs_.push_back(ex);
+  return (int)graphs_.size() - 1;
+}
+
+void Engine::refresh_shadows() {
+  AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
+                  buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+  launch_refresh_shadows(ad, compute_);
+  HIP_OK(hipGetLastError());
+}
+
+void Engine::broadcast_params(int root) {
+  if (!comm_) throw std::runtime_error("no communicator attached");
+  comm_->broadcast(buf_.param, PARAM_TOTAL, 0, root, compute_);
+  refresh_shadows();
+}
+
+void Engine::synchronize() {
+  HIP_OK(hipStreamSynchronize(compute_));
+  if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
+}
+
+}  // namespace mnist

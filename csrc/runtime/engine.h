@@ -1,0 +1,102 @@
+// Native training/eval step engine for the MNIST CNN on one MI355X.
+//
+// This is the hot loop of reference mnist_ddp.py:65-86 (train) and :89-105 (test) re-designed
+// for the GPU: the dataset is HBM resident, every step is a fixed sequence of 8 hand-written
+// kernels (no host work, no sync), DDP gradient averaging is an RCCL all-reduce per gradient
+// bucket on a second stream overlapped with the remaining backward kernels, and whole chunks of
+// steps are captured once into a hipGraph and replayed (launch overhead amortised to ~0).
+//
+// Per training step (compute stream C, comm stream M):
+//   C: trunk_fwd -> fc1_fwd -> head_train -> fc_bwd --ev_fc--> conv2_dgrad -> conv2_wgrad -> reduce --ev_conv-->
+//   M:                                         wait ev_fc: allreduce(fc bucket) -> adadelta(fc)
+//                                              wait ev_conv: allreduce(conv bucket) -> adadelta(conv, step++) --ev_done--> C
+// With world_size == 1 the comm stream is unused and a single adadelta(all) closes the step.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <map>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "../include/kernels.h"
+#include "rccl_comm.h"
+
+namespace mnist {
+
+struct EngineBuffers {
+  // model / optimizer state (allocated by the Python side so parameters are torch tensors)
+  float* param = nullptr;       // flat fp32 [PARAM_TOTAL]
+  float* grad = nullptr;        // flat fp32 [PARAM_TOTAL] (= DDP bucket storage)
+  float* square_avg = nullptr;
+  float* acc_delta = nullptr;
+  float* lr = nullptr;          // device scalar
+  uint16_t* w2f = nullptr;
+  uint16_t* w2d = nullptr;
+  uint16_t* w1 = nullptr;
+  uint16_t* w1t = nullptr;
+  StepState* state = nullptr;
+  float* loss_log = nullptr;    // [max steps per epoch]
+  // datasets (HBM resident)
+  const uint8_t* train_u8 = nullptr;
+  const int32_t* train_labels = nullptr;
+  const int32_t* train_idx = nullptr;   // [steps * B] this rank's epoch order
+  const uint8_t* test_u8 = nullptr;
+  const int32_t* test_labels = nullptr;
+  const int32_t* test_idx = nullptr;    // [N_test]
+  float* test_loss_rows = nullptr;      // [N_test]
+  int32_t* test_correct = nullptr;      // [N_test]
+};
+
+class Engine {
+ public:
+  Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipStream_t compute,
+         hipStream_t comm, int world_size, float rho, float eps, float weight_decay);
+  ~Engine();
+
+  void attach_comm(std::shared_ptr<RcclComm> comm);   // enables the overlapped DDP path
+  void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
+
+  // --- training
+  void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
+  // enqueue n steps eagerly; `stride` = full batch size (row offset of step s is s*stride)
+  void train_steps(int n, int batch, int stride);
+  int capture_train(int n, int batch, int stride);   // capture n steps into a graph, returns id
+  void replay(int graph_id);
+  // --- eval (SequentialSampler over the test set, `n_batches` of `batch`, last may be short)
+  void eval(int n_total, int batch);
+  int capture_eval(int n_total, int batch);
+  // --- misc
+  void refresh_shadows();
+  void broadcast_params(int root);                   // DDP construction: rank-0 params to all
+  void synchronize();
+  int64_t workspace_bytes() const { return ws_bytes_; }
+
+  // single-op entry points used by the numerics tests / module API
+  const EngineBuffers& buffers() const { return buf_; }
+
+ private:
+  void enqueue_step(int batch);
+  void enqueue_eval(int n_total, int batch);
+  void alloc_workspace();
+
+  EngineBuffers buf_;
+  int max_batch_, max_test_batch_;
+  hipStream_t compute_, comm_stream_;
+  int world_;
+  float rho_, eps_, wd_;
+  bool two_buckets_ = true;
+  int idx_stride_ = 0;
+  std::shared_ptr<RcclComm> comm_;
+  hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr;
+  // workspace
+  int64_t ws_bytes_ = 0;
+  void* ws_ = nullptr;
+  uint16_t *a1_, *p_, *dz1_, *h_bf_, *dl_bf_, *g_;
+  uint8_t* pmask_;
+  float *z1part_, *loss_rows_, *c1part_, *w2part_;
+  std::vector<hipGraphExec_t> graphs_;
+  std::vector<hipGraph_t> graph_defs_;
+};
+
+}  // namespace mnist

@@ -1,0 +1,114 @@
+#include "rccl_comm.h"
+
+#include <dlfcn.h>
+#include <stdexcept>
+#include <string.h>
+
+namespace mnist {
+
+namespace {
+// Minimal RCCL ABI (stable since NCCL 2.x): opaque comm, 128-byte unique id.
+typedef void* ncclComm_t;
+struct ncclUniqueId { char internal[RcclComm::kUniqueIdBytes]; };
+typedef int ncclResult_t;
+enum { ncclFloat32 = 7, ncclBfloat16 = 9 };   // ncclDataType_t values (rccl.h)
+enum { ncclSum = 0 };
+
+struct Api {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Broadcast)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GetVersion)(int*) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+
+void* find_sym(const char* name) {
+  void* p = dlsym(RTLD_DEFAULT, name);
+  if (!p) {
+    static void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+    if (h) p = dlsym(h, name);
+  }
+  return p;
+}
+
+Api& api() {
+  static Api a = [] {
+    Api x;
+    x.GetUniqueId = (decltype(x.GetUniqueId))find_sym("ncclGetUniqueId");
+    x.CommInitRank = (decltype(x.CommInitRank))find_sym("ncclCommInitRank");
+    x.CommDestroy = (decltype(x.CommDestroy))find_sym("ncclCommDestroy");
+    x.AllReduce = (decltype(x.AllReduce))find_sym("ncclAllReduce");
+    x.Broadcast = (decltype(x.Broadcast))find_sym("ncclBroadcast");
+    x.GetVersion = (decltype(x.GetVersion))find_sym("ncclGetVersion");
+    x.GetErrorString = (decltype(x.GetErrorString))find_sym("ncclGetErrorString");
+    x.ok = x.GetUniqueId && x.CommInitRank && x.CommDestroy && x.AllReduce && x.Broadcast;
+    return x;
+  }();
+  return a;
+}
+
+void check(ncclResult_t r, const char* what) {
+  if (r != 0) {
+    const char* s = api().GetErrorString ? api().GetErrorString(r) : "?";
+    throw std::runtime_error(std::string("RCCL ") + what + " failed: " + s);
+  }
+}
+int dt(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
+
+typedef int (*roctx_push_t)(const char*);
+typedef int (*roctx_pop_t)();
+}  // namespace
+
+bool RcclComm::available() { return api().ok; }
+
+std::string RcclComm::version() {
+  int v = 0;
+  if (api().GetVersion) api().GetVersion(&v);
+  return std::to_string(v);
+}
+
+std::vector<uint8_t> RcclComm::unique_id() {
+  if (!available()) throw std::runtime_error("RCCL symbols not found (import torch first)");
+  ncclUniqueId id;
+  check(api().GetUniqueId(&id), "ncclGetUniqueId");
+  return std::vector<uint8_t>(id.internal, id.internal + kUniqueIdBytes);
+}
+
+RcclComm::RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device)
+    : world_(world_size), rank_(rank) {
+  if (!available()) throw std::runtime_error("RCCL symbols not found (import torch first)");
+  if (uid.size() != kUniqueIdBytes) throw std::runtime_error("bad ncclUniqueId size");
+  if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+  ncclUniqueId id;
+  memcpy(id.internal, uid.data(), kUniqueIdBytes);
+  ncclComm_t c = nullptr;
+  check(api().CommInitRank(&c, world_size, id, rank), "ncclCommInitRank");
+  comm_ = c;
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) api().CommDestroy((ncclComm_t)comm_);
+}
+
+void RcclComm::allreduce_sum(void* buf, int64_t count, int dtype, hipStream_t stream) {
+  check(api().AllReduce(buf, buf, (size_t)count, dt(dtype), ncclSum, (ncclComm_t)comm_, stream), "ncclAllReduce");
+}
+
+void RcclComm::broadcast(void* buf, int64_t count, int dtype, int root, hipStream_t stream) {
+  check(api().Broadcast(buf, buf, (size_t)count, dt(dtype), root, (ncclComm_t)comm_, stream), "ncclBroadcast");
+}
+
+void roctx_push(const char* name) {
+  static roctx_push_t f = (roctx_push_t)dlsym(RTLD_DEFAULT, "roctxRangePushA");
+  if (f) f(name);
+}
+void roctx_pop() {
+  static roctx_pop_t f = (roctx_pop_t)dlsym(RTLD_DEFAULT, "roctxRangePop");
+  if (f) f();
+}
+
+}  // namespace mnist

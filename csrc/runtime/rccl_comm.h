@@ -1,0 +1,43 @@
+// RCCL communicator owned by the framework (one per process / GPU), used for the DDP gradient
+// all-reduce and the initial parameter broadcast on a dedicated HIP stream.
+//
+// Replaces the reference's implicit ProcessGroupNCCL (mnist_ddp.py:33-37, :173).  Symbols are
+// resolved at run time from the RCCL that PyTorch already loaded (torch/lib/librccl.so), so the
+// process holds exactly one RCCL and one HIP runtime; the ncclUniqueId is exchanged by the caller
+// through the torch.distributed TCPStore (env:// rendezvous).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+namespace mnist {
+
+class RcclComm {
+ public:
+  static constexpr int kUniqueIdBytes = 128;
+  static bool available();
+  static std::string version();
+  static std::vector<uint8_t> unique_id();
+
+  RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  // in-place sum all-reduce of fp32 (dtype 0) or bf16 (dtype 1) elements on `stream`
+  void allreduce_sum(void* buf, int64_t count, int dtype, hipStream_t stream);
+  void broadcast(void* buf, int64_t count, int dtype, int root, hipStream_t stream);
+  int world_size() const { return world_; }
+  int rank() const { return rank_; }
+
+ private:
+  void* comm_ = nullptr;
+  int world_, rank_;
+};
+
+// roctx ranges (no-ops when roctx is not loaded)
+void roctx_push(const char* name);
+void roctx_pop();
+
+}  // namespace mnist

@@ -1,0 +1,80 @@
+"""Command-line flags for ``mnist.py`` / ``mnist_ddp.py``.
+
+Reference flags and defaults are reproduced verbatim (``mnist.py:75-96``,
+``mnist_ddp.py:110-135``).  Deliberate additions (all default to reference
+behaviour):
+
+* ``--local-rank`` accepted as an alias of ``--local_rank``: torch>=2.0's
+  ``torch.distributed.launch`` appends ``--local-rank=<i>`` which the reference's
+  underscore-only flag rejects.
+* ``--synthetic`` / ``--data-root`` / ``--synthetic-train-size`` /
+  ``--synthetic-test-size``: offline data selection.
+* ``--bucket-cap-mb`` / ``--first-bucket-mb``: DDP gradient bucket sizing.
+* ``--graph-steps``: training steps captured per HIP graph (0 = eager launches).
+* ``--profile``: roctx ranges + per-epoch device timing; ``--json-log``: machine
+  readable per-epoch metrics.
+* ``--resume``: optional checkpoint to load before training (off by default).
+"""
+from __future__ import annotations
+
+import argparse
+
+
+def _reference_flags(parser: argparse.ArgumentParser) -> None:
+    parser.add_argument('--batch-size', type=int, default=64, metavar='N',
+                        help='input batch size for training (default: 64)')
+    parser.add_argument('--test-batch-size', type=int, default=1000, metavar='N',
+                        help='input batch size for testing (default: 1000)')
+    parser.add_argument('--epochs', type=int, default=14, metavar='N',
+                        help='number of epochs to train (default: 14)')
+    parser.add_argument('--lr', type=float, default=1.0, metavar='LR',
+                        help='learning rate (default: 1.0)')
+    parser.add_argument('--gamma', type=float, default=0.7, metavar='M',
+                        help='Learning rate step gamma (default: 0.7)')
+    parser.add_argument('--no-cuda', action='store_true', default=False,
+                        help='disables GPU training')
+    parser.add_argument('--dry-run', action='store_true', default=False,
+                        help='quickly check a single pass')
+    parser.add_argument('--seed', type=int, default=1, metavar='S',
+                        help='random seed (default: 1)')
+    parser.add_argument('--log-interval', type=int, default=10, metavar='N',
+                        help='how many batches to wait before logging training status')
+    parser.add_argument('--save-model', action='store_true', default=False,
+                        help='For Saving the current Model')
+
+
+def _framework_flags(parser: argparse.ArgumentParser) -> None:
+    g = parser.add_argument_group("mi355x framework options")
+    g.add_argument('--data-root', default='./data', help='MNIST root (torchvision layout)')
+    g.add_argument('--synthetic', action='store_true', default=None,
+                   help='use deterministic synthetic 28x28 data (auto when MNIST files are absent)')
+    g.add_argument('--synthetic-train-size', type=int, default=None)
+    g.add_argument('--synthetic-test-size', type=int, default=None)
+    g.add_argument('--graph-steps', type=int, default=None,
+                   help='training steps per captured HIP graph (default: log-interval; 0 = eager)')
+    g.add_argument('--bucket-cap-mb', type=float, default=25.0,
+                   help='DDP gradient bucket cap in MiB (default 25, as torch DDP)')
+    g.add_argument('--first-bucket-mb', type=float, default=1.0,
+                   help='DDP first-bucket cap in MiB (default 1, as torch DDP)')
+    g.add_argument('--profile', action='store_true', default=False,
+                   help='emit roctx ranges and per-epoch device timings')
+    g.add_argument('--json-log', default=None, help='append per-epoch JSON metrics to this file')
+    g.add_argument('--resume', default=None, help='load a state_dict checkpoint before training')
+
+
+def build_parser(ddp: bool) -> argparse.ArgumentParser:
+    parser = argparse.ArgumentParser(description='PyTorch MNIST Example')
+    _reference_flags(parser)
+    if ddp:
+        parser.add_argument('--local_rank', '--local-rank', dest='local_rank', type=int,
+                            help='local rank, will passed by ddp')
+        parser.add_argument("--world-size", default=1, type=int,
+                            help="number of distributed processes")
+        parser.add_argument("--dist-url", default="env://", type=str,
+                            help="url used to set up distributed training")
+    _framework_flags(parser)
+    return parser
+
+
+def parse_args(ddp: bool, argv=None) -> argparse.Namespace:
+    return build_parser(ddp).parse_args(argv)

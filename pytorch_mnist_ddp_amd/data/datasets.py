@@ -1,0 +1,75 @@
+"""MNIST dataset container (raw uint8 + labels) with torchvision-equivalent transforms.
+
+Replaces ``datasets.MNIST(root, train, download, transform=Compose([ToTensor(),
+Normalize((0.1307,), (0.3081,))]))`` from reference ``mnist_ddp.py:153-160``.
+Images are kept as raw uint8 (47 MB for the train split) so the GPU path can
+keep the whole split resident in HBM and gather+normalise inside the first
+kernel; the CPU path applies exactly torchvision's float ops
+(``u8.float().div(255)`` then ``sub_(mean).div_(std)``) for bit parity.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass
+
+import torch
+
+from . import idx, synthetic
+
+MNIST_MEAN = 0.1307
+MNIST_STD = 0.3081
+
+
+@dataclass
+class MNISTData:
+    images: torch.Tensor   # uint8 [N, 28, 28]
+    targets: torch.Tensor  # int64 [N]
+    train: bool
+    source: str            # "idx:<root>" or "synthetic"
+
+    def __len__(self) -> int:
+        return int(self.targets.shape[0])
+
+    def __getitem__(self, i):
+        """(normalised float32 [1,28,28], int label) like torchvision + transform."""
+        return normalize_u8(self.images[i:i + 1]), int(self.targets[i])
+
+
+def normalize_u8(u8: torch.Tensor) -> torch.Tensor:
+    """torchvision ToTensor()+Normalize((0.1307,),(0.3081,)) on a uint8 [..,28,28] batch.
+
+    Returns float32 [..., 1, 28, 28] (channel dim inserted before H, W).
+    """
+    x = u8.to(torch.float32).div(255)
+    x = x.sub_(MNIST_MEAN).div_(MNIST_STD)
+    return x.unsqueeze(-3)
+
+
+_warned = set()
+
+
+def load_mnist(root: str = "./data", train: bool = True, synthetic_data: bool | None = None,
+               synthetic_size: int | None = None, verbose: bool = True) -> MNISTData:
+    """Load the MNIST split from IDX files under ``root`` or build synthetic data.
+
+    ``synthetic_data``: True -> always synthetic; False -> IDX files required;
+    None -> IDX if present, else synthetic (with one warning per split; the
+    reference would try to download, which is impossible offline).
+    """
+    if synthetic_data is not True:
+        loaded = idx.load_mnist_idx(root, train)
+        if loaded is not None:
+            images, labels = loaded
+            return MNISTData(torch.from_numpy(images), torch.from_numpy(labels), train,
+                             f"idx:{os.path.abspath(root)}")
+        if synthetic_data is False:
+            raise FileNotFoundError(
+                f"MNIST IDX files not found under {root}/MNIST/raw and there is no network to "
+                f"download them; pass --synthetic to use synthetic 28x28 data")
+        if verbose and train not in _warned:
+            _warned.add(train)
+            print(f"[mnist-amd] MNIST {'train' if train else 'test'} IDX files not found under "
+                  f"{root}; using deterministic synthetic 28x28 data", file=sys.stderr)
+    images, labels = synthetic.synthetic_mnist(train, synthetic_size)
+    return MNISTData(images, labels, train, "synthetic")

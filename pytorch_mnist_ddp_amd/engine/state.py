@@ -1,0 +1,90 @@
+"""Device-resident model + optimizer state in the flat layouts the native kernels use.
+
+* ``param`` / ``grad``: one fp32 buffer each (``PARAM_TOTAL`` = 1,200,000 elements; every tensor
+  256-byte aligned).  The module's ``nn.Parameter``s are re-pointed at views of ``param`` and
+  their ``.grad`` at views of ``grad`` - the gradient buffer *is* the DDP bucket storage
+  (torch DDP's ``gradient_as_bucket_view=True`` taken to its conclusion: no copy-in/copy-out).
+  Bucket 0 = fc params (98.4 % of bytes, ready first in backward), bucket 1 = conv params:
+  the same rebuilt bucket layout torch DDP converges to for this model.
+* ``square_avg`` / ``acc_delta``: Adadelta state, same flat layout.
+* bf16 shadows ``w2f``, ``w2d``, ``w1``, ``w1t``: refreshed by the optimizer kernel.
+* ``state``: the 24-byte device ``StepState`` (step counter, flags, Philox seed / base).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import native
+
+FLAG_NO_DROPOUT = 1
+
+
+class ModelState:
+    def __init__(self, module: nn.Module, device: torch.device, lr: float = 1.0, rho: float = 0.9,
+                 eps: float = 1e-6, weight_decay: float = 0.0):
+        C = native.load()
+        self.C = C
+        self.device = torch.device(device)
+        self.offsets = dict(C.PARAM_OFFSETS)
+        total = int(C.PARAM_TOTAL)
+        self.bucket_split = int(C.BUCKET_SPLIT)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.param = torch.zeros(total, **f32)
+        self.grad = torch.zeros(total, **f32)
+        self.square_avg = torch.zeros(total, **f32)
+        self.acc_delta = torch.zeros(total, **f32)
+        self.lr = torch.full((1,), float(lr), **f32)
+        self.rho, self.eps, self.weight_decay = rho, eps, weight_decay
+        bf = dict(dtype=torch.bfloat16, device=self.device)
+        self.w2f = torch.zeros(64 * 9 * 32, **bf)
+        self.w2d = torch.zeros(9 * 32 * 64, **bf)
+        self.w1 = torch.zeros(128 * 9216, **bf)
+        self.w1t = torch.zeros(9216 * 128, **bf)
+        self.state = torch.zeros(3, dtype=torch.int64, device=self.device)  # StepState (24 B)
+        self.module = module
+        self.bind(module)
+
+    # ------------------------------------------------------------------ parameter binding
+    def views(self, buf: torch.Tensor) -> dict[str, torch.Tensor]:
+        out = {}
+        for name, p in self.module.named_parameters():
+            off = self.offsets[name]
+            out[name] = buf[off:off + p.numel()].view(p.shape)
+        return out
+
+    def bind(self, module: nn.Module) -> None:
+        """Copy the module's parameters into the flat buffer and alias them to it."""
+        with torch.no_grad():
+            for name, p in module.named_parameters():
+                if name not in self.offsets:
+                    raise KeyError(f"unexpected parameter {name}")
+                off = self.offsets[name]
+                view = self.param[off:off + p.numel()].view(p.shape)
+                view.copy_(p.detach().to(self.device, torch.float32))
+                p.data = view
+                p.grad = self.grad[off:off + p.numel()].view(p.shape)
+        self.refresh_shadows()
+
+    def refresh_shadows(self, stream: torch.cuda.Stream | None = None) -> None:
+        C = self.C
+        p = native.ptr
+        C.adadelta(p(self.param), p(self.grad), p(self.square_avg), p(self.acc_delta), p(self.lr),
+                   self.rho, self.eps, self.weight_decay, p(self.w2f), p(self.w2d), p(self.w1), p(self.w1t),
+                   0, 0, False, native.stream_handle(stream))
+
+    def buffers(self) -> dict[str, int]:
+        p = native.ptr
+        return {"param": p(self.param), "grad": p(self.grad), "square_avg": p(self.square_avg),
+                "acc_delta": p(self.acc_delta), "lr": p(self.lr), "w2f": p(self.w2f), "w2d": p(self.w2d),
+                "w1": p(self.w1), "w1t": p(self.w1t), "state": p(self.state)}
+
+    def set_state(self, step: int, seed: int, rng_base: int, flags: int = 0) -> None:
+        """Write the device StepState (step | flags<<32, seed, rng_base)."""
+        packed = (int(step) & 0xFFFFFFFF) | ((int(flags) & 0xFFFFFFFF) << 32)
+        vals = [packed, int(seed), int(rng_base)]
+        vals = [v - (1 << 64) if v >= (1 << 63) else v for v in vals]
+        self.state.copy_(torch.tensor(vals, dtype=torch.int64))
+
+    def get_step(self) -> int:
+        return int(self.state[0].item()) & 0xFFFFFFFF

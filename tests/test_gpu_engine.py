@@ -1,0 +1,60 @@
+"""Engine-level GPU tests: captured graphs vs eager, convergence on synthetic data."""
+import copy
+
+import pytest
+import torch
+
+from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+from pytorch_mnist_ddp_amd.data.samplers import RandomIndexStream
+from pytorch_mnist_ddp_amd.engine.state import ModelState
+from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+from pytorch_mnist_ddp_amd.models.net import Net
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(dev, graph_steps, n_train=2000, n_test=1000, B=200, seed=1):
+    torch.manual_seed(seed)
+    net = Net()
+    tr = load_mnist(synthetic_data=True, train=True, synthetic_size=n_train, verbose=False)
+    te = load_mnist(synthetic_data=True, train=False, synthetic_size=n_test, verbose=False)
+    ms = ModelState(net, dev, lr=1.0)
+    t = FusedTrainer(ms, tr, te, B, 1000, num_samples=n_train, seed=seed, graph_steps=graph_steps)
+    return net, ms, t
+
+
+def test_graph_replay_bitwise_equals_eager(cuda_device):
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(3))
+    _, ms_g, tg = _trainer(cuda_device, graph_steps=4)
+    _, ms_e, te = _trainer(cuda_device, graph_steps=0)
+    tg.train_epoch(1, idx)
+    te.train_epoch(1, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(ms_g.param, ms_e.param)
+    assert torch.equal(tg.loss_log, te.loss_log)
+    assert ms_g.get_step() == 10
+
+
+def test_training_converges_on_synthetic(cuda_device):
+    net, ms, t = _trainer(cuda_device, graph_steps=10, n_train=6000)
+    stream = RandomIndexStream(6000)
+    l0, c0, n = t.evaluate()
+    for ep in range(1, 4):
+        st = t.train_epoch(ep, stream.epoch_indices())
+        assert st.steps == 30
+    l1, c1, _ = t.evaluate()
+    assert l1 / n < 0.5 * (l0 / n)
+    assert c1 / n > 0.9, c1 / n
+    assert torch.isfinite(ms.param).all()
+
+
+def test_partial_last_batch_and_dry_run(cuda_device):
+    _, ms, t = _trainer(cuda_device, graph_steps=10, n_train=2000, B=64)   # 31 full + 1 of 16
+    idx = torch.randperm(2000)
+    logs = []
+    st = t.train_epoch(1, idx, log_interval=10, log_fn=lambda b, n, l: logs.append((b, n, l)))
+    assert st.steps == 32
+    assert [b for b, _, _ in logs] == [0, 10, 20, 30]
+    st = t.train_epoch(2, idx, dry_run=True, log_fn=lambda b, n, l: logs.append((b, n, l)))
+    assert st.steps == 1
+    assert torch.isfinite(ms.param).all()
