@@ -164,6 +164,31 @@ class FusedTrainer:
         self.compute.synchronize()
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
 
+    # ------------------------------------------------------------------ raw step stream (bench)
+    def start_stream(self, idx: torch.Tensor) -> None:
+        """Upload a flat index stream (steps * B rows) and reset the device step counter."""
+        self.upload_indices(idx)
+        self.engine.begin_epoch(self.seed, self.rng_base, 0, self.flags)
+        self.rng_base += 2 * (idx.numel() // self.B)
+
+    def _chunks(self, n: int) -> list[int]:
+        c = self.graph_steps if self.graph_steps > 0 else max(1, n)
+        out = [c] * (n // c)
+        if n % c:
+            out.append(n % c)
+        return out
+
+    def precapture(self, n: int) -> None:
+        """Capture every graph ``run_steps(n)`` will replay (capture executes nothing)."""
+        if self.use_graphs:
+            for k in set(self._chunks(n)):
+                self._graph(k, self.B)
+
+    def run_steps(self, n: int) -> None:
+        """Enqueue ``n`` full-batch steps continuing from the device step counter (no host sync)."""
+        for k in self._chunks(n):
+            self._run(k, self.B)
+
     # ------------------------------------------------------------------ evaluation
     def evaluate(self) -> tuple[float, int, int]:
         """Return (sum of per-sample NLL, correct, N) over the whole test split."""
