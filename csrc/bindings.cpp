@@ -107,19 +107,19 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   m.def("fc_bwd", [](uintptr_t dz1, uintptr_t p, uintptr_t pmask, uintptr_t w1t, uintptr_t h_bf, uintptr_t dl_bf,
-                     uintptr_t loss_rows, uintptr_t state, uintptr_t grad, uintptr_t g, uintptr_t loss_log,
+                     uintptr_t loss_rows, uintptr_t state, uintptr_t grad, uintptr_t dy, uintptr_t loss_log,
                      float grad_scale, float inv_batch, int B, int Bp, uintptr_t stream) {
     FcBwdArgs a{P<const uint16_t>(dz1), P<const uint16_t>(p), P<const uint8_t>(pmask), P<const uint16_t>(w1t),
                 P<const uint16_t>(h_bf), P<const uint16_t>(dl_bf), P<const float>(loss_rows),
-                P<const StepState>(state), P<float>(grad), P<uint16_t>(g), P<float>(loss_log), grad_scale,
+                P<const StepState>(state), P<float>(grad), P<uint16_t>(dy), P<float>(loss_log), grad_scale,
                 inv_batch};
     launch_fc_bwd(a, B, Bp, S(stream));
     check_launch();
   });
-  m.def("conv_bwd", [](uintptr_t g, uintptr_t pmask, uintptr_t a1, uintptr_t w2d, uintptr_t w1c, uintptr_t b1c,
+  m.def("conv_bwd", [](uintptr_t dy, uintptr_t a1, uintptr_t w2d, uintptr_t w1c, uintptr_t b1c,
                        uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t c1part,
                        uintptr_t w2part, uintptr_t grad, float grad_scale, int B, uintptr_t stream) {
-    ConvBwdArgs a{P<const uint16_t>(g), P<const uint8_t>(pmask), P<const uint16_t>(a1), P<const uint16_t>(w2d),
+    ConvBwdArgs a{P<const uint16_t>(dy), P<const uint16_t>(a1), P<const uint16_t>(w2d),
                   P<const float>(w1c), P<const float>(b1c), P<const uint8_t>(data_u8), P<const int32_t>(idx),
                   idx_stride, P<const StepState>(state), P<float>(c1part), P<float>(w2part), P<float>(grad),
                   grad_scale, conv_wgrad_groups(B)};
@@ -171,6 +171,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
       .def("attach_comm", &Engine::attach_comm)
       .def("set_bucket_split", &Engine::set_bucket_split)
+      .def("set_concurrent", &Engine::set_concurrent)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

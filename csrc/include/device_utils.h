@@ -86,8 +86,16 @@ __device__ __forceinline__ float conv1_preact(const float* x, int stride, const 
   return acc;
 }
 
-__device__ __forceinline__ float normalize_u8(uint8_t v) {
-  return ((float)v / 255.0f - MNIST_MEAN) / MNIST_STD;
-}
+// torchvision ToTensor()+Normalize((0.1307,),(0.3081,)) of one uint8 pixel: (v/255 - mean)/std in fp32.
+// The 256 possible results are folded at compile time (IEEE round-to-nearest, identical to the
+// runtime fp32 divisions) into a constant table: no divisions in any kernel.
+struct NormLut {
+  float v[256];
+  constexpr NormLut() : v() {
+    for (int i = 0; i < 256; ++i) v[i] = ((float)i / 255.0f - MNIST_MEAN) / MNIST_STD;
+  }
+};
+__constant__ constexpr NormLut kNormLut{};
+__device__ __forceinline__ float normalize_u8(uint8_t v) { return kNormLut.v[v]; }
 
 }  // namespace mnist

@@ -24,7 +24,7 @@ struct TrunkFwdArgs {
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
 
 // fc1 split-K partial GEMM: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
-constexpr int FC1_KSPLIT = 16;
+constexpr int FC1_KSPLIT = 32;
 void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s);
 
 // Head: reduce fc1 partials + bias -> ReLU -> dropout(0.5) -> fc2 -> log_softmax (+ NLL + backward)
@@ -61,7 +61,7 @@ struct FcBwdArgs {
   const float* loss_rows;     // [B]
   const StepState* state;
   float* grad;                // flat fp32 grad buffer (writes fc1.w, fc1.b, fc2.w, fc2.b)
-  uint16_t* g;                // bf16 [B][9216] grad wrt conv2 pooled output (pre-dropout, masked)
+  uint16_t* dy;               // bf16 [B][24][24][64] NHWC grad wrt conv2 output (dense, un-pooled)
   float* loss_log;            // [steps] mean loss per step (indexed by state->step)
   float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
   float inv_batch;
@@ -69,8 +69,7 @@ struct FcBwdArgs {
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 
 struct ConvBwdArgs {
-  const uint16_t* g;          // bf16 [B][9216]
-  const uint8_t* pmask;       // [B][9216]
+  const uint16_t* dy;         // bf16 [B][24][24][64] NHWC (written by fc_bwd)
   const uint16_t* a1;         // bf16 [B][26][26][32]
   const uint16_t* w2d;        // bf16 [9][32][64]
   const float* w1c;           // conv1 fp32 [32][9]
@@ -87,6 +86,8 @@ struct ConvBwdArgs {
 };
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad
+void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials
+void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 wgrad + bias partials
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s);
 
 // ---------------- optimizer ----------------

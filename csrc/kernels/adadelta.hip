@@ -9,7 +9,7 @@
 //     p  += -lr * d
 // One read of g, read-modify-write of sq/acc/p, and in the same pass the bf16 copies the next
 // forward/backward consume are written in the layouts their MFMA fragments want:
-//   fc1.weight -> w1 [128][9216] and w1t [9216][128] (64x64 tiles transposed through LDS),
+//   fc1.weight -> w1 [128][9216] and w1t [9216][128] (64x32 tiles transposed through LDS),
 //   conv2.weight -> w2f [64][9][32] and w2d [9][32][64].
 // lr is read from device memory so a captured graph picks up StepLR changes.
 #include "../include/device_utils.h"
@@ -18,7 +18,7 @@
 namespace mnist {
 
 namespace {
-constexpr int FC1_TILES = 2 * (NFLAT / 64);                       // 288 64x64 tiles of fc1.weight
+constexpr int FC1_TILES = 2 * (NFLAT / 32);                       // 576 64(o) x 32(i) tiles of fc1.weight
 constexpr int64_t FC_TAIL_N = OFF_CONV1_W - OFF_FC1_B;            // 1472 (fc1.b, fc2.w, fc2.b + pad)
 constexpr int64_t CONV_N = PARAM_TOTAL - OFF_CONV1_W;             // 18880
 constexpr int CONV_WGS = (int)((CONV_N / 4 + 255) / 256);         // 19
@@ -78,50 +78,51 @@ __device__ __forceinline__ void elementwise(const AdadeltaArgs& a, const Ada& ad
 
 template <bool UPDATE>
 __device__ __forceinline__ void fc1_tile(const AdadeltaArgs& a, const Ada& ad, int tile, uint16_t* ts) {
-  constexpr int TS = 72;  // padded LDS row (bf16 elements)
-  const int ot = tile / (NFLAT / 64), it = tile - ot * (NFLAT / 64);
+  constexpr int TS = 72;  // padded LDS row (bf16 elements): ts[32 i][64 o]
+  const int ot = tile / (NFLAT / 32), it = tile - ot * (NFLAT / 32);
   const int t = threadIdx.x;
-  const int ol = t >> 2, ic = (t & 3) * 16;
-  const int o = 64 * ot + ol, i0 = 64 * it;
+  const int ol = t >> 2, ic = (t & 3) * 8;
+  const int o = 64 * ot + ol, i0 = 32 * it;
   const int64_t e0 = OFF_FC1_W + (int64_t)o * NFLAT + i0 + ic;
-  float v[16];
+  float4 p[2], g[2], sq[2], ac[2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float4 p = *reinterpret_cast<float4*>(a.param + e0 + 4 * j);
+  for (int j = 0; j < 2; ++j) {
+    p[j] = *reinterpret_cast<float4*>(a.param + e0 + 4 * j);
     if (UPDATE) {
-      const float4 g = *reinterpret_cast<const float4*>(a.grad + e0 + 4 * j);
-      float4 sq = *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j);
-      float4 ac = *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j);
-      ad.step(p.x, g.x, sq.x, ac.x);
-      ad.step(p.y, g.y, sq.y, ac.y);
-      ad.step(p.z, g.z, sq.z, ac.z);
-      ad.step(p.w, g.w, sq.w, ac.w);
-      *reinterpret_cast<float4*>(a.param + e0 + 4 * j) = p;
-      *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j) = sq;
-      *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j) = ac;
+      g[j] = *reinterpret_cast<const float4*>(a.grad + e0 + 4 * j);
+      sq[j] = *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j);
+      ac[j] = *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j);
     }
-    v[4 * j] = p.x; v[4 * j + 1] = p.y; v[4 * j + 2] = p.z; v[4 * j + 3] = p.w;
   }
-  uint4 lo, hi;
-  lo.x = pack2bf(v[0], v[1]); lo.y = pack2bf(v[2], v[3]); lo.z = pack2bf(v[4], v[5]); lo.w = pack2bf(v[6], v[7]);
-  hi.x = pack2bf(v[8], v[9]); hi.y = pack2bf(v[10], v[11]); hi.z = pack2bf(v[12], v[13]); hi.w = pack2bf(v[14], v[15]);
-  uint4* w1p = reinterpret_cast<uint4*>(a.w1 + (int64_t)o * NFLAT + i0 + ic);
-  w1p[0] = lo;
-  w1p[1] = hi;
+  float v[8];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) ts[(ic + j) * TS + ol] = f2bf(v[j]);
+  for (int j = 0; j < 2; ++j) {
+    if (UPDATE) {
+      ad.step(p[j].x, g[j].x, sq[j].x, ac[j].x);
+      ad.step(p[j].y, g[j].y, sq[j].y, ac[j].y);
+      ad.step(p[j].z, g[j].z, sq[j].z, ac[j].z);
+      ad.step(p[j].w, g[j].w, sq[j].w, ac[j].w);
+      *reinterpret_cast<float4*>(a.param + e0 + 4 * j) = p[j];
+      *reinterpret_cast<float4*>(a.square_avg + e0 + 4 * j) = sq[j];
+      *reinterpret_cast<float4*>(a.acc_delta + e0 + 4 * j) = ac[j];
+    }
+    v[4 * j] = p[j].x; v[4 * j + 1] = p[j].y; v[4 * j + 2] = p[j].z; v[4 * j + 3] = p[j].w;
+  }
+  uint4 lo;
+  lo.x = pack2bf(v[0], v[1]); lo.y = pack2bf(v[2], v[3]); lo.z = pack2bf(v[4], v[5]); lo.w = pack2bf(v[6], v[7]);
+  *reinterpret_cast<uint4*>(a.w1 + (int64_t)o * NFLAT + i0 + ic) = lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ts[(ic + j) * TS + ol] = f2bf(v[j]);
   __syncthreads();
-  const int il = t >> 2, oc = (t & 3) * 16;
-  const uint4* src = reinterpret_cast<const uint4*>(ts + il * TS + oc);
-  uint4* dst = reinterpret_cast<uint4*>(a.w1t + (int64_t)(i0 + il) * NH + 64 * ot + oc);
-  dst[0] = src[0];
-  dst[1] = src[1];
+  const int il = t >> 3, oc = (t & 7) * 8;
+  *reinterpret_cast<uint4*>(a.w1t + (int64_t)(i0 + il) * NH + 64 * ot + oc) =
+      *reinterpret_cast<const uint4*>(ts + il * TS + oc);
 }
 }  // namespace
 
 template <bool UPDATE>
 __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int region) {
-  __shared__ __attribute__((aligned(16))) uint16_t ts[64 * 72];
+  __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;

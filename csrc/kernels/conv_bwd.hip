@@ -3,10 +3,10 @@
 // Replaces the autograd backward of reference mnist_ddp.py:50-55 (dropout1, max_pool2d, relu, conv2,
 // relu, conv1): max_pool2d_with_indices_backward, threshold_backward x2, convolution_backward x2.
 //
-//  * conv2_dgrad_kernel  (WG = image x strip of 7 conv1 rows): builds the un-pooled gradient dy
-//    (zero except at each window's argmax) in a zero-padded NHWC LDS tile, runs the transposed
+//  * conv2_dgrad_kernel  (WG = image x strip of 7 conv1 rows): stages the dense un-pooled gradient dy
+//    (written by fc_bwd) into a zero-padded NHWC LDS tile with 16-B copies, runs the transposed
 //    convolution as an MFMA implicit GEMM (M = pixels, N = 32 ci, K = 9 taps x 64 co), applies the
-//    conv1 ReLU mask (conv1 recomputed bit-identically from the input, never stored), and folds
+//    conv1 ReLU mask (stored bf16 a1 > 0, prefetched under the MFMA loop), and folds
 //    the conv1 weight/bias gradient (K = 9 tiny) into the epilogue as per-workgroup partials.
 //  * conv2_wgrad_kernel  (G persistent WGs, each looping over half-images): dW2 = dy^T (x) im2col(a1),
 //    contraction over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
@@ -33,13 +33,16 @@ constexpr int WDYS_BYTES = WG_HALF_ROWS * H2 * C2 * 2;  // 36864
 constexpr int WA1S_BYTES = (WG_HALF_ROWS + 2) * H1 * C1 * 2;  // 23296
 constexpr int WG_LDS = WDYS_BYTES + WA1S_BYTES;
 constexpr int W2PART_STRIDE = 18432 + 64;
+
+// 16-byte-chunk XOR swizzles against ds_read_b128 / ds_read_b64_tr_b16 bank conflicts (rows of
+// 128 B = 8 chunks, or 64 B = 4 chunks).  Chosen with tools/lds_banks.py (gfx950 lane-group model).
+__device__ __forceinline__ int swz8(int row) { return row & 7; }
+__device__ __forceinline__ int swz_dy(int pix) { return (pix ^ (pix >> 1)) & 7; }
 }  // namespace
 
 int conv_wgrad_groups(int B) {
   const int units = 2 * B;
-  int g = units < 128 ? units : 128;
-  if (B >= 2048) g = 256;
-  return g;
+  return units < 256 ? units : 256;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -57,97 +60,126 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
   const int npix = nrows * H1;
   const int step = a.state ? a.state->step : 0;
 
-  // ---- phase 0: zero dy tile, stage w2d, gather input rows
+  // ---- phase 0: stage the padded dy tile (rows r0-2..r0+6, cols -2..25), w2d and the input rows.
+  // All global loads are independent 16-B loads issued before any LDS store.
   {
-    uint4 z = {0u, 0u, 0u, 0u};
-    for (int c = tid; c < DYS_BYTES / 16; c += 256) reinterpret_cast<uint4*>(dys)[c] = z;
+    constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
+    uint4 v[8];
+    const uint4 z = {0u, 0u, 0u, 0u};
+    const uint16_t* dyb = a.dy + (int64_t)b * H2 * H2 * C2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = tid + 256 * k;
+      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
+      const int y = r0 - 2 + ly, x = col - 2;
+      v[k] = z;
+      if (c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2)
+        v[k] = *reinterpret_cast<const uint4*>(dyb + (y * H2 + x) * C2 + c8 * 8);
+    }
+    uint4 w[9];
     const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) reinterpret_cast<uint4*>(w2ds)[tid + 256 * i] = src[tid + 256 * i];
+    for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
     const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
     const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG);
     for (int e = tid; e < DG_TROWS * IMG; e += 256) {
       const int row = r0 + e / IMG;
       xs[e] = (row < IMG) ? normalize_u8(src8[r0 * IMG + e]) : 0.0f;
     }
-  }
-  __syncthreads();
-  // ---- phase 1: un-pool the gradient into the padded NHWC tile (rows r0-2 .. r0+6)
-  {
-    const int py0 = (r0 >= 2) ? (r0 - 2) >> 1 : 0;
-    const int py1 = min(HP - 1, (r0 + DG_ROWS - 1) >> 1);
-    const int per_c = (py1 - py0 + 1) * HP;
-    const int total = per_c * C2;
-    const uint16_t* gb = a.g + (int64_t)b * NFLAT;
-    const uint8_t* mb = a.pmask + (int64_t)b * NFLAT;
-    for (int e = tid; e < total; e += 256) {
-      const int c = e / per_c, s = e - c * per_c;
-      const int flat = c * NPOOL + py0 * HP + s;
-      const uint16_t gv = gb[flat];
-      if (gv == 0) continue;
-      const int mk = mb[flat];
-      const int py = py0 + s / HP, px = s % HP;
-      const int y = 2 * py + ((mk >> 1) & 1), x = 2 * px + (mk & 1);
-      const int ly = y - r0 + 2;
-      if (ly >= 0 && ly < DG_TROWS) dys[(ly * DG_TCOLS + x + 2) * C2 + c] = gv;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = tid + 256 * k;
+      if (c < NCH) {
+        const int row = c >> 3, c8 = c & 7;
+        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = v[k];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, c8 = c & 7;
+      reinterpret_cast<uint4*>(w2ds)[row * 8 + (c8 ^ swz8(row))] = w[i];
     }
   }
   __syncthreads();
 
-  // ---- phase 2: transposed conv on MFMA: M-tiles 3w..3w+2 (16 pixels), N = 2 tiles of 16 ci
+  // ---- phase 2: transposed conv on MFMA: M-tiles 3w..3w+2 (16 pixels of the 26-wide strip),
+  // N = 2 tiles of 16 ci, K = 9 taps x 64 co.  (Enumerating M over the 28-wide padded grid is
+  // bank-conflict free but needs 13 tiles per strip - an unbalanced, branchy split that measured
+  // slower; this balanced split keeps the row&7 swizzle at ~1.6x the ideal read cost.)
   const int m = lane & 15, kg = lane >> 4;
-  int qy[3], qx[3];
+  constexpr int MT = 3;
+  int qbase[MT];
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt) {
-    int q = 16 * (3 * wave + mt) + m;
+  for (int i = 0; i < MT; ++i) {
+    int q = 16 * (3 * wave + i) + m;
     if (q >= npix) q = 0;
-    qy[mt] = q / H1;
-    qx[mt] = q - qy[mt] * H1;
+    const int qy = q / H1, qx = q - qy * H1;
+    qbase[i] = (qy + 2) * DG_TCOLS + qx + 2;     // LDS row of the un-shifted pixel
   }
-  floatx4 acc[3][2];
+  floatx4 acc[MT][2];
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt) acc[mt][0] = acc[mt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // conv1 ReLU mask for the epilogue = (a1 > 0): prefetch the stored bf16 a1 values now so the
+  // loads overlap the MFMA loop (no conv1 recompute)
+  uint16_t a1v[MT][4][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int q = 16 * (3 * wave + i) + 4 * kg + r;
+      q = q < npix ? q : npix - 1;
+      const uint16_t* src = a.a1 + ((int64_t)b * H1 * H1 + r0 * H1 + q) * C1 + m;
+      a1v[i][r][0] = src[0];
+      a1v[i][r][1] = src[16];
+    }
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) {
     const int t = ks >> 1, co0 = 32 * (ks & 1);
-    const int ky = t / 3, kx = t % 3;
-    bf16x8 A[3], Bf[2];
+    const int toff = (t / 3) * DG_TCOLS + (t % 3);
+    const int ch = (co0 >> 3) + kg;
+    bf16x8 A[MT], Bf[2];
 #pragma unroll
-    for (int mt = 0; mt < 3; ++mt)
-      A[mt] = ld16(dys + ((qy[mt] + 2 - ky) * DG_TCOLS + (qx[mt] + 2 - kx)) * C2 + co0 + 8 * kg);
+    for (int i = 0; i < MT; ++i) {
+      const int row = qbase[i] - toff;
+      A[i] = ld16(dys + row * C2 + ((ch ^ swz8(row)) << 3));
+    }
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) Bf[nt] = ld16(w2ds + (t * C1 + nt * 16 + m) * C2 + co0 + 8 * kg);
+    for (int nt = 0; nt < 2; ++nt) {
+      const int row = t * C1 + nt * 16 + m;
+      Bf[nt] = ld16(w2ds + row * C2 + ((ch ^ swz8(row)) << 3));
+    }
 #pragma unroll
-    for (int mt = 0; mt < 3; ++mt)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(A[mt], Bf[nt], acc[mt][nt]);
+      for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bf[nt], acc[i][nt]);
   }
 
-  // ---- phase 3: conv1 ReLU mask (recomputed) + conv1 weight/bias gradient partials
-  float w[2][9], bias[2], sdw[2][9], sdb[2];
+  // ---- phase 3: conv1 ReLU mask (a1 > 0) + conv1 weight/bias gradient partials
+  float sdw[2][9], sdb[2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
-    const int ci = nt * 16 + m;
-    bias[nt] = a.b1c[ci];
     sdb[nt] = 0.f;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) { w[nt][t] = a.w1c[ci * 9 + t]; sdw[nt][t] = 0.f; }
+    for (int t = 0; t < 9; ++t) sdw[nt][t] = 0.f;
   }
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = 16 * (3 * wave + mt) + 4 * kg + r;
+      const int q = 16 * (3 * wave + i) + 4 * kg + r;
       if (q < npix) {
         const int py = q / H1, px = q - py * H1;
         const float* xp = xs + py * IMG + px;
+        float xv[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) xv[t] = xp[(t / 3) * IMG + (t % 3)];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const float z = conv1_preact(xp, IMG, w[nt], bias[nt]);
-          const float d = (z > 0.0f) ? acc[mt][nt][r] : 0.0f;
+          const uint16_t av = a1v[i][r][nt];
+          const float d = (av != 0 && !(av & 0x8000)) ? acc[i][nt][r] : 0.0f;
           sdb[nt] += d;
 #pragma unroll
-          for (int t = 0; t < 9; ++t) sdw[nt][t] = __builtin_fmaf(d, xp[(t / 3) * IMG + (t % 3)], sdw[nt][t]);
+          for (int t = 0; t < 9; ++t) sdw[nt][t] = __builtin_fmaf(d, xv[t], sdw[nt][t]);
         }
       }
     }
@@ -192,103 +224,146 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(ConvBwdArgs a, int B) 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;   // conv2 bias grad partial for channel tid>>2 (4 lanes per channel)
-  const int bc = tid >> 2, bsub = tid & 3;
+  // conv2 bias partial: each thread always stages channels 8*(tid&7)..+7 of the dy tile
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  constexpr int DY_CH = WDYS_BYTES / 16;   // 2304 = 9 per thread
+  // per-lane fragment offsets (elements), hoisted out of the unit and k-step loops
+  const int clo = 8 * gq + q, chi = clo + 4;
+  int aoff_lo[2], aoff_hi[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cb = 16 * (mt0 + i) + 4 * pp;
+    aoff_lo[i] = clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7));
+    aoff_hi[i] = chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7));
+  }
+  constexpr int A1_CH = WA1S_BYTES / 16;   // 1456
 
   for (int u = blockIdx.x; u < 2 * B; u += G) {
     const int b = u >> 1, h = u & 1;
     {
-      uint4 z = {0u, 0u, 0u, 0u};
-      for (int c = tid; c < WDYS_BYTES / 16; c += 256) reinterpret_cast<uint4*>(dys)[c] = z;
-      const uint4* src = reinterpret_cast<const uint4*>(a.a1 + ((int64_t)b * H1 + WG_HALF_ROWS * h) * H1 * C1);
-      for (int c = tid; c < WA1S_BYTES / 16; c += 256) reinterpret_cast<uint4*>(a1s)[c] = src[c];
-    }
-    __syncthreads();
-    {
-      const uint16_t* gb = a.g + (int64_t)b * NFLAT + bc * NPOOL + 6 * h * HP;
-      const uint8_t* mb = a.pmask + (int64_t)b * NFLAT + bc * NPOOL + 6 * h * HP;
-#pragma unroll 2
-      for (int k = 0; k < 18; ++k) {
-        const int s = bsub + 4 * k;           // 0..71 within the 6 pooled rows
-        const uint16_t gv = gb[s];
-        if (gv != 0) {
-          bsum += bf2f(gv);
-          const int mk = mb[s];
-          const int py = s / HP, px = s - py * HP;
-          const int y = 2 * py + ((mk >> 1) & 1), x = 2 * px + (mk & 1);
-          dys[(y * H2 + x) * C2 + bc] = gv;
+      const uint4* dsrc = reinterpret_cast<const uint4*>(a.dy + ((int64_t)b * H2 + WG_HALF_ROWS * h) * H2 * C2);
+      const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + ((int64_t)b * H1 + WG_HALF_ROWS * h) * H1 * C1);
+      uint4 vd[9], va[6];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) vd[k] = dsrc[tid + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int c = tid + 256 * k;
+        va[k] = asrc[c < A1_CH ? c : A1_CH - 1];   // clamped: no conditional load (keeps va in VGPRs)
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int c = tid + 256 * k, pix = c >> 3;
+        reinterpret_cast<uint4*>(dys)[pix * 8 + ((c & 7) ^ swz_dy(pix))] = vd[k];
+        const uint32_t w4[4] = {vd[k].x, vd[k].y, vd[k].z, vd[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bsum[2 * j] += bf2f((uint16_t)(w4[j] & 0xFFFF));
+          bsum[2 * j + 1] += bf2f((uint16_t)(w4[j] >> 16));
         }
       }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int c = tid + 256 * k;
+        if (c < A1_CH) reinterpret_cast<uint4*>(a1s)[c] = va[k];
+      }
+      (void)DY_CH;
     }
     __syncthreads();
 #pragma unroll 1
     for (int ks = 0; ks < 9; ++ks) {
-      const int plo = 32 * ks + 8 * gq + q, phi = plo + 4;
-      const int ylo = plo / H2, xlo = plo - ylo * H2;
-      const int yhi = phi / H2, xhi = phi - yhi * H2;
+      // A: dy rows (pixels) 32ks + c; the chunk swizzle (c ^ c>>1) & 7 does not depend on ks
       bf16x8 A[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int cb = 16 * (mt0 + i) + 4 * pp;
-        A[i] = tr_frag(dys + plo * C2 + cb, dys + phi * C2 + cb);
-      }
+      for (int i = 0; i < 2; ++i) A[i] = tr_frag(dys + ks * 32 * C2 + aoff_lo[i], dys + ks * 32 * C2 + aoff_hi[i]);
+      // B: a1 pixel of dy pixel p = 32ks + c shifted by the tap = p + 2*(p/24) + (ky*26 + kx)
+      const int plo = 32 * ks + clo, phi = plo + 4;
+      const uint16_t* blo = a1s + (plo + 2 * (plo / H2)) * C1 + 4 * pp;
+      const uint16_t* bhi = a1s + (phi + 2 * (phi / H2)) * C1 + 4 * pp;
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
-        const int nt = nt0 + j, t = nt >> 1, ci0 = 16 * (nt & 1) + 4 * pp;
-        const int ky = t / 3, kx = t % 3;
-        const bf16x8 Bf = tr_frag(a1s + ((ylo + ky) * H1 + xlo + kx) * C1 + ci0,
-                                  a1s + ((yhi + ky) * H1 + xhi + kx) * C1 + ci0);
+        const int nt = nt0 + j, t = nt >> 1, ci0 = 16 * (nt & 1);
+        const int toff = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
+        const bf16x8 Bf = tr_frag(blo + toff, bhi + toff);
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
       }
     }
     __syncthreads();
   }
+  // slab layout = MFMA-native [co-tile 4][n-tile 18][lane 64][4]: one coalesced float4 per tile
   float* out = a.w2part + (int64_t)blockIdx.x * W2PART_STRIDE;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-      const int nt = nt0 + j, t = nt >> 1, ci = 16 * (nt & 1) + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = 16 * (mt0 + i) + 4 * gq + r;
-        out[co * 288 + ci * 9 + t] = acc[i][j][r];
-      }
+      const int tile = (mt0 + i) * 18 + nt0 + j;
+      *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
     }
-  bsum += __shfl_xor(bsum, 1, 64);
-  bsum += __shfl_xor(bsum, 2, 64);
-  if (bsub == 0) out[18432 + bc] = bsum;
+  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 32 such threads via LDS
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[j * 256 + tid] = bsum[j];
+  __syncthreads();
+  if (tid < 64) {
+    const int c8 = tid >> 3, j = tid & 7;     // channel = 8*c8 + j
+    float s = 0.f;
+    for (int k = 0; k < 32; ++k) s += red[j * 256 + k * 8 + c8];
+    out[18432 + 8 * c8 + j] = s;
+  }
 }
 
 // --------------------------------------------------------------------------------------------
-// roles: [0, 72) conv2.weight columns, 72: conv2.bias, [73, 93): conv1 weight+bias (16 outputs each)
+// Deterministic fixed-order reduction of the partial slabs into the flat fp32 gradient buffer.
+//   [0, 288): conv2.weight, 64 outputs per WG, the 4 waves split the slabs, 8 loads in flight
+//   288:      conv2.bias
+//   [289, 309): conv1 weight+bias, 16 outputs x 16 slab-slices per WG
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
   __shared__ float red[256];
   const int tid = threadIdx.x, bid = blockIdx.x;
   const int G = a.wgrad_groups;
   const float sc = a.grad_scale;
-  if (bid < 72) {
-    const int e = bid * 256 + tid;
-    float s = 0.f;
-    for (int g0 = 0; g0 < G; ++g0) s += a.w2part[(int64_t)g0 * W2PART_STRIDE + e];
-    a.grad[OFF_CONV2_W + e] = s * sc;
-  } else if (bid == 72) {
+  if (bid < 288 || bid == 288) {
+    const int e = (bid < 288) ? bid * 64 + (tid & 63) : 18432 + (tid & 63);
+    const int sl = tid >> 6;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int g0 = sl;
+    for (; g0 + 28 < G; g0 += 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += a.w2part[(int64_t)(g0 + 4 * k) * W2PART_STRIDE + e];
+    }
+    for (; g0 < G; g0 += 4) s[0] += a.w2part[(int64_t)g0 * W2PART_STRIDE + e];
+    red[tid] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    __syncthreads();
     if (tid < 64) {
-      float s = 0.f;
-      for (int g0 = 0; g0 < G; ++g0) s += a.w2part[(int64_t)g0 * W2PART_STRIDE + 18432 + tid];
-      a.grad[OFF_CONV2_B + tid] = s * sc;
+      const float t = (red[tid] + red[tid + 64]) + (red[tid + 128] + red[tid + 192]);
+      if (bid < 288) {
+        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
+        const int r = e & 3, ln = (e >> 2) & 63, tile = e >> 8;
+        const int mtile = tile / 18, ntile = tile - mtile * 18;
+        const int co = 16 * mtile + 4 * (ln >> 4) + r;
+        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
+        a.grad[OFF_CONV2_W + co * 288 + ci * 9 + tap] = t * sc;
+      }
+      else a.grad[OFF_CONV2_B + tid] = t * sc;
     }
   } else {
-    const int j = (bid - 73) * 16 + (tid & 15), sl = tid >> 4;
+    const int j = (bid - 289) * 16 + (tid & 15), sl = tid >> 4;
     const int nslab = 4 * B;
-    float s = 0.f;
-    for (int k = sl; k < nslab; k += 16) s += a.c1part[(int64_t)k * 320 + j];
-    red[tid] = s;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = sl;
+    for (; k + 48 < nslab; k += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += a.c1part[(int64_t)(k + 16 * u) * 320 + j];
+    }
+    for (; k < nslab; k += 16) s[0] += a.c1part[(int64_t)k * 320 + j];
+    red[tid] = (s[0] + s[1]) + (s[2] + s[3]);
     __syncthreads();
     if (tid < 16) {
       float t = 0.f;
-      for (int k = 0; k < 16; ++k) t += red[k * 16 + tid];
+      for (int q = 0; q < 16; ++q) t += red[q * 16 + tid];
       const int ci = j / 10, kk = j - ci * 10;
       if (kk < 9) a.grad[OFF_CONV1_W + ci * 9 + kk] = t * sc;
       else a.grad[OFF_CONV1_B + ci] = t * sc;
@@ -296,13 +371,19 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, in
   }
 }
 
-void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
+void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
+}
+void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(256), 0, s, a, B);
+}
+void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
+  launch_conv_dgrad(a, B, s);
+  launch_conv_wgrad(a, B, s);
 }
 
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(93), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(289 + 20), dim3(256), 0, s, a, B);
 }
 
 }  // namespace mnist

@@ -10,44 +10,50 @@ namespace mnist {
 
 // ============================================================================================
 // fc1 forward: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
-// M = B rows, N = 128, K = 9216 split 16 ways (576 each).  One wave = 16 rows x 128 cols x one
-// K-chunk; fragments stream straight from L2 (w1 is 2.4 MB bf16, L2/MALL resident) into VGPRs.
+// M = B rows, N = 128, K = 9216 split FC1_KSPLIT (32) ways (288 = 9 k-steps each).
+// WG = (16-row M-tile, K-chunk); its 4 waves split N (32 columns each), so every CU streams a
+// distinct 18 KB slice of w1 (L2/MALL resident) and the grid is ceil(B/16) x 32 WGs.  All 27
+// fragment loads of a wave are independent and issued before the MFMAs.
 // ============================================================================================
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
                                                       const uint16_t* __restrict__ w1,
                                                       float* __restrict__ z1part, int B) {
-  constexpr int KC = NFLAT / FC1_KSPLIT;
+  constexpr int KC = NFLAT / FC1_KSPLIT;   // 288
+  constexpr int KS = KC / 32;              // 9
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int m = lane & 15, kg = lane >> 4;
-  const int chunk = blockIdx.y * 4 + wave;
+  const int chunk = blockIdx.y;
   const int row = blockIdx.x * 16 + m;
   const bool valid = row < B;
   const uint16_t* pa = p + (int64_t)(valid ? row : 0) * NFLAT + chunk * KC + 8 * kg;
-  const uint16_t* pb = w1 + (int64_t)m * NFLAT + chunk * KC + 8 * kg;
-  floatx4 acc[8];
+  const uint16_t* pb = w1 + (int64_t)(32 * wave + m) * NFLAT + chunk * KC + 8 * kg;
+  bf16x8 A[KS], B0[KS], B1[KS];
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-  for (int ks = 0; ks < KC / 32; ++ks) {
-    bf16x8 A = ld16(pa + ks * 32);
-    if (!valid) A = zero_frag();
-    bf16x8 Bf[8];
+  for (int ks = 0; ks < KS; ++ks) {
+    A[ks] = ld16(pa + ks * 32);
+    B0[ks] = ld16(pb + ks * 32);
+    B1[ks] = ld16(pb + 16 * NFLAT + ks * 32);
+  }
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt) Bf[nt] = ld16(pb + (int64_t)nt * 16 * NFLAT + ks * 32);
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) acc[nt] = mfma16x16x32(A, Bf[nt], acc[nt]);
+  for (int ks = 0; ks < KS; ++ks) {
+    const bf16x8 a = valid ? A[ks] : zero_frag();
+    acc0 = mfma16x16x32(a, B0[ks], acc0);
+    acc1 = mfma16x16x32(a, B1[ks], acc1);
   }
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = blockIdx.x * 16 + 4 * kg + r;
-      if (b < B) z1part[((int64_t)chunk * B + b) * NH + nt * 16 + m] = acc[nt][r];
+  for (int r = 0; r < 4; ++r) {
+    const int b = blockIdx.x * 16 + 4 * kg + r;
+    if (b < B) {
+      float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
+      dst[0] = acc0[r];
+      dst[16] = acc1[r];
     }
+  }
 }
 
 void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s) {
-  dim3 grid((B + 15) / 16, FC1_KSPLIT / 4);
+  dim3 grid((B + 15) / 16, FC1_KSPLIT);
   hipLaunchKernelGGL(fc1_fwd_kernel, grid, dim3(256), 0, s, p, w1, z1part, B);
 }
 
@@ -188,20 +194,20 @@ void launch_head_eval(const HeadArgs& a, int B, hipStream_t s) {
 //   A (145 WGs): dW_fc1[o][i] = sum_b dz1[b][o] p[b][i]  (M=128, N=64 per WG, K=B); WG 144 computes
 //                db_fc1 = dz1^T * ones.  Both operands are k(=batch)-major in memory, so each
 //                32-row k-slab is staged in LDS and read with ds_read_b64_tr_b16 (hardware transpose).
-//   B (ceil(B/64)*144 WGs): g[b][i] = (dz1 . w1)[b][i] * dropout1/relu/pool mask  (M=B, N=9216, K=128)
+//   B (ceil(B/16)*36 WGs): dy = unpool((dz1 . w1) * dropout-1 / ReLU mask) as dense NHWC bf16 (M=B, N=9216, K=128)
 //   C (1 WG): dW_fc2 = dl^T h, db_fc2 = dl^T 1 (MFMA, 4 waves split K, LDS reduce) + mean loss.
 // ============================================================================================
 namespace {
 constexpr int ROLE_A_WGS = NFLAT / 64 + 1;   // 145
+constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
 
+// A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
+// loaded into VGPRs while the current one (double-buffered LDS) feeds the MFMAs; one barrier per slab.
 __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, unsigned char* smem) {
-  uint16_t* dzs = reinterpret_cast<uint16_t*>(smem);           // [32][128]
-  uint16_t* ps = reinterpret_cast<uint16_t*>(smem + 8192);     // [32][64]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const bool ones = (ib == NFLAT / 64);
   const int i0 = ones ? 0 : ib * 64;
-  const int ntiles = ones ? 1 : 4;
   floatx4 acc[2][4];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -214,19 +220,24 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
     us8 v = {one, one, one, one, one, one, one, one};
     onesfrag = __builtin_bit_cast(bf16x8, v);
   }
-  for (int kb = 0; kb < Bp / 32; ++kb) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = tid + 256 * j, row = c >> 4, c16 = c & 15;
-      *reinterpret_cast<uint4*>(dzs + row * 128 + c16 * 8) =
-          *reinterpret_cast<const uint4*>(a.dz1 + (int64_t)(kb * 32 + row) * NH + c16 * 8);
-    }
-    if (!ones) {
-      const int row = tid >> 3, c8 = tid & 7, b = kb * 32 + row;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (b < B) v = *reinterpret_cast<const uint4*>(a.p + (int64_t)b * NFLAT + i0 + c8 * 8);
-      *reinterpret_cast<uint4*>(ps + row * 64 + c8 * 8) = v;
-    }
+  const int nkb = Bp / 32;
+  const int prow = tid >> 3, pc8 = tid & 7;
+  uint4 rz0, rz1, rp = {0u, 0u, 0u, 0u};
+  auto fetch = [&](int kb) {
+    rz0 = *reinterpret_cast<const uint4*>(a.dz1 + (int64_t)(kb * 32 + (tid >> 4)) * NH + (tid & 15) * 8);
+    rz1 = *reinterpret_cast<const uint4*>(a.dz1 + (int64_t)(kb * 32 + 16 + (tid >> 4)) * NH + (tid & 15) * 8);
+    const int b = kb * 32 + prow;
+    rp = uint4{0u, 0u, 0u, 0u};
+    if (!ones && b < B) rp = *reinterpret_cast<const uint4*>(a.p + (int64_t)b * NFLAT + i0 + pc8 * 8);
+  };
+  fetch(0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    uint16_t* dzs = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288);          // [32][128]
+    uint16_t* ps = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288 + 8192);    // [32][64]
+    *reinterpret_cast<uint4*>(dzs + (tid >> 4) * 128 + (tid & 15) * 8) = rz0;
+    *reinterpret_cast<uint4*>(dzs + (16 + (tid >> 4)) * 128 + (tid & 15) * 8) = rz1;
+    *reinterpret_cast<uint4*>(ps + prow * 64 + pc8 * 8) = rp;
+    if (kb + 1 < nkb) fetch(kb + 1);
     __syncthreads();
     const int rlo = 8 * g + q, rhi = rlo + 4;
 #pragma unroll
@@ -244,9 +255,7 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
         }
       }
     }
-    __syncthreads();
   }
-  (void)ntiles;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -262,39 +271,70 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
     }
 }
 
-__device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb) {
+// B: gradient into the conv trunk.  WG = 16 batch rows x 4 consecutive pooled positions x 64 channels
+// (N = 256 columns of dz1 . w1).  The epilogue applies dropout-1 scale/keep, the ReLU (pooled > 0)
+// and max-pool routing (argmax) and writes the *dense* NHWC conv2-output gradient dy for the 2x8-pixel
+// footprint through LDS, so every global store is a full 1 KB row segment and the conv backward
+// kernels stage dy with plain 16-byte copies.
+__device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb, unsigned char* smem) {
+  uint8_t* pms = smem;                                          // [16 b][64 c][4 j]
+  uint16_t* dyst = reinterpret_cast<uint16_t*>(smem + 4096);    // [16 b][2 y][8 x][64 c]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m = lane & 15, kg = lane >> 4;
-  const int bm = rb / (NFLAT / 64), ib = rb - bm * (NFLAT / 64);
-  const int i0 = ib * 64;
-  const int row = bm * 64 + 16 * wave + m;
-  const bool rvalid = row < Bp;
+  const int bb = rb / ROLE_B_SBLOCKS, sb = rb - bb * ROLE_B_SBLOCKS;
+  const int py = sb / 3, px0 = (sb - py * 3) * 4;
+  const int s0 = py * HP + px0;
+  const int b0 = bb * 16;
   const float dscale = (a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT)) ? 1.0f : (1.0f / KEEP1);
+  // pmask tile (4 consecutive pooled positions per (b, c) = one u32) + zero the dy staging tile
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
+    uint32_t v = 0;
+    if (b0 + bl < B) v = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)(b0 + bl) * NFLAT + c * NPOOL + s0);
+    reinterpret_cast<uint32_t*>(pms)[idx] = v;
+  }
+  {
+    const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) reinterpret_cast<uint4*>(dyst)[tid + 256 * k] = z;
+  }
+  // MFMA: wave w owns pooled position s0 + w, 4 N-tiles = 64 channels; K = 128
   floatx4 acc[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;
 #pragma unroll
   for (int ks = 0; ks < NH / 32; ++ks) {
-    bf16x8 A = ld16(a.dz1 + (int64_t)(rvalid ? row : 0) * NH + ks * 32 + 8 * kg);
-    if (!rvalid) A = zero_frag();
+    const bf16x8 A = ld16(arow + ks * 32);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const bf16x8 Bf = ld16(a.w1t + (int64_t)(i0 + 16 * nt + m) * NH + ks * 32 + 8 * kg);
+      const int c = 16 * nt + m;
+      const bf16x8 Bf = ld16(a.w1t + (int64_t)(c * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
       acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
     }
   }
+  __syncthreads();
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int b = bm * 64 + 16 * wave + 4 * kg + r;
-      const int i = i0 + 16 * nt + m;
-      if (b < B) {
-        const uint8_t mk = a.pmask[(int64_t)b * NFLAT + i];
-        const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;
-        a.g[(int64_t)b * NFLAT + i] = f2bf(v);
+      const int bl = 4 * kg + r, c = 16 * nt + m;
+      const int mk = pms[(bl * 64 + c) * 4 + wave];
+      if ((mk & 12) == 12) {
+        const int yl = (mk >> 1) & 1, xl = 2 * wave + (mk & 1);
+        dyst[((bl * 2 + yl) * 8 + xl) * 64 + c] = f2bf(acc[nt][r] * dscale);
       }
     }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int cidx = tid + 256 * k, bl = cidx >> 7, yl = (cidx >> 6) & 1, off = cidx & 63;
+    if (b0 + bl < B) {
+      uint4* dst = reinterpret_cast<uint4*>(a.dy + (((int64_t)(b0 + bl) * H2 + 2 * py + yl) * H2 + 2 * px0) * C2);
+      dst[off] = reinterpret_cast<const uint4*>(dyst)[cidx];
+    }
+  }
 }
 
 __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp, unsigned char* smem) {
@@ -369,24 +409,22 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
 }  // namespace
 
 __global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 9216];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   const int bid = blockIdx.x;
-  const int nbm = (B + 63) / 64;
-  const int nb_roles = nbm * (NFLAT / 64);
+  const int nb_roles = 0;
   // role C (one long-running WG) first so it is dispatched before the short role-B tiles
   if (bid == 0) {
     fc_bwd_role_c(a, B, Bp, smem);
   } else if (bid <= ROLE_A_WGS) {
     fc_bwd_role_a(a, B, Bp, bid - 1, smem);
   } else {
-    fc_bwd_role_b(a, B, Bp, bid - 1 - ROLE_A_WGS);
+    fc_bwd_role_b(a, B, Bp, bid - 1 - ROLE_A_WGS, smem);
   }
   (void)nb_roles;
 }
 
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
-  const int nbm = (B + 63) / 64;
-  const int grid = ROLE_A_WGS + nbm * (NFLAT / 64) + 1;
+  const int grid = 1 + ROLE_A_WGS + ((B + 15) / 16) * ROLE_B_SBLOCKS;
   hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp);
 }
 

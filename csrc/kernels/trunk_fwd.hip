@@ -35,7 +35,7 @@ constexpr int LDS_TOTAL = FLAG_OFF + FLAG_BYTES;
 
 // 16-byte-chunk XOR swizzles (4 chunks of 8 channels per 64-byte row) against ds_read_b128 bank
 // conflicts: a1 rows are indexed by pixel, w2 rows by (channel, tap).
-__device__ __forceinline__ int swz_a1(int pix) { return (pix >> 2) & 3; }
+__device__ __forceinline__ int swz_a1(int pix) { return 0 * pix; }   // model: no XOR beats (p>>2)&3
 __device__ __forceinline__ int swz_w2(int n) { return (4 - ((n >> 2) & 3)) & 3; }
 }  // namespace
 
@@ -53,33 +53,56 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
   const int b = blockIdx.y;       // row in batch
   const int step = a.state ? a.state->step : 0;
 
-  // ---- phase 0: conv2 weights -> LDS (swizzled), input rows -> LDS (normalised fp32)
+  // ---- phase 0: issue every global load first (conv2 weights, conv1 weights, the gathered image
+  // rows), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
+  const int c = tid & 3;                         // conv1: fixed 8-channel chunk per thread
+  float w[8][9], bias[8];
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.w2f);
+    uint4 wv[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) wv[i] = src[tid + 256 * i];
+    const float4* w1v = reinterpret_cast<const float4*>(a.w1c + c * 72);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      const float4 f = w1v[k];
+      const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[(4 * k + e) / 9][(4 * k + e) % 9] = fv[e];
+    }
+    const float4* b1v = reinterpret_cast<const float4*>(a.b1c + c * 8);
+    const float4 b0 = b1v[0], b1 = b1v[1];
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+    const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
+    uint4 xv = {0u, 0u, 0u, 0u};
+    constexpr int XCH = X_ROWS * IMG / 16;       // 21 16-byte chunks (image rows are 16-B aligned)
+    if (tid < XCH)
+      xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-      const int c = tid + 256 * i;                 // 2304 chunks of 16 B
-      const int row = c >> 2, kc = c & 3;          // row = n*9 + tap
+      const int ch = tid + 256 * i;                // 2304 chunks of 16 B
+      const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
       const int n = row / 9;
-      uint4 v = src[c];
-      *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = v;
+      *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = wv[i];
     }
-    const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
-    const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG;
-    for (int e = tid; e < X_ROWS * IMG; e += 256) xs[e] = normalize_u8(src8[e]);
+    if (tid < XCH) {
+      const uint32_t words[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float4 f;
+        f.x = normalize_u8((uint8_t)(words[k] & 0xFF));
+        f.y = normalize_u8((uint8_t)((words[k] >> 8) & 0xFF));
+        f.z = normalize_u8((uint8_t)((words[k] >> 16) & 0xFF));
+        f.w = normalize_u8((uint8_t)(words[k] >> 24));
+        *reinterpret_cast<float4*>(xs + tid * 16 + 4 * k) = f;
+      }
+    }
   }
   __syncthreads();
 
   // ---- phase 1: conv1 + bias + ReLU (fp32 VALU) -> a1 tile (bf16 NHWC, swizzled) [+ HBM copy]
   {
-    const int c = tid & 3;                         // fixed 8-channel chunk per thread
-    float w[8][9], bias[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bias[j] = a.b1c[c * 8 + j];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) w[j][t] = a.w1c[(c * 8 + j) * 9 + t];
-    }
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int pidx = (tid >> 2) + 64 * i;

@@ -25,6 +25,8 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_conv_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_w_, hipEventDisableTiming));
+  HIP_OK(hipStreamCreateWithFlags(&wgrad_stream_, hipStreamNonBlocking));
   alloc_workspace();
 }
 
@@ -34,6 +36,8 @@ Engine::~Engine() {
   if (ev_fc_) hipEventDestroy(ev_fc_);
   if (ev_conv_) hipEventDestroy(ev_conv_);
   if (ev_done_) hipEventDestroy(ev_done_);
+  if (ev_w_) hipEventDestroy(ev_w_);
+  if (wgrad_stream_) hipStreamDestroy(wgrad_stream_);
   if (ws_) hipFree(ws_);
 }
 
@@ -51,7 +55,7 @@ void Engine::alloc_workspace() {
   const int64_t o_dz = carve((int64_t)Mp * NH * 2);
   const int64_t o_h = carve((int64_t)Mp * NH * 2);
   const int64_t o_dl = carve((int64_t)Mp * 16 * 2);
-  const int64_t o_g = carve((int64_t)M * NFLAT * 2);
+  const int64_t o_g = carve((int64_t)M * H2 * H2 * C2 * 2);   // dense dy
   const int64_t o_c1 = carve((int64_t)4 * M * 320 * 4);
   const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
   ws_bytes_ = off;
@@ -66,7 +70,7 @@ void Engine::alloc_workspace() {
   dz1_ = reinterpret_cast<uint16_t*>(base + o_dz);
   h_bf_ = reinterpret_cast<uint16_t*>(base + o_h);
   dl_bf_ = reinterpret_cast<uint16_t*>(base + o_dl);
-  g_ = reinterpret_cast<uint16_t*>(base + o_g);
+  dy_ = reinterpret_cast<uint16_t*>(base + o_g);
   c1part_ = reinterpret_cast<float*>(base + o_c1);
   w2part_ = reinterpret_cast<float*>(base + o_w2);
 }
@@ -99,42 +103,50 @@ void Engine::enqueue_step(int batch) {
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
-  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, g_,
+  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, dy_,
                buf_.loss_log, gscale, 1.0f / (float)B};
   launch_fc_bwd(fb, B, Bp, compute_);
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
   const bool dist = comm_ && world_ > 1;
-  if (dist && two_buckets_) {
-    // bucket 0 (fc params, 98.4% of the bytes) is complete here: reduce it under the conv backward
-    HIP_OK(hipEventRecord(ev_fc_, compute_));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
-    comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
+  // serial mode keeps every kernel of the optimizer / wgrad branches on the compute stream
+  hipStream_t ws = concurrent_ ? wgrad_stream_ : compute_;
+  hipStream_t ms = (concurrent_ || dist) ? comm_stream_ : compute_;
+  // fork: the fc bucket (98.4 % of the bytes) is complete; conv2 wgrad and the fc optimizer branch off
+  HIP_OK(hipEventRecord(ev_fc_, compute_));
+  if (ws != compute_) HIP_OK(hipStreamWaitEvent(ws, ev_fc_, 0));
+  if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_fc_, 0));
+  // single GPU, serial schedule: one fused Adadelta launch over everything at the end of the step
+  const bool one_update = !dist && !concurrent_;
+  if (!one_update && (two_buckets_ || !dist)) {
+    if (dist) comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, ms);
+    launch_adadelta(ad, ADA_FC, ms);
   }
-  ConvBwdArgs cb{g_, pmask_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
+  ConvBwdArgs cb{dy_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
                  buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B)};
-  launch_conv_bwd(cb, B, compute_);
+  launch_conv_wgrad(cb, B, ws);
+  if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
+  launch_conv_dgrad(cb, B, compute_);
+  if (ws != compute_) HIP_OK(hipStreamWaitEvent(compute_, ev_w_, 0));
   launch_conv_grad_reduce(cb, B, compute_);
-  if (dist) {
-    HIP_OK(hipEventRecord(ev_conv_, compute_));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_conv_, 0));
-    AdadeltaArgs adc = ad;
-    adc.state_inc = buf_.state;
-    if (two_buckets_) {
-      comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, comm_stream_);
-      launch_adadelta(adc, ADA_CONV, comm_stream_);
-    } else {
-      comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, comm_stream_);
-      launch_adadelta(adc, ADA_ALL, comm_stream_);
-    }
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+  HIP_OK(hipEventRecord(ev_conv_, compute_));
+  if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_conv_, 0));
+  AdadeltaArgs adc = ad;
+  adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
+  if (one_update) {
+    launch_adadelta(adc, ADA_ALL, ms);
+  } else if (dist && !two_buckets_) {
+    comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, ms);
+    launch_adadelta(adc, ADA_ALL, ms);
   } else {
-    ad.state_inc = buf_.state;
-    launch_adadelta(ad, ADA_ALL, compute_);
+    if (dist) comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, ms);
+    launch_adadelta(adc, ADA_CONV, ms);
+  }
+  if (ms != compute_) {
+    HIP_OK(hipEventRecord(ev_done_, ms));
+    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
   }
 }
 
@@ -221,6 +233,7 @@ void Engine::broadcast_params(int root) {
 void Engine::synchronize() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
+  if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
 }
 
 }  // namespace mnist

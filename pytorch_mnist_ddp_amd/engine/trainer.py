@@ -19,6 +19,7 @@ Index order, RNG consumption, log lines and the loss values printed follow the r
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -42,7 +43,7 @@ class FusedTrainer:
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
-                 two_buckets: bool = True):
+                 two_buckets: bool = True, concurrent: bool | None = None):
         C = native.load()
         self.C, self.ms = C, mstate
         dev = mstate.device
@@ -81,6 +82,9 @@ class FusedTrainer:
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay)
         self.engine.set_bucket_split(two_buckets)
+        if concurrent is None:
+            concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
+        self.engine.set_concurrent(bool(concurrent))
         if comm is not None:
             self.engine.attach_comm(comm)
         self.comm = comm

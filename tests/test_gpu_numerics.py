@@ -152,21 +152,20 @@ def test_backward_kernels_stagewise_exact(cuda_device, B):
     hq, dlq = buf.h_bf[:B].cpu().double(), buf.dl_bf[:B, :10].cpu().double()
     assert rel_err(grads["fc2.weight"], dlq.t() @ hq) < 1e-5
     assert rel_err(grads["fc2.bias"], dlq.sum(0)) < 1e-5
-    # dgrad into the pooled map, masked by keep & (pooled > 0), scaled 4/3
+    # dgrad into the pooled map, masked by keep & (pooled > 0), scaled 4/3, routed to the argmax
     dp = dz1 @ q(d["fc1.weight"])
     keep_pos = ((pm & 12) == 12).double()
-    g_ref = q(dp * keep_pos / 0.75)
-    g = buf.g.cpu().double()
-    mism = (g != g_ref).double().mean().item()
-    assert mism < 1e-3 and rel_err(g, g_ref) < 1e-3, mism
-    # conv backward from the kernel's g, argmax and a1
-    arg = (pm & 3)
-    py = torch.arange(12).view(1, 1, 12, 1) * 2 + (arg.view(B, 64, 12, 12) >> 1)
-    px = torch.arange(12).view(1, 1, 1, 12) * 2 + (arg.view(B, 64, 12, 12) & 1)
-    dy = torch.zeros(B, 64, 24, 24, dtype=torch.float64)
+    g_ref = q(dp * keep_pos / 0.75).view(B, 64, 12, 12)
+    arg = (pm & 3).view(B, 64, 12, 12)
+    py = torch.arange(12).view(1, 1, 12, 1) * 2 + (arg >> 1)
+    px = torch.arange(12).view(1, 1, 1, 12) * 2 + (arg & 1)
+    dy_ref = torch.zeros(B, 64, 24, 24, dtype=torch.float64)
     bi = torch.arange(B).view(B, 1, 1, 1).expand(B, 64, 12, 12)
     ci = torch.arange(64).view(1, 64, 1, 1).expand(B, 64, 12, 12)
-    dy[bi, ci, py, px] = g.view(B, 64, 12, 12)
+    dy_ref[bi, ci, py, px] = g_ref
+    dy = buf.dy.cpu().double().permute(0, 3, 1, 2)          # NHWC -> NCHW
+    mism = (dy != dy_ref).double().mean().item()
+    assert mism < 1e-3 and rel_err(dy, dy_ref) < 1e-3, mism
     a1 = buf.a1.cpu().double().permute(0, 3, 1, 2)          # NHWC -> NCHW
     w2q = q(d["conv2.weight"])
     assert rel_err(grads["conv2.weight"], G.conv2d_weight(a1, w2q.shape, dy)) < 1e-4
