@@ -73,27 +73,40 @@ PYBIND11_MODULE(_C, m) {
   // ---------------- per-kernel entry points ----------------
   m.def("trunk_fwd", [](uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t w1c,
                         uintptr_t b1c, uintptr_t w2f, uintptr_t b2c, uintptr_t a1_out, uintptr_t p_out,
-                        uintptr_t pmask_out, int B, bool train, uintptr_t stream) {
+                        uintptr_t pmask_out, int B, bool train, uintptr_t stream, uintptr_t xin) {
     TrunkFwdArgs a{P<const uint8_t>(data_u8), P<const int32_t>(idx), idx_stride, P<const StepState>(state),
                    P<const float>(w1c), P<const float>(b1c), P<const uint16_t>(w2f), P<const float>(b2c),
-                   P<uint16_t>(a1_out), P<uint16_t>(p_out), P<uint8_t>(pmask_out)};
+                   P<uint16_t>(a1_out), P<uint16_t>(p_out), P<uint8_t>(pmask_out), P<const float>(xin)};
     launch_trunk_fwd(a, B, train, S(stream));
     check_launch();
-  });
+  }, py::arg("data_u8"), py::arg("idx"), py::arg("idx_stride"), py::arg("state"), py::arg("w1c"), py::arg("b1c"),
+     py::arg("w2f"), py::arg("b2c"), py::arg("a1_out"), py::arg("p_out"), py::arg("pmask_out"), py::arg("B"),
+     py::arg("train"), py::arg("stream"), py::arg("xin") = 0);
   m.def("fc1_fwd", [](uintptr_t p, uintptr_t w1, uintptr_t z1part, int B, uintptr_t stream) {
     launch_fc1_fwd(P<const uint16_t>(p), P<const uint16_t>(w1), P<float>(z1part), B, S(stream));
     check_launch();
   });
   m.def("head_train", [](uintptr_t z1part, uintptr_t b_fc1, uintptr_t w_fc2, uintptr_t b_fc2, uintptr_t labels,
                          uintptr_t idx, int64_t idx_stride, uintptr_t state, float inv_batch, uintptr_t loss_rows,
-                         uintptr_t dz1, uintptr_t h_bf, uintptr_t dl_bf, int B, int Bp, uintptr_t stream) {
+                         uintptr_t dz1, uintptr_t h_bf, uintptr_t dl_bf, int B, int Bp, uintptr_t stream,
+                         uintptr_t dlogp) {
     HeadArgs a{};
     a.z1part = P<const float>(z1part); a.b_fc1 = P<const float>(b_fc1); a.w_fc2 = P<const float>(w_fc2);
     a.b_fc2 = P<const float>(b_fc2); a.labels = P<const int32_t>(labels); a.idx = P<const int32_t>(idx);
     a.idx_step_stride = idx_stride; a.state = P<const StepState>(state); a.inv_batch = inv_batch;
     a.loss_rows = P<float>(loss_rows); a.dz1 = P<uint16_t>(dz1); a.h_bf = P<uint16_t>(h_bf);
-    a.dl_bf = P<uint16_t>(dl_bf);
+    a.dl_bf = P<uint16_t>(dl_bf); a.dlogp = P<const float>(dlogp);
     launch_head_train(a, B, Bp, S(stream));
+    check_launch();
+  }, py::arg("z1part"), py::arg("b_fc1"), py::arg("w_fc2"), py::arg("b_fc2"), py::arg("labels"), py::arg("idx"),
+     py::arg("idx_stride"), py::arg("state"), py::arg("inv_batch"), py::arg("loss_rows"), py::arg("dz1"),
+     py::arg("h_bf"), py::arg("dl_bf"), py::arg("B"), py::arg("Bp"), py::arg("stream"), py::arg("dlogp") = 0);
+  m.def("head_fwd", [](uintptr_t z1part, uintptr_t b_fc1, uintptr_t w_fc2, uintptr_t b_fc2, uintptr_t state,
+                       uintptr_t logp, int B, bool train, uintptr_t stream) {
+    HeadArgs a{};
+    a.z1part = P<const float>(z1part); a.b_fc1 = P<const float>(b_fc1); a.w_fc2 = P<const float>(w_fc2);
+    a.b_fc2 = P<const float>(b_fc2); a.state = P<const StepState>(state); a.logp_out = P<float>(logp);
+    launch_head_fwd(a, B, train, S(stream));
     check_launch();
   });
   m.def("head_eval", [](uintptr_t z1part, uintptr_t b_fc1, uintptr_t w_fc2, uintptr_t b_fc2, uintptr_t labels,
@@ -118,15 +131,18 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_bwd", [](uintptr_t dy, uintptr_t a1, uintptr_t w2d, uintptr_t w1c, uintptr_t b1c,
                        uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t c1part,
-                       uintptr_t w2part, uintptr_t grad, float grad_scale, int B, uintptr_t stream) {
+                       uintptr_t w2part, uintptr_t grad, float grad_scale, int B, uintptr_t stream,
+                       uintptr_t xin) {
     ConvBwdArgs a{P<const uint16_t>(dy), P<const uint16_t>(a1), P<const uint16_t>(w2d),
                   P<const float>(w1c), P<const float>(b1c), P<const uint8_t>(data_u8), P<const int32_t>(idx),
                   idx_stride, P<const StepState>(state), P<float>(c1part), P<float>(w2part), P<float>(grad),
-                  grad_scale, conv_wgrad_groups(B)};
+                  grad_scale, conv_wgrad_groups(B), P<const float>(xin)};
     launch_conv_bwd(a, B, S(stream));
     launch_conv_grad_reduce(a, B, S(stream));
     check_launch();
-  });
+  }, py::arg("dy"), py::arg("a1"), py::arg("w2d"), py::arg("w1c"), py::arg("b1c"), py::arg("data_u8"), py::arg("idx"),
+     py::arg("idx_stride"), py::arg("state"), py::arg("c1part"), py::arg("w2part"), py::arg("grad"),
+     py::arg("grad_scale"), py::arg("B"), py::arg("stream"), py::arg("xin") = 0);
   m.def("adadelta", [](uintptr_t param, uintptr_t grad, uintptr_t sq, uintptr_t acc, uintptr_t lr, float rho,
                        float eps, float wd, uintptr_t w2f, uintptr_t w2d, uintptr_t w1, uintptr_t w1t,
                        uintptr_t state_inc, int region, bool update, uintptr_t stream) {

@@ -20,6 +20,8 @@ struct TrunkFwdArgs {
   uint16_t* a1_out;           // bf16 [B][26][26][32]  (train only)
   uint16_t* p_out;            // bf16 [B][9216]
   uint8_t* pmask_out;         // u8   [B][9216]        (train only)
+  const float* xin;           // optional fp32 [B][784] already-normalised input (module API);
+                              // when set, data_u8/idx are ignored
 };
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
 
@@ -46,9 +48,12 @@ struct HeadArgs {
   // outputs (eval)
   float* logp_out;            // optional [B][10]
   int32_t* correct_out;       // [B] 1 if argmax == label
+  const float* dlogp;         // module API backward: upstream grad wrt log-probs [B][10] (replaces NLL)
 };
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s);
 void launch_head_eval(const HeadArgs& a, int B, hipStream_t s);
+// module API forward: log-probs with (train) or without (eval) dropout-2
+void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
 
 // ---------------- backward ----------------
 struct FcBwdArgs {
@@ -83,6 +88,7 @@ struct ConvBwdArgs {
   float* grad;                // flat fp32 grad buffer (conv params written by the reduce kernel)
   float grad_scale;
   int wgrad_groups;           // G
+  const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
 };
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad

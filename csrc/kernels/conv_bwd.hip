@@ -80,11 +80,19 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
     const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
 #pragma unroll
     for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
-    const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
-    const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG);
-    for (int e = tid; e < DG_TROWS * IMG; e += 256) {
-      const int row = r0 + e / IMG;
-      xs[e] = (row < IMG) ? normalize_u8(src8[r0 * IMG + e]) : 0.0f;
+    if (a.xin) {
+      const float* srcf = a.xin + (int64_t)b * (IMG * IMG);
+      for (int e = tid; e < DG_TROWS * IMG; e += 256) {
+        const int row = r0 + e / IMG;
+        xs[e] = (row < IMG) ? srcf[r0 * IMG + e] : 0.0f;
+      }
+    } else {
+      const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
+      const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG);
+      for (int e = tid; e < DG_TROWS * IMG; e += 256) {
+        const int row = r0 + e / IMG;
+        xs[e] = (row < IMG) ? normalize_u8(src8[r0 * IMG + e]) : 0.0f;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

@@ -131,14 +131,23 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   head_forward_row(a, B, b, lane, true, no_drop, seed, off, r);
   float lp[NCLS];
   log_softmax10(r.logit, lp);
-  const int y = a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
-  if (lane == 0) a.loss_rows[b] = -lp[y];
-  // nll(mean) backward: go[c] = -[c==y]/B; log_softmax backward: go - exp(lp) * sum(go)
   float dl[NCLS];
+  if (a.dlogp) {
+    // module API: generic log_softmax backward  dl = go - exp(lp) * sum(go)
+    float go[NCLS], sg = 0.f;
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) {
-    const float go = (c == y) ? -a.inv_batch : 0.0f;
-    dl[c] = go - expf(lp[c]) * (-a.inv_batch);
+    for (int c = 0; c < NCLS; ++c) { go[c] = a.dlogp[(int64_t)b * NCLS + c]; sg += go[c]; }
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) dl[c] = go[c] - expf(lp[c]) * sg;
+  } else {
+    const int y = a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
+    if (lane == 0) a.loss_rows[b] = -lp[y];
+    // nll(mean) backward: go[c] = -[c==y]/B; log_softmax backward: go - exp(lp) * sum(go)
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) {
+      const float go = (c == y) ? -a.inv_batch : 0.0f;
+      dl[c] = go - expf(lp[c]) * (-a.inv_batch);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -180,6 +189,30 @@ __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
     for (int c = 1; c < NCLS; ++c) v = (lane == c) ? lp[c] : v;
     a.logp_out[(int64_t)b * NCLS + lane] = v;
   }
+}
+
+// module API forward: log-probs (train: with dropout-2 drawn from StepState exactly as head_train does)
+__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, int B, int train) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const bool no_drop = !train || (a.state->flags & STEP_FLAG_NO_DROPOUT) != 0;
+  const uint64_t seed = a.state ? a.state->seed : 0;
+  const uint64_t off = a.state ? a.state->rng_base + 2ull * (uint64_t)a.state->step + 1ull : 0;
+  HeadRow r;
+  head_forward_row(a, B, b, lane, train != 0, no_drop, seed, off, r);
+  float lp[NCLS];
+  log_softmax10(r.logit, lp);
+  if (lane < NCLS) {
+    float v = lp[0];
+#pragma unroll
+    for (int c = 1; c < NCLS; ++c) v = (lane == c) ? lp[c] : v;
+    a.logp_out[(int64_t)b * NCLS + lane] = v;
+  }
+}
+
+void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B, train ? 1 : 0);
 }
 
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {

@@ -74,11 +74,17 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
     const float4 b0 = b1v[0], b1 = b1v[1];
     bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
     bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
-    const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
     uint4 xv = {0u, 0u, 0u, 0u};
+    float4 xf = {0.f, 0.f, 0.f, 0.f};
     constexpr int XCH = X_ROWS * IMG / 16;       // 21 16-byte chunks (image rows are 16-B aligned)
-    if (tid < XCH)
-      xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
+    if (a.xin) {                                  // module API: fp32 input rows (84 float4)
+      if (tid < X_ROWS * IMG / 4)
+        xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + strip * STRIP * IMG + tid * 4);
+    } else {
+      const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
+      if (tid < XCH)
+        xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
+    }
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int ch = tid + 256 * i;                // 2304 chunks of 16 B
@@ -86,7 +92,9 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
       const int n = row / 9;
       *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = wv[i];
     }
-    if (tid < XCH) {
+    if (a.xin) {
+      if (tid < X_ROWS * IMG / 4) *reinterpret_cast<float4*>(xs + tid * 4) = xf;
+    } else if (tid < XCH) {
       const uint32_t words[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {

@@ -94,7 +94,7 @@ void Engine::enqueue_step(int batch) {
   const float gscale = 1.0f / (float)world_;
 
   TrunkFwdArgs tf{buf_.train_u8, buf_.train_idx, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
-                  buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_};
+                  buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
   launch_trunk_fwd(tf, B, true, compute_);
   launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
@@ -109,7 +109,7 @@ void Engine::enqueue_step(int batch) {
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
-  const bool dist = comm_ && world_ > 1;
+  const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
   // serial mode keeps every kernel of the optimizer / wgrad branches on the compute stream
   hipStream_t ws = concurrent_ ? wgrad_stream_ : compute_;
   hipStream_t ms = (concurrent_ || dist) ? comm_stream_ : compute_;
@@ -125,7 +125,7 @@ void Engine::enqueue_step(int batch) {
   }
   ConvBwdArgs cb{dy_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
                  buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
-                 conv_wgrad_groups(B)};
+                 conv_wgrad_groups(B), nullptr};
   launch_conv_wgrad(cb, B, ws);
   if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
   launch_conv_dgrad(cb, B, compute_);
@@ -187,7 +187,7 @@ void Engine::enqueue_eval(int n_total, int batch) {
   for (int s = 0; s < n_total; s += batch) {
     const int B = (n_total - s) < batch ? (n_total - s) : batch;
     TrunkFwdArgs tf{buf_.test_u8, buf_.test_idx + s, 0, nullptr, P + OFF_CONV1_W, P + OFF_CONV1_B,
-                    buf_.w2f, P + OFF_CONV2_B, nullptr, p_, nullptr};
+                    buf_.w2f, P + OFF_CONV2_B, nullptr, p_, nullptr, nullptr};
     launch_trunk_fwd(tf, B, false, compute_);
     launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
     HeadArgs ha{};

@@ -10,6 +10,7 @@ behaviour):
 * ``--synthetic`` / ``--data-root`` / ``--synthetic-train-size`` /
   ``--synthetic-test-size``: offline data selection.
 * ``--bucket-cap-mb`` / ``--first-bucket-mb``: DDP gradient bucket sizing.
+* ``--engine {fused,module}``: native step engine vs the reference's module-level loop.
 * ``--graph-steps``: training steps captured per HIP graph (0 = eager launches).
 * ``--profile``: roctx ranges + per-epoch device timing; ``--json-log``: machine
   readable per-epoch metrics.
@@ -50,6 +51,9 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='use deterministic synthetic 28x28 data (auto when MNIST files are absent)')
     g.add_argument('--synthetic-train-size', type=int, default=None)
     g.add_argument('--synthetic-test-size', type=int, default=None)
+    g.add_argument('--engine', choices=['fused', 'module'], default=None,
+                   help='fused: native step engine (GPU default); module: the reference loop over '
+                        'Net/DDP/Adadelta (always used with --no-cuda)')
     g.add_argument('--graph-steps', type=int, default=None,
                    help='training steps per captured HIP graph (default: log-interval; 0 = eager)')
     g.add_argument('--bucket-cap-mb', type=float, default=25.0,

@@ -1,0 +1,221 @@
+"""Application drivers: the reference's ``main()`` of mnist.py (mnist.py:73-133) and mnist_ddp.py
+(mnist_ddp.py:108-197) on the MI355X framework.
+
+Two execution engines, same flags / log lines / checkpoints / RNG consumption:
+
+* ``fused`` (default on GPU): the native step engine - HBM-resident data, 8 hand-written kernels
+  per step captured in hipGraphs, DDP gradient buckets all-reduced over RCCL from C++.
+* ``module``: the reference's literal loop (``model(data)``, ``F.nll_loss``, ``loss.backward()``,
+  ``optimizer.step()``) over :class:`~pytorch_mnist_ddp_amd.models.Net` (fused kernels via autograd
+  on GPU, torch ops on CPU), :class:`~pytorch_mnist_ddp_amd.parallel.DistributedDataParallel`
+  hooks and :class:`~pytorch_mnist_ddp_amd.optim.Adadelta`.  Always used for ``--no-cuda``.
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+from . import cli
+from .data import (DistributedIndexStream, HostLoader, RandomIndexStream, SequentialIndexStream,
+                   consume_loader_base_seed, load_mnist, num_batches)
+from .models.net import Net
+from .optim import Adadelta, StepLR
+from .utils.checkpoint import load_state_dict, save_state_dict
+from .utils.logging import test_line, total_time_line, train_line
+
+
+def _json_log(path, rec):
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
+# ----------------------------------------------------------------------------- module engine
+def _train_module(args, model, device, loader, optimizer, epoch, distributed, world, rank):
+    model.train()
+    n_batches = len(loader)
+    for batch_idx, (data, target) in enumerate(loader):
+        data, target = data.to(device), target.to(device)
+        optimizer.zero_grad()
+        output = model(data)
+        loss = F.nll_loss(output, target)
+        loss.backward()
+        optimizer.step()
+        if batch_idx % args.log_interval == 0 and (not distributed or rank == 0):
+            seen = (world if distributed else 1) * batch_idx * len(data)
+            print(train_line(epoch, seen, len(loader.dataset), batch_idx, n_batches, loss.item()))
+            if args.dry_run and not getattr(args, "_ddp_script", False):
+                break
+        if args.dry_run and getattr(args, "_ddp_script", False):
+            break
+
+
+def _test_module(model, device, loader):
+    model.eval()
+    test_loss, correct = 0.0, 0
+    with torch.no_grad():
+        for data, target in loader:
+            data, target = data.to(device), target.to(device)
+            output = model(data)
+            test_loss += F.nll_loss(output, target, reduction='sum').item()
+            pred = output.argmax(dim=1, keepdim=True)
+            correct += pred.eq(target.view_as(pred)).sum().item()
+    n = len(loader.dataset)
+    test_loss /= n
+    print(test_line(test_loss, correct, n))
+    return test_loss, correct
+
+
+# ----------------------------------------------------------------------------- main flows
+def run(argv=None, ddp_script: bool = True) -> int:
+    args = cli.parse_args(ddp=ddp_script, argv=argv)
+    args._ddp_script = ddp_script
+    use_cuda = not args.no_cuda and torch.cuda.is_available()
+    distributed, world, rank, gpu = False, 1, 0, 0
+    if ddp_script:
+        from .parallel.distributed import init_distributed_mode
+        init_distributed_mode(args)
+        distributed = args.distributed
+        if distributed:
+            world, rank, gpu = args.world_size, args.rank, args.gpu
+    torch.manual_seed(args.seed)
+    device = torch.device(f"cuda:{gpu}" if use_cuda else "cpu") if ddp_script else \
+        torch.device("cuda" if use_cuda else "cpu")
+
+    train_data = load_mnist(args.data_root, True, args.synthetic, args.synthetic_train_size, verbose=rank == 0)
+    test_data = load_mnist(args.data_root, False, args.synthetic, args.synthetic_test_size, verbose=rank == 0)
+    if ddp_script:
+        train_stream = (DistributedIndexStream(len(train_data), world, rank, shuffle=True) if distributed
+                        else RandomIndexStream(len(train_data)))
+        test_stream = SequentialIndexStream(len(test_data))
+    else:  # mnist.py: shuffle=True for both loaders only on CUDA (mnist.py:103-110)
+        train_stream = RandomIndexStream(len(train_data)) if use_cuda else SequentialIndexStream(len(train_data))
+        test_stream = RandomIndexStream(len(test_data)) if use_cuda else SequentialIndexStream(len(test_data))
+
+    model = Net()
+    engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
+    if not use_cuda:
+        engine = "module"
+    if args.resume:
+        load_state_dict(model, args.resume, map_location="cpu")
+
+    if engine == "fused":
+        _run_fused(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world,
+                   rank, gpu, ddp_script)
+    else:
+        _run_module(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world,
+                    rank, gpu, ddp_script)
+    return 0
+
+
+def _run_module(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world, rank,
+                gpu, ddp_script):
+    model = model.to(device)
+    model_without_ddp = model
+    if distributed:
+        from .parallel.ddp import DistributedDataParallel
+        model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None,
+                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
+        model_without_ddp = model.module
+    optimizer = Adadelta(model.parameters(), lr=args.lr)
+    scheduler = StepLR(optimizer, step_size=1, gamma=args.gamma)
+    train_loader = HostLoader(train_data, train_stream, args.batch_size)
+    test_loader = HostLoader(test_data, test_stream, args.test_batch_size)
+    for epoch in range(1, args.epochs + 1):
+        if distributed:
+            train_stream.set_epoch(epoch)
+        t0 = time.perf_counter()
+        _train_module(args, model, device, train_loader, optimizer, epoch, distributed, world, rank)
+        rec = {"epoch": epoch, "train_s": time.perf_counter() - t0}
+        if not distributed or rank == 0:
+            rec["test_loss"], rec["correct"] = _test_module(model_without_ddp, device, test_loader)
+        _json_log(args.json_log, rec)
+        scheduler.step()
+    _save(args, model, distributed, rank, ddp_script)
+
+
+def _run_fused(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world, rank,
+               gpu, ddp_script):
+    from .engine.state import ModelState
+    from .engine.trainer import FusedTrainer
+    from .utils.profiling import roctx_range
+    ms = ModelState(model, device, lr=args.lr)
+    model_for_save = model
+    comm = None
+    if distributed:
+        from .parallel.ddp import DistributedDataParallel
+        from .parallel.distributed import create_rccl_comm
+        ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
+                                      bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
+        model_for_save = ddp
+        comm = create_rccl_comm(world, rank, gpu)
+    optimizer = Adadelta(model.parameters(), lr=args.lr, model_state=ms)
+    scheduler = StepLR(optimizer, step_size=1, gamma=args.gamma)
+    graph_steps = args.log_interval if args.graph_steps is None else args.graph_steps
+    trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
+                           args.batch_size, args.test_batch_size, num_samples=len(train_stream),
+                           world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps)
+    trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper
+    n_train = len(train_data)
+    n_batches = num_batches(len(train_stream), args.batch_size)
+    log_rank = (not distributed) or rank == 0
+    for epoch in range(1, args.epochs + 1):
+        if distributed:
+            train_stream.set_epoch(epoch)
+        consume_loader_base_seed()          # iter(train_loader)
+        idx = train_stream.epoch_indices()
+        trainer.set_lr(optimizer.param_groups[0]["lr"])
+
+        def log_fn(batch_idx, blen, loss, epoch=epoch):
+            seen = (world if distributed else 1) * batch_idx * blen
+            print(train_line(epoch, seen, n_train, batch_idx, n_batches, loss), flush=False)
+
+        with roctx_range(f"train_epoch_{epoch}", args.profile):
+            st = trainer.train_epoch(epoch, idx, args.log_interval,
+                                     dry_run=args.dry_run, log_fn=log_fn if log_rank else None)
+        rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
+               "img_per_s": st.samples / max(st.train_seconds, 1e-9)}
+        if log_rank:
+            consume_loader_base_seed()      # iter(test_loader)
+            if isinstance(test_stream, RandomIndexStream):
+                test_stream.epoch_indices()  # mnist.py CUDA path shuffles the test set: same RNG draw
+            with roctx_range(f"eval_epoch_{epoch}", args.profile):
+                loss_sum, correct, n = trainer.evaluate()
+            print(test_line(loss_sum / n, correct, n))
+            rec.update(test_loss=loss_sum / n, correct=correct)
+        _json_log(args.json_log, rec)
+        for p in optimizer.param_groups[0]["params"]:      # keep torch-format optimizer bookkeeping
+            st_ = optimizer.state[p]
+            if "step" in st_:
+                st_["step"] += st.steps
+        scheduler.step()
+    trainer.synchronize()
+    _save(args, model_for_save, distributed, rank, ddp_script)
+
+
+def _save(args, model, distributed, rank, ddp_script):
+    if not args.save_model:
+        return
+    if not ddp_script:
+        save_state_dict(model, "mnist_cnn.pt")
+    elif distributed:
+        if rank == 0:
+            save_state_dict(model, "mnist_cnn.pt")
+    else:
+        save_state_dict(model, "mnist_cnn_.pt")
+
+
+def main_mnist(argv=None) -> int:
+    return run(argv, ddp_script=False)
+
+
+def main_mnist_ddp(argv=None) -> int:
+    start = time.time()
+    rc = run(argv, ddp_script=True)
+    print(total_time_line(time.time() - start))
+    sys.stdout.flush()
+    return rc

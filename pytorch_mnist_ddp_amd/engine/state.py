@@ -64,6 +64,7 @@ class ModelState:
                 view.copy_(p.detach().to(self.device, torch.float32))
                 p.data = view
                 p.grad = self.grad[off:off + p.numel()].view(p.shape)
+                p._amd_model_state = self     # lets the fused Adadelta find the flat buffers
         self.refresh_shadows()
 
     def refresh_shadows(self, stream: torch.cuda.Stream | None = None) -> None:

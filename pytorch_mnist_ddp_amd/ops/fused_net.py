@@ -1,0 +1,138 @@
+"""Module-level GPU path: ``Net.forward(x)`` on a CUDA/ROCm tensor runs the fused MI355X kernels.
+
+This is the reference's programming model (mnist_ddp.py:65-73: ``output = model(data);
+loss = F.nll_loss(output, target); loss.backward(); optimizer.step()``) on the hand-written
+kernels, with autograd.  One ``torch.autograd.Function`` covers the whole network:
+
+forward  = trunk_fwd (conv1 -> conv2 MFMA -> ReLU -> max-pool -> dropout-1) -> fc1 split-K MFMA
+           -> head_fwd (bias -> ReLU -> dropout-2 -> fc2 -> log_softmax)
+backward = head_train (generic log_softmax backward from dlogp) -> fc_bwd -> conv_bwd
+
+Dropout masks come from the same counter-based Philox stream as the engine: the forward draws
+a fresh (seed, offset) pair per call and the backward replays exactly that pair, so masks are
+consistent without being stored (dropout-1's keep bits are in the saved pmask anyway).
+
+The module's parameters are re-pointed at a flat device buffer (``engine.state.ModelState``) on
+the first GPU forward; the bf16 shadow copies the kernels read are refreshed lazily whenever any
+parameter's version counter moved (an optimizer step, ``load_state_dict``, manual edits), so any
+optimizer - ours or stock torch - can drive it.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import native
+from .functional import StepBuffers, round_up
+
+_SEED_MIX = 0x9E3779B97F4A7C15
+
+
+class _FusedState:
+    def __init__(self, net, device):
+        from ..engine.state import ModelState
+        self.ms = ModelState(net, device)
+        self.params = list(net.parameters())
+        self.versions = self._snapshot()
+        self.rng_offset = 0
+        self.seed = (torch.initial_seed() * _SEED_MIX) & 0xFFFFFFFFFFFFFFFF
+
+    def _snapshot(self):
+        return tuple((p._version, p.data_ptr()) for p in self.params)
+
+    def sync(self):
+        snap = self._snapshot()
+        if snap != self.versions:
+            ptrs = tuple(self.ms.views(self.ms.param)[n].data_ptr()
+                         for n, _ in self.ms.module.named_parameters())
+            if tuple(s[1] for s in snap) != ptrs:      # parameters were re-assigned: re-bind
+                self.ms.bind(self.ms.module)
+            else:
+                self.ms.refresh_shadows()
+            self.versions = self._snapshot()
+
+
+def fused_state(net) -> _FusedState:
+    st = getattr(net, "_amd_fused_state", None)
+    dev = next(net.parameters()).device
+    if st is None or st.ms.device != dev:
+        st = _FusedState(net, dev)
+        object.__setattr__(net, "_amd_fused_state", st)
+    return st
+
+
+def _dropout_flags(net) -> int:
+    p1, p2 = net.dropout1.p, net.dropout2.p
+    if (p1, p2) == (0.25, 0.5):
+        return 0
+    if (p1, p2) == (0.0, 0.0):
+        return 1                                   # STEP_FLAG_NO_DROPOUT
+    raise NotImplementedError(f"fused GPU Net supports dropout (0.25, 0.5) or (0, 0), got ({p1}, {p2})")
+
+
+def _step_state(st: _FusedState, training: bool, device, flags: int = 0) -> torch.Tensor:
+    t = torch.zeros(3, dtype=torch.int64)
+    t[0] = (flags & 0xFFFFFFFF) << 32
+    if training:
+        t[1] = st.seed - (1 << 64) if st.seed >= (1 << 63) else st.seed
+        t[2] = st.rng_offset
+        st.rng_offset += 2
+    return t.to(device, non_blocking=True)
+
+
+class FusedNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, st, training, flags, *params):
+        C = native.load()
+        ms = st.ms
+        p, o = native.ptr, ms.offsets
+        x = x.reshape(x.shape[0], -1).to(torch.float32).contiguous()
+        if x.shape[1] != 784:
+            raise ValueError(f"Net expects [B,1,28,28] inputs, got {tuple(x.shape)}")
+        B = x.shape[0]
+        buf = StepBuffers.allocate(B, x.device)
+        state = _step_state(st, training, x.device, flags)
+        s = native.stream_handle()
+        P = p(ms.param)
+        C.trunk_fwd(0, 0, 0, p(state), P + 4 * o["conv1.weight"], P + 4 * o["conv1.bias"], p(ms.w2f),
+                    P + 4 * o["conv2.bias"], p(buf.a1) if training else 0, p(buf.p),
+                    p(buf.pmask) if training else 0, B, bool(training), s, xin=p(x))
+        C.fc1_fwd(p(buf.p), p(ms.w1), p(buf.z1part), B, s)
+        logp = torch.empty(B, 10, dtype=torch.float32, device=x.device)
+        C.head_fwd(p(buf.z1part), P + 4 * o["fc1.bias"], P + 4 * o["fc2.weight"], P + 4 * o["fc2.bias"],
+                   p(state), p(logp), B, bool(training), s)
+        ctx.training = bool(training)
+        ctx.st = st
+        ctx.buf = buf
+        ctx.save_for_backward(x, state)
+        return logp
+
+    @staticmethod
+    def backward(ctx, dlogp):
+        if not ctx.training:
+            raise RuntimeError("fused Net backward requires model.train() mode during forward")
+        C = native.load()
+        x, state = ctx.saved_tensors
+        st, buf = ctx.st, ctx.buf
+        ms = st.ms
+        p, o = native.ptr, ms.offsets
+        B = buf.B
+        s = native.stream_handle()
+        P = p(ms.param)
+        dlogp = dlogp.to(torch.float32).contiguous()
+        grad = torch.empty_like(ms.grad)
+        C.head_train(p(buf.z1part), P + 4 * o["fc1.bias"], P + 4 * o["fc2.weight"], P + 4 * o["fc2.bias"],
+                     0, 0, 0, p(state), 1.0 / B, p(buf.loss_rows), p(buf.dz1), p(buf.h_bf), p(buf.dl_bf),
+                     B, round_up(B, 32), s, dlogp=p(dlogp))
+        C.fc_bwd(p(buf.dz1), p(buf.p), p(buf.pmask), p(ms.w1t), p(buf.h_bf), p(buf.dl_bf), p(buf.loss_rows),
+                 p(state), p(grad), p(buf.dy), 0, 1.0, 1.0 / B, B, round_up(B, 32), s)
+        C.conv_bwd(p(buf.dy), p(buf.a1), p(ms.w2d), P + 4 * o["conv1.weight"], P + 4 * o["conv1.bias"],
+                   0, 0, 0, p(state), p(buf.c1part), p(buf.w2part), p(grad), 1.0, B, s, xin=p(x))
+        views = [grad[o[n]:o[n] + t.numel()].view(t.shape) for n, t in ms.module.named_parameters()]
+        return (None, None, None, None, *views)
+
+
+def fused_net_forward(net, x: torch.Tensor) -> torch.Tensor:
+    st = fused_state(net)
+    st.sync()
+    flags = _dropout_flags(net) if net.training else 0
+    return FusedNetFunction.apply(x, st, net.training, flags, *st.params)

@@ -1,0 +1,147 @@
+"""GPU: the reference programming model on the fused kernels (Net + autograd + Adadelta + DDP)."""
+import copy
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_mnist_ddp_amd.models.net import Net
+from pytorch_mnist_ddp_amd.optim import Adadelta, StepLR
+
+from refmodel import rel_err
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _data(B, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    from pytorch_mnist_ddp_amd.data.synthetic import generate
+    from pytorch_mnist_ddp_amd.data.datasets import normalize_u8
+    imgs, lab = generate(B, seed=seed + 3)
+    return normalize_u8(imgs).to(dev), lab.to(dev)
+
+
+def test_module_forward_backward_matches_cpu_reference(cuda_device):
+    torch.manual_seed(1)
+    net = Net()
+    ref = copy.deepcopy(net)
+    net = net.to(cuda_device)
+    for m in (net, ref):
+        m.dropout1.p = m.dropout2.p = 0.0
+    x, y = _data(64, cuda_device)
+    net.eval()
+    with torch.no_grad():
+        lp = net(x)
+    ref.eval()
+    lp_ref = ref(x.cpu())
+    assert rel_err(lp.cpu(), lp_ref) < 1e-2
+    net.train(), ref.train()
+    F.nll_loss(net(x), y).backward()
+    F.nll_loss(ref(x.cpu()), y.cpu()).backward()
+    for (n, a), b in zip(net.named_parameters(), ref.parameters()):
+        assert rel_err(a.grad.cpu(), b.grad) < 0.1, n
+
+
+def test_module_training_loop_converges_and_checkpoints(cuda_device, tmp_path):
+    torch.manual_seed(1)
+    net = Net().to(cuda_device)
+    opt = Adadelta(net.parameters(), lr=1.0)
+    sched = StepLR(opt, step_size=1, gamma=0.7)
+    x, y = _data(512, cuda_device, seed=1)
+    losses = []
+    for epoch in range(3):
+        for i in range(0, 512, 64):
+            opt.zero_grad()
+            loss = F.nll_loss(net(x[i:i + 64]), y[i:i + 64])
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        sched.step()
+    assert losses[-1] < 0.5 * losses[0]
+    sd = opt.state_dict()
+    assert len(sd["state"]) == 8 and "square_avg" in sd["state"][0]
+    torch.save(net.state_dict(), tmp_path / "m.pt")
+    cpu = Net()
+    cpu.load_state_dict(torch.load(tmp_path / "m.pt", weights_only=True, map_location="cpu"))
+    net.eval(), cpu.eval()
+    with torch.no_grad():
+        assert rel_err(net(x[:32]).cpu(), cpu(x[:32].cpu())) < 2e-2
+
+
+def test_module_path_with_stock_torch_optimizer(cuda_device):
+    torch.manual_seed(2)
+    net = Net().to(cuda_device)
+    opt = torch.optim.SGD(net.parameters(), lr=0.05)
+    x, y = _data(128, cuda_device, seed=2)
+    first = None
+    for _ in range(20):
+        opt.zero_grad()
+        loss = F.nll_loss(net(x), y)
+        loss.backward()
+        opt.step()                       # in-place param update: fused shadows refresh lazily
+        first = first if first is not None else loss.item()
+    assert loss.item() < first
+
+
+def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
+    """world_size=1 process group: DDP wrapper hooks (nccl) + engine's RCCL-overlapped schedule."""
+    import socket
+    import torch.distributed as dist
+    from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+    from pytorch_mnist_ddp_amd.engine.state import ModelState
+    from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+    from pytorch_mnist_ddp_amd.ops import native
+    from pytorch_mnist_ddp_amd.parallel.ddp import DistributedDataParallel
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=cuda_device)
+    try:
+        torch.manual_seed(3)
+        net = Net().to(cuda_device)
+        ddp = DistributedDataParallel(net, device_ids=[0])
+        x, y = _data(64, cuda_device, seed=4)
+        F.nll_loss(ddp(x), y).backward()
+        assert [c[0] for c in ddp.reducer.calls] == [0, 1]
+        assert list(ddp.state_dict())[0] == "module.conv1.weight"
+        # engine with an attached RCCL communicator: fc bucket all-reduce + Adadelta on the comm
+        # stream overlapped with the conv backward, captured into graphs; must equal no-comm run
+        C = native.load()
+        comm = C.RcclComm(C.RcclComm.unique_id(), 1, 0, 0)
+        tr = load_mnist(synthetic_data=True, train=True, synthetic_size=1024, verbose=False)
+        idx = torch.randperm(1024, generator=torch.Generator().manual_seed(0))
+        res = []
+        for c in (comm, None):
+            torch.manual_seed(5)
+            ms = ModelState(Net(), cuda_device)
+            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=4)
+            t.train_epoch(1, idx)
+            t.synchronize()
+            res.append(ms.param.clone())
+        assert torch.equal(res[0], res[1])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scripts_on_gpu(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    common = ["--epochs", "2", "--batch-size", "200", "--synthetic", "--synthetic-train-size", "4000",
+              "--synthetic-test-size", "1000", "--save-model"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "mnist_ddp.py"), *common], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout
+    assert "Not using distributed mode" in out and out.count("Test set: Average loss:") == 2
+    assert "Train Epoch: 2 [2000/4000 (50%)]" in out and "Total cost time:" in out
+    sd = torch.load(os.path.join(tmp_path, "mnist_cnn_.pt"), weights_only=True)
+    assert sd["fc1.weight"].is_cuda and sd["fc1.weight"].dtype == torch.float32
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "mnist.py"), *common, "--engine", "module", "--dry-run"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("Train Epoch:") == 2 and os.path.exists(os.path.join(tmp_path, "mnist_cnn.pt"))
