@@ -59,6 +59,8 @@ def main() -> int:
     ap.add_argument("--no-full-run", dest="full_run", action="store_false")
     ap.add_argument("--epochs", type=int, default=EPOCHS, help="epochs for the full-run wallclock")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--force-comm", action="store_true",
+                    help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -71,7 +73,8 @@ def main() -> int:
             return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
+    if use_pg:
         dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank, device_id=dev)
     t_setup = time.perf_counter()
 
@@ -85,7 +88,7 @@ def main() -> int:
     steps_per_epoch = math.ceil(len(sampler) / B)
     num_samples = max(total * B, steps_per_epoch * B)
     ms = ModelState(net, dev, lr=1.0)
-    comm = create_rccl_comm(world, rank, local) if world > 1 else None
+    comm = create_rccl_comm(world, rank, local) if use_pg else None
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
                       two_buckets=not args.single_bucket)
@@ -107,18 +110,18 @@ def main() -> int:
         tr.synchronize()
     tr.run_steps(args.warmup)
     tr.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tr.run_steps(args.steps)
     tr.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if use_pg:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -137,7 +140,7 @@ def main() -> int:
                            two_buckets=not args.single_bucket)
         if comm is not None:
             tr2.engine.broadcast_params(0)
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
         w0 = time.perf_counter()
@@ -149,11 +152,11 @@ def main() -> int:
                 ls, correct, n = tr2.evaluate()
                 acc = correct / max(1, n)
         tr2.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         w1 = time.perf_counter()
         wall = w1 - w0
-        if world > 1:
+        if use_pg:
             t = torch.tensor([wall], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             wall = float(t.item())
@@ -186,7 +189,7 @@ def main() -> int:
             "setup_s": round(t0 - t_setup, 2),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     return 0

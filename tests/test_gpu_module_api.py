@@ -145,3 +145,26 @@ def test_scripts_on_gpu(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.count("Train Epoch:") == 2 and os.path.exists(os.path.join(tmp_path, "mnist_cnn.pt"))
+
+
+def test_torchrun_ddp_paths_on_one_gpu(tmp_path):
+    """torchrun world_size=1: env rendezvous, c10d-store RCCL unique-id exchange, engine broadcast,
+    comm-attached graphs (fused engine) and hook-driven buckets (module engine)."""
+    import socket
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for engine in ("fused", "module"):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "mnist_ddp.py"),
+               "--epochs", "1", "--batch-size", "200", "--synthetic", "--synthetic-train-size", "2000",
+               "--synthetic-test-size", "1000", "--save-model", "--engine", engine]
+        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "| distributed init (rank 0): env://, local rank:0, world size:1" in r.stdout
+        assert "Test set: Average loss:" in r.stdout
+        sd = torch.load(os.path.join(tmp_path, "mnist_cnn.pt"), weights_only=True)
+        assert list(sd)[0] == "module.conv1.weight"
+        os.remove(os.path.join(tmp_path, "mnist_cnn.pt"))
