@@ -110,6 +110,30 @@ void Engine::enqueue_step(int batch) {
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
   const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
+  ConvBwdArgs cb{dy_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
+                 buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
+                 conv_wgrad_groups(B), nullptr};
+  AdadeltaArgs adc = ad;
+  adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
+  if (dist && two_buckets_ && !concurrent_ && dist_sched_ == 1) {
+    // Every cross-queue edge costs ~5-10 us of signal latency, so the critical path (conv backward,
+    // conv bucket, conv update) never leaves the compute queue; only the fc bucket (98.4 % of the
+    // bytes) forks onto the comm stream, and the join is on an edge that has long completed.
+    // (capture order matters: the graph executor keeps a fork's first-captured child on the
+    // launching queue, so conv2 wgrad is enqueued before the comm branch)
+    HIP_OK(hipEventRecord(ev_fc_, compute_));
+    launch_conv_wgrad(cb, B, compute_);
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    launch_conv_dgrad(cb, B, compute_);
+    launch_conv_grad_reduce(cb, B, compute_);
+    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));   // also orders the two all-reduces
+    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+    launch_adadelta(adc, ADA_CONV, compute_);
+    return;
+  }
   // serial mode keeps every kernel of the optimizer / wgrad branches on the compute stream
   hipStream_t ws = concurrent_ ? wgrad_stream_ : compute_;
   hipStream_t ms = (concurrent_ || dist) ? comm_stream_ : compute_;
@@ -123,9 +147,6 @@ void Engine::enqueue_step(int batch) {
     if (dist) comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, ms);
     launch_adadelta(ad, ADA_FC, ms);
   }
-  ConvBwdArgs cb{dy_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
-                 buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
-                 conv_wgrad_groups(B), nullptr};
   launch_conv_wgrad(cb, B, ws);
   if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
   launch_conv_dgrad(cb, B, compute_);
@@ -133,8 +154,6 @@ void Engine::enqueue_step(int batch) {
   launch_conv_grad_reduce(cb, B, compute_);
   HIP_OK(hipEventRecord(ev_conv_, compute_));
   if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_conv_, 0));
-  AdadeltaArgs adc = ad;
-  adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
   if (one_update) {
     launch_adadelta(adc, ADA_ALL, ms);
   } else if (dist && !two_buckets_) {

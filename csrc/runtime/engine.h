@@ -59,7 +59,10 @@ class Engine {
 
   void attach_comm(std::shared_ptr<RcclComm> comm);   // enables the overlapped DDP path
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
-  void set_concurrent(bool on) { concurrent_ = on; }   // parallel graph branches (wgrad || dgrad, fc optimizer || conv bwd)
+  void set_concurrent(bool on) { concurrent_ = on; }
+  // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
+  // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute
+  void set_dist_schedule(int s) { dist_sched_ = s; }   // parallel graph branches (wgrad || dgrad, fc optimizer || conv bwd)
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -92,6 +95,7 @@ class Engine {
   bool two_buckets_ = true;
   int idx_stride_ = 0;
   bool concurrent_ = false;
+  int dist_sched_ = 1;
   std::shared_ptr<RcclComm> comm_;
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;
   hipStream_t wgrad_stream_ = nullptr;

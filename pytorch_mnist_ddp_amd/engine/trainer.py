@@ -85,6 +85,7 @@ class FusedTrainer:
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
+        self.engine.set_dist_schedule(int(os.environ.get("MNIST_AMD_DIST_SCHED", "1")))
         if comm is not None:
             self.engine.attach_comm(comm)
         self.comm = comm
