@@ -69,10 +69,14 @@ __device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c
   u32x4 r = {c0, c1, c2, c3};
   return r;
 }
-// Random words for elements [4*quad, 4*quad+4) of one dropout invocation (counter = offset).
-__device__ __forceinline__ u32x4 dropout_words(uint64_t seed, uint64_t offset, uint64_t quad) {
-  return philox4x32((uint32_t)quad, (uint32_t)(quad >> 32), (uint32_t)offset,
+// Random bytes for elements [16*blk, 16*blk+16) of one dropout invocation (counter = offset):
+// element k of the block uses byte (k & 3) of word (k >> 2).
+__device__ __forceinline__ u32x4 dropout_block(uint64_t seed, uint64_t offset, uint64_t blk) {
+  return philox4x32((uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)offset,
                     (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__device__ __forceinline__ uint32_t dropout_byte(const u32x4& w, int k) {
+  return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 }
 
 // conv1 pre-activation at one output pixel/channel from an fp32 input tile with row stride 28.

@@ -24,8 +24,10 @@ constexpr int NFLAT = C2 * NPOOL;       // 9216
 constexpr int NH = 128, NCLS = 10;
 constexpr float MNIST_MEAN = 0.1307f, MNIST_STD = 0.3081f;
 constexpr float KEEP1 = 0.75f, KEEP2 = 0.5f;          // dropout(0.25), dropout(0.5)
-constexpr uint32_t KEEP1_THR = 0xC0000000u;           // u32 < thr  <=>  U[0,1) < 0.75
-constexpr uint32_t KEEP2_THR = 0x80000000u;
+// Dropout draws one random byte per element (16 elements per Philox-4x32-10 call); keep <=> byte < thr.
+// 192/256 = 0.75 and 128/256 = 0.5 exactly, so the keep probabilities are exact.
+constexpr uint32_t KEEP1_THR8 = 192u;
+constexpr uint32_t KEEP2_THR8 = 128u;
 
 // Flat fp32 parameter buffer: every tensor starts on a 64-element (256 B) boundary.
 // Bucket 0 (fc params, ready first in backward) = [0, OFF_CONV1_W); bucket 1 = conv params.

@@ -40,9 +40,12 @@ __device__ __forceinline__ int swz8(int row) { return row & 7; }
 __device__ __forceinline__ int swz_dy(int pix) { return (pix ^ (pix >> 1)) & 7; }
 }  // namespace
 
+// As few groups (= partial slabs for the reduce) as keep the per-group unit count minimal:
+// B=200 -> 400 units -> 200 groups x 2 units (not 256 groups doing 1 or 2).
 int conv_wgrad_groups(int B) {
   const int units = 2 * B;
-  return units < 256 ? units : 256;
+  const int per = (units + 255) / 256;
+  return (units + per - 1) / per;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -325,56 +328,99 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(ConvBwdArgs a, int B) 
 
 // --------------------------------------------------------------------------------------------
 // Deterministic fixed-order reduction of the partial slabs into the flat fp32 gradient buffer.
-//   [0, 288): conv2.weight, 64 outputs per WG, the 4 waves split the slabs, 8 loads in flight
-//   288:      conv2.bias
-//   [289, 309): conv1 weight+bias, 16 outputs x 16 slab-slices per WG
+// Latency-bound by construction (19 MB of partials at B=200, mostly MALL-resident), so every
+// thread issues all of its float4 loads before the first add:
+//   [0, 289): conv2 weight+bias slab columns, 16 float4 columns x 16 slab slices per WG
+//             (<= 16 loads in flight per thread for G <= 256), fixed-order LDS tree over slices
+//   [289, 309): conv1 weight+bias, 4 float4 columns x 64 slices of the 4*B dgrad partials
+namespace {
+constexpr int RED_W2_WGS = (W2PART_STRIDE / 4 + 15) / 16;   // 289
+constexpr int RED_C1_WGS = 320 / 16;                         // 20
+}  // namespace
+
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
-  __shared__ float red[256];
+  __shared__ float4 red[256];
   const int tid = threadIdx.x, bid = blockIdx.x;
-  const int G = a.wgrad_groups;
   const float sc = a.grad_scale;
-  if (bid < 288 || bid == 288) {
-    const int e = (bid < 288) ? bid * 64 + (tid & 63) : 18432 + (tid & 63);
-    const int sl = tid >> 6;
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int g0 = sl;
-    for (; g0 + 28 < G; g0 += 32) {
+  if (bid < RED_W2_WGS) {
+    const int G = a.wgrad_groups;
+    const int col = bid * 16 + (tid & 15), sl = tid >> 4;          // float4 column, slab slice
+    const float4* src = reinterpret_cast<const float4*>(a.w2part) + col;
+    constexpr int S4 = W2PART_STRIDE / 4;
+    float4 v[16];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] += a.w2part[(int64_t)(g0 + 4 * k) * W2PART_STRIDE + e];
+    for (int k = 0; k < 16; ++k) {
+      const int g = sl + 16 * k;
+      v[k] = (g < G) ? src[(int64_t)g * S4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (; g0 < G; g0 += 4) s[0] += a.w2part[(int64_t)g0 * W2PART_STRIDE + e];
-    red[tid] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    float4 t = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+    for (int g = sl + 256; g < G; g += 16) {          // G > 256 never happens today; kept general
+      const float4 u = src[(int64_t)g * S4];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    red[tid] = t;
     __syncthreads();
-    if (tid < 64) {
-      const float t = (red[tid] + red[tid + 64]) + (red[tid + 128] + red[tid + 192]);
-      if (bid < 288) {
-        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
-        const int r = e & 3, ln = (e >> 2) & 63, tile = e >> 8;
-        const int mtile = tile / 18, ntile = tile - mtile * 18;
-        const int co = 16 * mtile + 4 * (ln >> 4) + r;
-        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
-        a.grad[OFF_CONV2_W + co * 288 + ci * 9 + tap] = t * sc;
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) {                 // fixed-order tree over the 16 slices
+      if (sl < w) {
+        const float4 u = red[tid + 16 * w];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        red[tid] = t;
       }
-      else a.grad[OFF_CONV2_B + tid] = t * sc;
+      __syncthreads();
+    }
+    if (sl == 0) {
+      const int e = 4 * col;
+      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+      if (e < 18432) {
+        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
+        const int ln = (e >> 2) & 63, tile = e >> 8;
+        const int mtile = tile / 18, ntile = tile - mtile * 18;
+        const int co0 = 16 * mtile + 4 * (ln >> 4);
+        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.grad[OFF_CONV2_W + (co0 + r) * 288 + ci * 9 + tap] = o[r];
+      } else if (e < 18432 + C2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.grad[OFF_CONV2_B + (e - 18432) + r] = o[r];
+      }
     }
   } else {
-    const int j = (bid - 289) * 16 + (tid & 15), sl = tid >> 4;
+    const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
     const int nslab = 4 * B;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    int k = sl;
-    for (; k + 48 < nslab; k += 64) {
+    const float4* src = reinterpret_cast<const float4*>(a.c1part) + col;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {
+      float4 v[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s[u] += a.c1part[(int64_t)(k + 16 * u) * 320 + j];
+      for (int k = 0; k < 16; ++k) {
+        const int r = k0 + 64 * k;
+        v[k] = (r < nslab) ? src[(int64_t)r * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
     }
-    for (; k < nslab; k += 16) s[0] += a.c1part[(int64_t)k * 320 + j];
-    red[tid] = (s[0] + s[1]) + (s[2] + s[3]);
+    red[tid] = t;
     __syncthreads();
-    if (tid < 16) {
-      float t = 0.f;
-      for (int q = 0; q < 16; ++q) t += red[q * 16 + tid];
-      const int ci = j / 10, kk = j - ci * 10;
-      if (kk < 9) a.grad[OFF_CONV1_W + ci * 9 + kk] = t * sc;
-      else a.grad[OFF_CONV1_B + ci] = t * sc;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+      if (sl < w) {
+        const float4 u = red[tid + 4 * w];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        red[tid] = t;
+      }
+      __syncthreads();
+    }
+    if (sl == 0) {
+      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
+        if (kk < 9) a.grad[OFF_CONV1_W + ci * 9 + kk] = o[r];
+        else a.grad[OFF_CONV1_B + ci] = o[r];
+      }
     }
   }
 }
@@ -391,7 +437,7 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
 }
 
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(289 + 20), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_W2_WGS + RED_C1_WGS), dim3(256), 0, s, a, B);
 }
 
 }  // namespace mnist

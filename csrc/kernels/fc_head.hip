@@ -83,8 +83,8 @@ __device__ __forceinline__ void head_forward_row(const HeadArgs& a, int B, int b
     bool keep = true;
     if (train) {
       if (!no_dropout) {
-        const u32x4 w = dropout_words(seed, off, ((uint64_t)b * NH + o) >> 2);
-        keep = w[o & 3] < KEEP2_THR;
+        const u32x4 w = dropout_block(seed, off, ((uint64_t)b * NH + o) >> 4);
+        keep = dropout_byte(w, o & 15) < KEEP2_THR8;
       }
       h = keep ? (no_dropout ? h : h * (1.0f / KEEP2)) : 0.0f;
     }

@@ -12,8 +12,9 @@
 //     16-byte LDS read of 8 contiguous channels at (pixel + tap offset);
 //   * the M index is ordered pool-window-major (m = 4*window + q), so each lane's 4 accumulator
 //     registers hold one whole 2x2 window: max-pool + argmax happen in registers;
-//   * dropout uses Philox-4x32-10 keyed by (seed, per-step offset, element index), so the mask is a
-//     pure function of (step, position) and identical across launch geometries and graph replays.
+//   * dropout uses Philox-4x32-10 keyed by (seed, per-step offset, element index / 16) with one
+//     random byte per element, so the mask is a pure function of (step, position) and identical
+//     across launch geometries and graph replays.
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
@@ -25,13 +26,20 @@ constexpr int A1_ROWS = STRIP + 2;            // 10 conv1 rows
 constexpr int X_ROWS = STRIP + 4;             // 12 input rows
 constexpr int WIN = (STRIP / 2) * HP;         // 48 pool windows per strip
 
-// LDS carve (bytes, all 16-aligned)
-constexpr int XS_OFF = 0, XS_BYTES = X_ROWS * IMG * 4;                     // 1344
-constexpr int A1S_OFF = XS_OFF + XS_BYTES, A1S_BYTES = A1_ROWS * H1 * C1 * 2;   // 16640
-constexpr int W2S_OFF = A1S_OFF + A1S_BYTES, W2S_BYTES = C2 * 9 * C1 * 2;      // 36864
-constexpr int POOL_OFF = W2S_OFF + W2S_BYTES, POOL_BYTES = C2 * WIN * 4;       // 12288
-constexpr int FLAG_OFF = POOL_OFF + POOL_BYTES, FLAG_BYTES = C2 * WIN;         // 3072
-constexpr int LDS_TOTAL = FLAG_OFF + FLAG_BYTES;
+// LDS carve (bytes, all 16-aligned).  53,504 B so that three workgroups fit a CU (160 KiB): the
+// conv2-weight region is time-shared.  Weight chunks 0..6 of every thread (rows 0..447) are stored
+// in phase 0; the input rows live where chunks 7..8 go (rows 448..575) until conv1 has consumed
+// them, then those two chunks are stored from VGPRs (phase 1b).  After the MFMA loop the same
+// region holds the pool/flag staging (phases 3-4).
+constexpr int A1S_OFF = 0, A1S_BYTES = A1_ROWS * H1 * C1 * 2;                   // 16640
+constexpr int W2S_OFF = A1S_OFF + A1S_BYTES, W2S_BYTES = C2 * 9 * C1 * 2;       // 36864
+constexpr int W2_EARLY = 7;                                                     // chunks stored in phase 0
+constexpr int XS_OFF = W2S_OFF + W2_EARLY * 256 * 16, XS_BYTES = X_ROWS * IMG * 4;   // 1344 (alias)
+constexpr int POOL_OFF = W2S_OFF, POOL_BYTES = C2 * WIN * 4;                    // 12288 (alias)
+constexpr int FLAG_OFF = POOL_OFF + POOL_BYTES, FLAG_BYTES = C2 * WIN;          // 3072 (alias)
+constexpr int LDS_TOTAL = W2S_OFF + W2S_BYTES;
+static_assert(FLAG_OFF + FLAG_BYTES <= LDS_TOTAL && XS_OFF + XS_BYTES <= LDS_TOTAL, "LDS aliasing");
+static_assert(3 * LDS_TOTAL <= 160 * 1024, "three workgroups per CU");
 
 // 16-byte-chunk XOR swizzles (4 chunks of 8 channels per 64-byte row) against ds_read_b128 bank
 // conflicts: a1 rows are indexed by pixel, w2 rows by (channel, tap).
@@ -40,7 +48,7 @@ __device__ __forceinline__ int swz_w2(int n) { return (4 - ((n >> 2) & 3)) & 3; 
 }  // namespace
 
 template <bool TRAIN>
-__global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
+__global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_TOTAL];
   float* xs = reinterpret_cast<float*>(smem + XS_OFF);
   uint16_t* a1s = reinterpret_cast<uint16_t*>(smem + A1S_OFF);
@@ -57,11 +65,14 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
   // rows), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
   const int c = tid & 3;                         // conv1: fixed 8-channel chunk per thread
   float w[8][9], bias[8];
+  uint4 wv7, wv8;                                // last two conv2-weight chunks, parked until phase 1b
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.w2f);
-    uint4 wv[9];
+    uint4 wv[W2_EARLY];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) wv[i] = src[tid + 256 * i];
+    for (int i = 0; i < W2_EARLY; ++i) wv[i] = src[tid + 256 * i];
+    wv7 = src[tid + 256 * 7];
+    wv8 = src[tid + 256 * 8];
     const float4* w1v = reinterpret_cast<const float4*>(a.w1c + c * 72);
 #pragma unroll
     for (int k = 0; k < 18; ++k) {
@@ -77,6 +88,12 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
     uint4 xv = {0u, 0u, 0u, 0u};
     float4 xf = {0.f, 0.f, 0.f, 0.f};
     constexpr int XCH = X_ROWS * IMG / 16;       // 21 16-byte chunks (image rows are 16-B aligned)
+#pragma unroll
+    for (int i = 0; i < W2_EARLY; ++i) {          // swizzle only permutes chunks inside a 64-B row
+      const int ch = tid + 256 * i;
+      const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
+      *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(row / 9)) * 8)) = wv[i];
+    }
     if (a.xin) {                                  // module API: fp32 input rows (84 float4)
       if (tid < X_ROWS * IMG / 4)
         xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + strip * STRIP * IMG + tid * 4);
@@ -84,13 +101,6 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
       const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
       if (tid < XCH)
         xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int ch = tid + 256 * i;                // 2304 chunks of 16 B
-      const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
-      const int n = row / 9;
-      *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = wv[i];
     }
     if (a.xin) {
       if (tid < X_ROWS * IMG / 4) *reinterpret_cast<float4*>(xs + tid * 4) = xf;
@@ -133,6 +143,17 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
   }
   __syncthreads();
 
+  // ---- phase 1b: the last two conv2-weight chunks (swizzled) over the consumed input rows
+  static_assert(W2_EARLY == 7, "phase 1b stores chunks 7 and 8");
+#pragma unroll
+  for (int i = W2_EARLY; i < 9; ++i) {
+    const int ch = tid + 256 * i;                // 2304 chunks of 16 B
+    const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
+    const int n = row / 9;
+    *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = (i == 7) ? wv7 : wv8;
+  }
+  __syncthreads();
+
   // ---- phase 2: conv2 implicit GEMM on MFMA. wave w owns M-tiles 3w..3w+2 (16 pixels = 4 windows
   // each) x all 4 N-tiles (64 channels); K loop = 9 taps of 32 channels.
   const int wave = tid >> 6, lane = tid & 63;
@@ -170,6 +191,7 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
       for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(A[mt], Bf[nt], acc[mt][nt]);
   }
 
+  __syncthreads();   // every wave is done with the conv2 weights: their region becomes the staging
   // ---- phase 3: bias + ReLU + 2x2 max-pool (in registers) -> LDS staging [channel][window]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -191,34 +213,42 @@ __global__ __launch_bounds__(256) void trunk_fwd_kernel(TrunkFwdArgs a) {
   }
   __syncthreads();
 
-  // ---- phase 4: dropout + coalesced stores (4 contiguous flat elements = one Philox block)
+  // ---- phase 4: dropout + coalesced stores.  One thread = 16 contiguous flat elements of one
+  // channel = exactly one Philox block (48 = 3 x 16 per channel-strip), waves 0-2 only.
   const uint64_t seed = a.state ? a.state->seed : 0;
   const uint64_t off = a.state ? a.state->rng_base + 2ull * (uint64_t)step : 0;
   const bool drop = TRAIN && !(a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT));
+  if (tid < C2 * 3) {
+    const int n = tid / 3, j16 = (tid - n * 3) * 16;
+    const int flat = n * NPOOL + strip * WIN + j16;
+    const float* ps = pool_s + n * WIN + j16;
+    float o[16];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int qd = tid + 256 * i;           // 768 quads
-    const int n = qd / 12, j4 = (qd - n * 12) * 4;
-    const int flat = n * NPOOL + strip * WIN + j4;
-    const float4 pv = *reinterpret_cast<const float4*>(pool_s + n * WIN + j4);
-    const uint32_t fl = *reinterpret_cast<const uint32_t*>(flag_s + n * WIN + j4);
-    float o[4] = {pv.x, pv.y, pv.z, pv.w};
-    uint32_t mk = fl;
-    if (TRAIN) {
-      u32x4 rw = {0u, 0u, 0u, 0u};
-      if (drop) rw = dropout_words(seed, off, ((uint64_t)b * NFLAT + flat) >> 2);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool keep = rw[k] < KEEP1_THR;
-        o[k] = keep ? (drop ? o[k] * (1.0f / KEEP1) : o[k]) : 0.0f;
-        if (keep) mk |= 4u << (8 * k);
-      }
-      *reinterpret_cast<uint32_t*>(a.pmask_out + (int64_t)b * NFLAT + flat) = mk;
+    for (int q = 0; q < 4; ++q) {
+      const float4 pv = *reinterpret_cast<const float4*>(ps + 4 * q);
+      o[4 * q] = pv.x; o[4 * q + 1] = pv.y; o[4 * q + 2] = pv.z; o[4 * q + 3] = pv.w;
     }
-    uint2 st;
-    st.x = pack2bf(o[0], o[1]);
-    st.y = pack2bf(o[2], o[3]);
-    *reinterpret_cast<uint2*>(a.p_out + (int64_t)b * NFLAT + flat) = st;
+    if (TRAIN) {
+      const uint4 fl = *reinterpret_cast<const uint4*>(flag_s + n * WIN + j16);
+      u32x4 rw = {0u, 0u, 0u, 0u};
+      if (drop) rw = dropout_block(seed, off, ((uint64_t)b * NFLAT + flat) >> 4);
+      uint32_t mk[4] = {fl.x, fl.y, fl.z, fl.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const bool keep = dropout_byte(rw, k) < KEEP1_THR8;
+        o[k] = keep ? (drop ? o[k] * (1.0f / KEEP1) : o[k]) : 0.0f;
+        if (keep) mk[k >> 2] |= 4u << (8 * (k & 3));
+      }
+      *reinterpret_cast<uint4*>(a.pmask_out + (int64_t)b * NFLAT + flat) = uint4{mk[0], mk[1], mk[2], mk[3]};
+    }
+    uint4 s0, s1;
+    s0.x = pack2bf(o[0], o[1]);   s0.y = pack2bf(o[2], o[3]);
+    s0.z = pack2bf(o[4], o[5]);   s0.w = pack2bf(o[6], o[7]);
+    s1.x = pack2bf(o[8], o[9]);   s1.y = pack2bf(o[10], o[11]);
+    s1.z = pack2bf(o[12], o[13]); s1.w = pack2bf(o[14], o[15]);
+    uint4* dst = reinterpret_cast<uint4*>(a.p_out + (int64_t)b * NFLAT + flat);
+    dst[0] = s0;
+    dst[1] = s1;
   }
 }
 

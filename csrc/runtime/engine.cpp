@@ -44,7 +44,8 @@ Engine::~Engine() {
 void Engine::alloc_workspace() {
   const int M = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
   const int Mp = round_up(M, 64);
-  const int G = conv_wgrad_groups(max_batch_);
+  // conv_wgrad_groups is not monotonic in B (a smaller last batch can use more groups): size for the max
+  const int G = 2 * max_batch_ < 256 ? 2 * max_batch_ : 256;
   int64_t off = 0;
   auto carve = [&](int64_t bytes) { int64_t o = off; off += align256(bytes); return o; };
   const int64_t o_a1 = carve((int64_t)M * H1 * H1 * C1 * 2);

@@ -62,10 +62,12 @@ def philox4x32(ctr, key):
     return c0, c1, c2, c3
 
 
-def dropout_keep(seed: int, offset: int, elem: int, thr: int) -> bool:
-    quad = elem >> 2
-    w = philox4x32((quad & MASK, quad >> 32, offset & MASK, offset >> 32), (seed & MASK, seed >> 32))
-    return w[elem & 3] < thr
+def dropout_keep(seed: int, offset: int, elem: int, thr8: int) -> bool:
+    """Kernel dropout rule: one Philox block per 16 elements, one byte per element, keep <=> byte < thr8."""
+    blk = elem >> 4
+    w = philox4x32((blk & MASK, blk >> 32, offset & MASK, offset >> 32), (seed & MASK, seed >> 32))
+    k = elem & 15
+    return ((w[k >> 2] >> (8 * (k & 3))) & 0xFF) < thr8
 
 
 # ---------------------------------------------------------------- bf16-emulating reference

@@ -80,12 +80,12 @@ def test_train_step_dropout_masks_consistent(cuda_device):
     off = base + 2 * 3
     for e in [0, 1, 2, 3, 4, 9215, 9216, 50000, B * 9216 - 1]:
         b, i = divmod(e, 9216)
-        assert bool(keep1[b, i]) == dropout_keep(seed, off, e, 0xC0000000), e
+        assert bool(keep1[b, i]) == dropout_keep(seed, off, e, 192), e
     # reconstruct the reference with the kernel's own masks: dropout-1 from pmask, dropout-2 from Philox
     mask2 = torch.zeros(B, 128)
     for b in range(B):
         for o in range(128):
-            mask2[b, o] = float(dropout_keep(seed, off + 1, b * 128 + o, 0x80000000))
+            mask2[b, o] = float(dropout_keep(seed, off + 1, b * 128 + o, 128))
     loss_ref, _, g_ref = reference_step(ref, imgs, labels, mask1=keep1.float().view(B, 64, 12, 12), mask2=mask2)
     assert abs(buf.loss_rows.mean().item() - loss_ref.item()) < 3e-2
     grads = ms.views(ms.grad)
