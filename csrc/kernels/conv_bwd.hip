@@ -7,7 +7,8 @@
 //    (written by fc_bwd) into a zero-padded NHWC LDS tile with 16-B copies, runs the transposed
 //    convolution as an MFMA implicit GEMM (M = pixels, N = 32 ci, K = 9 taps x 64 co), applies the
 //    conv1 ReLU mask (stored bf16 a1 > 0, prefetched under the MFMA loop), and folds
-//    the conv1 weight/bias gradient (K = 9 tiny) into the epilogue as per-workgroup partials.
+//    the conv1 weight/bias gradient into the epilogue as a second 16x16x16 MFMA fed straight
+//    from the masked accumulators (per-workgroup partials).
 //  * conv2_wgrad_kernel  (G persistent WGs, each looping over half-images): dW2 = dy^T (x) im2col(a1),
 //    contraction over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
 //    from ds_read_b64_tr_b16 with per-lane row addresses, so the im2col gather is free.
@@ -165,55 +166,43 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
       for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bf[nt], acc[i][nt]);
   }
 
-  // ---- phase 3: conv1 ReLU mask (a1 > 0) + conv1 weight/bias gradient partials
-  float sdw[2][9], sdb[2];
+  // ---- phase 3: conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
+  // second, tiny MFMA: D[tap][ci] = sum_px X[px][tap] * d[px][ci] on v_mfma_f32_16x16x16_bf16
+  // (row 9 of X = ones -> the bias gradient).  That instruction's B-operand layout (lane l holds
+  // k = 4(l>>4)+j, n = l&15) is exactly the C layout of the dgrad accumulators, so the masked
+  // accumulators feed it straight from registers (bf16-rounded operands, fp32 accumulation).
+  floatx4 dw[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  {
+    const int tap = lane & 15, ty = tap / 3, tx = tap - 3 * ty;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    sdb[nt] = 0.f;
+    for (int i = 0; i < MT; ++i) {
+      short4_t ax, bd[2];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) sdw[nt][t] = 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 16 * (3 * wave + i) + 4 * kg + r;
-      if (q < npix) {
-        const int py = q / H1, px = q - py * H1;
-        const float* xp = xs + py * IMG + px;
-        float xv[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) xv[t] = xp[(t / 3) * IMG + (t % 3)];
+      for (int j = 0; j < 4; ++j) {
+        const int q = 16 * (3 * wave + i) + 4 * kg + j;
+        const int qc = q < npix ? q : npix - 1;
+        const int py = qc / H1, px = qc - py * H1;
+        const float xv = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
+        ax[j] = (short)f2bf(xv);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const uint16_t av = a1v[i][r][nt];
-          const float d = (av != 0 && !(av & 0x8000)) ? acc[i][nt][r] : 0.0f;
-          sdb[nt] += d;
-#pragma unroll
-          for (int t = 0; t < 9; ++t) sdw[nt][t] = __builtin_fmaf(d, xv[t], sdw[nt][t]);
+          const uint16_t av = a1v[i][j][nt];
+          const float d = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
+          bd[nt][j] = (short)f2bf(d);
         }
       }
-    }
-  // lanes l, l^16, l^32, l^48 share a channel
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    sdb[nt] += __shfl_xor(sdb[nt], 16, 64);
-    sdb[nt] += __shfl_xor(sdb[nt], 32, 64);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      sdw[nt][t] += __shfl_xor(sdw[nt][t], 16, 64);
-      sdw[nt][t] += __shfl_xor(sdw[nt][t], 32, 64);
+      for (int nt = 0; nt < 2; ++nt) dw[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ax, bd[nt], dw[nt], 0, 0, 0);
     }
   }
-  if (kg == 0) {
+  // dw[nt]: lane l holds D[tap = 4(l>>4) + r][ci = 16nt + (l&15)]
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      float* dst = red + (wave * 32 + nt * 16 + m) * 10;
+  for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) dst[t] = sdw[nt][t];
-      dst[9] = sdb[nt];
+    for (int r = 0; r < 4; ++r) {
+      const int t = 4 * kg + r;
+      if (t < 10) red[(wave * 32 + nt * 16 + m) * 10 + t] = dw[nt][r];
     }
-  }
   __syncthreads();
   for (int e = tid; e < 320; e += 256) {
     const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];

@@ -112,6 +112,7 @@ def emulated_bf16_step(net, images_u8, labels, mask1=None, mask2=None):
     grads["conv2.weight"] = G.conv2d_weight(a1, w2q.shape, dy)
     grads["conv2.bias"] = dy.sum((0, 2, 3))
     da1 = G.conv2d_input(a1.shape, w2q, dy) * (z0 > 0)
-    grads["conv1.weight"] = G.conv2d_weight(x, d["conv1.weight"].shape, da1)
-    grads["conv1.bias"] = da1.sum((0, 2, 3))
+    # conv1 weight/bias gradient: bf16 MFMA operands (input image and masked da1), fp32 accumulation
+    grads["conv1.weight"] = G.conv2d_weight(q(x), d["conv1.weight"].shape, q(da1))
+    grads["conv1.bias"] = q(da1).sum((0, 2, 3))
     return loss, lp, grads

@@ -174,8 +174,9 @@ def test_backward_kernels_stagewise_exact(cuda_device, B):
     x = normalize_u8(imgs).double()
     z0 = F.conv2d(x, d["conv1.weight"], d["conv1.bias"])
     da1 = G.conv2d_input(a1.shape, w2q, dy) * (z0 > 0)
-    assert rel_err(grads["conv1.weight"], G.conv2d_weight(x, d["conv1.weight"].shape, da1)) < 1e-4
-    assert rel_err(grads["conv1.bias"], da1.sum((0, 2, 3))) < 1e-4
+    # the dgrad kernel's da1 is fp32 in registers; its conv1 weight/bias GEMM takes bf16 operands
+    assert rel_err(grads["conv1.weight"], G.conv2d_weight(q(x), d["conv1.weight"].shape, q(da1))) < 2e-3
+    assert rel_err(grads["conv1.bias"], q(da1).sum((0, 2, 3))) < 2e-3
     # forward: a1 == bf16(relu(conv1)) exactly up to fp32 accumulation order
     a1_ref = q(F.relu(z0)).float()
     assert (a1.float() != a1_ref).float().mean().item() < 1e-3
