@@ -8,6 +8,7 @@
 #include <stdexcept>
 
 #include "include/kernels.h"
+#include "runtime/bucket_reducer.h"
 #include "runtime/engine.h"
 #include "runtime/rccl_comm.h"
 
@@ -175,6 +176,22 @@ PYBIND11_MODULE(_C, m) {
       })
       .def_property_readonly("world_size", &RcclComm::world_size)
       .def_property_readonly("rank", &RcclComm::rank);
+
+  // ---------------- DDP gradient reducer (module-level path) ----------------
+  py::class_<BucketReducer>(m, "BucketReducer")
+      .def(py::init([](std::vector<std::vector<int64_t>> numels, int world, std::shared_ptr<RcclComm> comm) {
+             return new BucketReducer(numels, world, std::move(comm));
+           }),
+           py::arg("bucket_numels"), py::arg("world_size"), py::arg("comm") = nullptr)
+      .def("prepare", &BucketReducer::prepare)
+      .def("mark_ready", [](BucketReducer& r, int b, int slot, uintptr_t grad, uintptr_t out, uintptr_t stream) {
+        r.mark_ready(b, slot, P<const float>(grad), P<float>(out), S(stream));
+      })
+      .def("finalize", [](BucketReducer& r, uintptr_t stream) { r.finalize(S(stream)); })
+      .def_property_readonly("num_buckets", &BucketReducer::num_buckets)
+      .def("bucket_numel", &BucketReducer::bucket_numel)
+      .def("bucket_ptr", &BucketReducer::bucket_ptr)
+      .def_property_readonly("launches", &BucketReducer::launches);
 
   // ---------------- engine ----------------
   py::class_<Engine>(m, "Engine")

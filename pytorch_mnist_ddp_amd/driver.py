@@ -118,8 +118,13 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
     model_without_ddp = model
     if distributed:
         from .parallel.ddp import DistributedDataParallel
+        comm = None
+        if device.type == "cuda":             # native C++ bucket reducer over the framework's RCCL comm
+            from .parallel.distributed import create_rccl_comm
+            comm = create_rccl_comm(world, rank, gpu)
         model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None,
-                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
+                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb,
+                                        comm=comm)
         model_without_ddp = model.module
     optimizer = Adadelta(model.parameters(), lr=args.lr)
     scheduler = StepLR(optimizer, step_size=1, gamma=args.gamma)

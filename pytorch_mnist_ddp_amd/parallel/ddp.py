@@ -14,8 +14,9 @@ Semantics reproduced from torch DDP (torch/nn/parallel/distributed.py, reducer.h
   copies the averaged buckets back into ``.grad``;
 * ``state_dict()`` keys carry the ``module.`` prefix; ``no_sync()`` skips reduction.
 
-Transport: ``torch.distributed`` (``nccl`` = RCCL on ROCm, ``gloo`` on CPU), or the framework's own
-RCCL communicator (``comm=``) for device tensors.  The fused training engine does not use these
+Transport: ``torch.distributed`` (``nccl`` = RCCL on ROCm, ``gloo`` on CPU), or - given the
+framework's own RCCL communicator (``comm=``) and device parameters - the native C++ reducer
+(:class:`NativeBucketReducer` over ``csrc/runtime/bucket_reducer.cpp``).  The fused training engine does not use these
 hooks - it reduces the flat gradient buffer in two buckets from C++ (``csrc/runtime/engine.cpp``)
 and the wrapper then only provides DDP's construction / state_dict semantics (``engine_managed``).
 """
@@ -130,6 +131,70 @@ class BucketReducer:
         self._armed = False
 
 
+class NativeBucketReducer:
+    """Adapter over the C++ ``_C.BucketReducer`` (csrc/runtime/bucket_reducer.cpp): same interface as
+    :class:`BucketReducer`, but the copy-in, the RCCL all-reduce on a high-priority comm stream
+    and the copy-out are enqueued from C++ with HIP events - no Python on the reduction path
+    beyond the hook dispatch itself."""
+
+    def __init__(self, params: list[torch.Tensor], buckets: list[list[int]], world_size: int, comm):
+        from ..ops import native
+        C = native.load()
+        self.params = params
+        self.world = world_size
+        self.buckets = buckets
+        self.slot = {}
+        for b, idxs in enumerate(buckets):
+            for s, i in enumerate(idxs):
+                self.slot[i] = (b, s)
+        self.impl = C.BucketReducer([[params[i].numel() for i in idxs] for idxs in buckets], world_size, comm)
+        self._armed = False
+        self._seen = set()
+        self.enabled = True
+        self.calls = []
+
+    def prepare_for_backward(self) -> None:
+        self.impl.prepare()
+        self._armed = False
+        self._seen = set()
+
+    def mark_ready(self, i: int) -> None:
+        if not self.enabled:
+            return
+        self._seen.add(i)
+        if not self._armed:
+            self._armed = True
+            torch.autograd.Variable._execution_engine.queue_callback(self.finalize)
+        b, s = self.slot[i]
+        p = self.params[i]
+        g = p.grad
+        ptr = g.data_ptr() if g is not None else 0
+        if g is not None and (not g.is_contiguous() or g.dtype != torch.float32):
+            raise RuntimeError("native DDP reducer expects contiguous fp32 gradients")
+        self.impl.mark_ready(b, s, ptr, ptr, torch.cuda.current_stream(p.device).cuda_stream)
+        self._log_launches()
+
+    def _log_launches(self) -> None:
+        # buckets leave in index order every iteration, so launch k is bucket k % num_buckets
+        for k in range(len(self.calls), self.impl.launches):
+            nb = k % len(self.buckets)
+            self.calls.append((nb, self.impl.bucket_numel(nb)))
+
+    def finalize(self) -> None:
+        dev = self.params[0].device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        for i, p in enumerate(self.params):      # parameters without a gradient contribute zeros
+            if i not in self._seen:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                b, s = self.slot[i]
+                self.impl.mark_ready(b, s, 0, p.grad.data_ptr(), stream)
+        self._log_launches()
+        self.impl.finalize(stream)
+        self._log_launches()
+        self._armed = False
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: float | None = None, find_unused_parameters: bool = False,
@@ -155,7 +220,10 @@ class DistributedDataParallel(nn.Module):
         self.bucket_indices = [[ready_order[j] for j in b] for b in assignment]
         self.reducer = None
         if not engine_managed:
-            self.reducer = BucketReducer(params, self.bucket_indices, self.world_size, process_group, comm)
+            if comm is not None and params and params[0].is_cuda:
+                self.reducer = NativeBucketReducer(params, self.bucket_indices, self.world_size, comm)
+            else:
+                self.reducer = BucketReducer(params, self.bucket_indices, self.world_size, process_group, comm)
             for i, p in enumerate(params):
                 p.register_post_accumulate_grad_hook(lambda _p, i=i: self.reducer.mark_ready(i))
 

@@ -110,6 +110,29 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         F.nll_loss(ddp(x), y).backward()
         assert [c[0] for c in ddp.reducer.calls] == [0, 1]
         assert list(ddp.state_dict())[0] == "module.conv1.weight"
+        # native C++ reducer (RCCL comm from the c10d store) == python reducer == no DDP
+        from pytorch_mnist_ddp_amd.parallel.ddp import NativeBucketReducer
+        from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comm
+        ncomm = create_rccl_comm(1, 0, 0, tag="native-reducer-test")
+        grads = []
+        for mode in ("plain", "python", "native"):
+            torch.manual_seed(7)
+            m = Net().to(cuda_device)
+            m.dropout1.p = m.dropout2.p = 0.0
+            w = m if mode == "plain" else DistributedDataParallel(m, device_ids=[0],
+                                                                  comm=ncomm if mode == "native" else None)
+            if mode == "native":
+                assert isinstance(w.reducer, NativeBucketReducer)
+            for _ in range(2):                       # two iterations: reducer state resets cleanly
+                for p_ in m.parameters():
+                    p_.grad = None
+                F.nll_loss(w(x), y).backward()
+            if mode == "native":
+                assert [c[0] for c in w.reducer.calls] == [0, 1, 0, 1]
+            torch.cuda.synchronize()
+            grads.append([p_.grad.detach().clone() for p_ in m.parameters()])
+        for a_, b_, c_ in zip(*grads):
+            assert torch.equal(a_, b_) and torch.equal(a_, c_)
         # engine with an attached RCCL communicator: fc bucket all-reduce + Adadelta on the comm
         # stream overlapped with the conv backward, captured into graphs; must equal no-comm run
         C = native.load()
