@@ -11,6 +11,10 @@ behaviour):
   ``--synthetic-test-size``: offline data selection.
 * ``--bucket-cap-mb`` / ``--first-bucket-mb``: DDP gradient bucket sizing.
 * ``--engine {fused,module}``: native step engine vs the reference's module-level loop.
+* ``--dtype {bf16,fp32}``: bf16 = the MI355X kernels (bf16 MFMA operands, fp32 accumulation,
+  fp32 master weights / optimizer state / gradient all-reduce); fp32 = stock torch fp32 ops on
+  the GPU (module engine) for exact-parity debugging.
+* ``--check-sync``: all-gather a parameter checksum after every epoch (DDP desync detector).
 * ``--graph-steps``: training steps captured per HIP graph (0 = eager launches).
 * ``--profile``: roctx ranges + per-epoch device timing; ``--json-log``: machine
   readable per-epoch metrics.
@@ -51,6 +55,12 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='use deterministic synthetic 28x28 data (auto when MNIST files are absent)')
     g.add_argument('--synthetic-train-size', type=int, default=None)
     g.add_argument('--synthetic-test-size', type=int, default=None)
+    g.add_argument('--synthetic-size', dest='synthetic_train_size', type=int, default=None,
+                   help='alias of --synthetic-train-size')
+    g.add_argument('--dtype', choices=['bf16', 'fp32'], default='bf16',
+                   help='bf16: MI355X MFMA kernels (default); fp32: torch fp32 ops (parity/debug, module engine)')
+    g.add_argument('--check-sync', action='store_true', default=False,
+                   help='verify parameters are identical on every rank after each epoch')
     g.add_argument('--engine', choices=['fused', 'module'], default=None,
                    help='fused: native step engine (GPU default); module: the reference loop over '
                         'Net/DDP/Adadelta (always used with --no-cuda)')

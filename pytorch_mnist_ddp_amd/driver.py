@@ -35,6 +35,11 @@ def _json_log(path, rec):
 
 
 # ----------------------------------------------------------------------------- module engine
+def _check_finite(loss: float, epoch: int, batch_idx: int) -> None:
+    if loss != loss or loss in (float("inf"), float("-inf")):     # fail fast
+        raise FloatingPointError(f"non-finite training loss {loss} at epoch {epoch} batch {batch_idx}")
+
+
 def _train_module(args, model, device, loader, optimizer, epoch, distributed, world, rank):
     model.train()
     n_batches = len(loader)
@@ -47,7 +52,9 @@ def _train_module(args, model, device, loader, optimizer, epoch, distributed, wo
         optimizer.step()
         if batch_idx % args.log_interval == 0 and (not distributed or rank == 0):
             seen = (world if distributed else 1) * batch_idx * len(data)
-            print(train_line(epoch, seen, len(loader.dataset), batch_idx, n_batches, loss.item()))
+            lv = loss.item()
+            _check_finite(lv, epoch, batch_idx)
+            print(train_line(epoch, seen, len(loader.dataset), batch_idx, n_batches, lv))
             if args.dry_run and not getattr(args, "_ddp_script", False):
                 break
         if args.dry_run and getattr(args, "_ddp_script", False):
@@ -100,6 +107,9 @@ def run(argv=None, ddp_script: bool = True) -> int:
     engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
     if not use_cuda:
         engine = "module"
+    if getattr(args, "dtype", "bf16") == "fp32":     # stock torch fp32 ops: module engine only
+        model.compute_dtype = torch.float32
+        engine = "module"
     if args.resume:
         load_state_dict(model, args.resume, map_location="cpu")
 
@@ -138,6 +148,9 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
         rec = {"epoch": epoch, "train_s": time.perf_counter() - t0}
         if not distributed or rank == 0:
             rec["test_loss"], rec["correct"] = _test_module(model_without_ddp, device, test_loader)
+        if distributed and args.check_sync:
+            from .parallel.ddp import assert_params_in_sync
+            assert_params_in_sync(list(model_without_ddp.parameters()))
         _json_log(args.json_log, rec)
         scheduler.step()
     _save(args, model, distributed, rank, ddp_script)
@@ -176,6 +189,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         trainer.set_lr(optimizer.param_groups[0]["lr"])
 
         def log_fn(batch_idx, blen, loss, epoch=epoch):
+            _check_finite(loss, epoch, batch_idx)
             seen = (world if distributed else 1) * batch_idx * blen
             print(train_line(epoch, seen, n_train, batch_idx, n_batches, loss), flush=False)
 
@@ -192,6 +206,10 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                 loss_sum, correct, n = trainer.evaluate()
             print(test_line(loss_sum / n, correct, n))
             rec.update(test_loss=loss_sum / n, correct=correct)
+        if distributed and args.check_sync:
+            from .parallel.ddp import assert_params_in_sync
+            trainer.synchronize()
+            assert_params_in_sync([ms.param])
         _json_log(args.json_log, rec)
         for p in optimizer.param_groups[0]["params"]:      # keep torch-format optimizer bookkeeping
             st_ = optimizer.state[p]

@@ -7,7 +7,9 @@ initial weights.  ``forward`` dispatches on the input device:
 
 * CPU: the reference math with torch ops (the ``mnist.py --no-cuda`` configuration);
 * GPU: the fused MI355X kernels (``ops.fused_net``) - gather/normalise-free conv trunk on
-  MFMA, split-K fc1, fused head - with autograd support through ``FusedNetFunction``.
+  MFMA, split-K fc1, fused head - with autograd support through ``FusedNetFunction``
+  (bf16 MFMA operands, fp32 accumulation / parameters).  ``compute_dtype = torch.float32``
+  selects the stock-torch fp32 path on the GPU instead (the ``--dtype fp32`` parity mode).
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ NUM_PARAMS = 1199882
 class Net(nn.Module):
     def __init__(self):
         super().__init__()
+        self.compute_dtype = torch.bfloat16     # GPU: fused bf16-MFMA kernels; float32: torch ops
         self.conv1 = nn.Conv2d(1, 32, 3, 1)
         self.conv2 = nn.Conv2d(32, 64, 3, 1)
         self.dropout1 = nn.Dropout(0.25)
@@ -49,7 +52,7 @@ class Net(nn.Module):
         return F.log_softmax(x, dim=1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.is_cuda:
+        if x.is_cuda and self.compute_dtype == torch.bfloat16:
             from ..ops.fused_net import fused_net_forward
             return fused_net_forward(self, x)
         return self.forward_reference(x)

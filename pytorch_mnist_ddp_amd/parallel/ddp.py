@@ -272,3 +272,30 @@ class DistributedDataParallel(nn.Module):
         finally:
             if self.reducer:
                 self.reducer.enabled = prev
+
+
+# ---------------------------------------------------------------------------- desync detection
+def params_fingerprint(tensors) -> torch.Tensor:
+    """Bit-exact fingerprint of fp32 tensors: int64 sums of their raw int32 bit patterns (plain and
+    position-weighted), so any single-bit difference between ranks changes it."""
+    parts = []
+    for t in tensors:
+        b = t.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+        w = torch.arange(b.numel(), device=b.device, dtype=torch.int64) % 8191 + 1
+        parts.append(torch.stack([b.sum(), (b * w).sum()]))
+    return torch.stack(parts).sum(0)
+
+
+def assert_params_in_sync(tensors, group=None) -> None:
+    """SURVEY §5.2 'DDP desync detector': every rank's parameters must be bitwise identical."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    fp = params_fingerprint(tensors)
+    if dist.get_backend(group) != "nccl":
+        fp = fp.cpu()
+    allv = [torch.zeros_like(fp) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(allv, fp, group=group)
+    bad = [r for r, v in enumerate(allv) if not torch.equal(v, allv[0])]
+    if bad:
+        raise RuntimeError(f"DDP desync: parameters on ranks {bad} differ from rank 0")
+

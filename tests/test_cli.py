@@ -29,3 +29,15 @@ def test_framework_flags_default_to_reference_behaviour():
     a = cli.parse_args(ddp=True, argv=[])
     assert a.resume is None and a.profile is False and a.bucket_cap_mb == 25.0 and a.first_bucket_mb == 1.0
     assert a.synthetic is None and a.data_root == "./data"
+    assert a.dtype == "bf16" and a.check_sync is False
+    b = cli.parse_args(ddp=False, argv=["--dtype", "fp32", "--synthetic-size", "123", "--check-sync"])
+    assert b.dtype == "fp32" and b.synthetic_train_size == 123 and b.check_sync
+
+
+def test_fail_fast_on_non_finite_loss():
+    import pytest
+    from pytorch_mnist_ddp_amd.driver import _check_finite
+    _check_finite(0.5, 1, 0)
+    for bad in (float("nan"), float("inf")):
+        with pytest.raises(FloatingPointError):
+            _check_finite(bad, 1, 10)

@@ -70,7 +70,19 @@ def _worker(rank, world, port, q):
     cs = torch.tensor([sum(p.double().sum().item() for p in ours.parameters())], dtype=torch.float64)
     allcs = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
     dist.all_gather(allcs, cs)
-    q.put((rank, max_diff, keys[:2], [c.item() for c in allcs], ours.reducer.calls[:2]))
+    # bit-exact desync detector: passes now, fires on every rank after a 1-ulp change on rank 1
+    from pytorch_mnist_ddp_amd.parallel.ddp import assert_params_in_sync
+    assert_params_in_sync(list(ours.parameters()))
+    if rank == 1:
+        with torch.no_grad():
+            w = next(ours.parameters()).view(-1)
+            w[5] = torch.nextafter(w[5], torch.tensor(float("inf")))
+    try:
+        assert_params_in_sync(list(ours.parameters()))
+        desync = False
+    except RuntimeError:
+        desync = True
+    q.put((rank, max_diff, keys[:2], [c.item() for c in allcs], ours.reducer.calls[:2], desync))
     dist.destroy_process_group()
 
 
@@ -85,7 +97,8 @@ def test_ddp_wrapper_matches_torch_ddp_on_gloo():
     res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(60)
-    for rank, max_diff, keys, css, calls in res:
+    for rank, max_diff, keys, css, calls, desync in res:
+        assert desync, rank
         assert max_diff < 1e-6, (rank, max_diff)
         assert keys == ["module.conv1.weight", "module.conv1.bias"]
         assert abs(css[0] - css[1]) < 1e-9
@@ -98,7 +111,7 @@ def test_mnist_ddp_script_two_ranks_gloo(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(ROOT, "mnist_ddp.py"), "--no-cuda", "--epochs", "2",
            "--batch-size", "64", "--synthetic", "--synthetic-train-size", "512", "--synthetic-test-size", "200",
-           "--log-interval", "2", "--save-model"]
+           "--log-interval", "2", "--save-model", "--check-sync"]
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -191,3 +191,17 @@ def test_torchrun_ddp_paths_on_one_gpu(tmp_path):
         sd = torch.load(os.path.join(tmp_path, "mnist_cnn.pt"), weights_only=True)
         assert list(sd)[0] == "module.conv1.weight"
         os.remove(os.path.join(tmp_path, "mnist_cnn.pt"))
+
+
+def test_fp32_parity_mode_uses_torch_ops(cuda_device):
+    """--dtype fp32: Net.compute_dtype = float32 runs stock torch fp32 ops on the GPU."""
+    torch.manual_seed(4)
+    net = Net()
+    ref = copy.deepcopy(net)
+    net = net.to(cuda_device)
+    net.compute_dtype = torch.float32
+    net.eval(), ref.eval()
+    x, _ = _data(32, cuda_device, seed=5)
+    with torch.no_grad():
+        assert rel_err(net(x).cpu(), ref(x.cpu())) < 1e-4
+    assert not hasattr(net, "_amd_fused_state")
