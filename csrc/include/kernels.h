@@ -112,6 +112,8 @@ struct AdadeltaArgs {
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
 void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
+// conv gradient slab reduce + the whole Adadelta update in one launch (single-GPU step tail)
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 // Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
 void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 

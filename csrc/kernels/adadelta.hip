@@ -14,6 +14,7 @@
 // lr is read from device memory so a captured graph picks up StepLR changes.
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "conv_grad_reduce.h"
 
 namespace mnist {
 
@@ -133,6 +134,36 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
     bid -= 1;
   }
   elementwise<UPDATE>(a, ad, OFF_CONV1_W, CONV_N, bid, CONV_WGS);
+}
+
+// Single-GPU step tail in ONE launch: the fc-tile / fc-tail updates of adadelta_kernel next to the
+// conv-gradient slab reduction, whose workgroups apply the update to each conv parameter as soon as
+// its gradient is final (no grad round trip, no extra kernel boundary; both halves are memory-
+// bound and overlap).  Same per-element math as the two-kernel path, so results are bitwise equal.
+__global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B) {
+  __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
+  __shared__ float4 red[256];
+  const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
+  int bid = blockIdx.x;
+  if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }
+  bid -= FC1_TILES;
+  if (bid == 0) { elementwise<true>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
+  bid -= 1;
+  float* gbuf = c.grad;
+  reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
+    gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
+    float p = a.param[e], sq = a.square_avg[e], acc = a.acc_delta[e];
+    ad.step(p, g, sq, acc);
+    a.param[e] = p;
+    a.square_avg[e] = sq;
+    a.acc_delta[e] = acc;
+    conv2_shadow(a, e, p);
+  });
+}
+
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(FC1_TILES + 1 + RED_WGS), dim3(256), 0, s, a, c, B);
 }
 
 static int adadelta_grid(int region) {

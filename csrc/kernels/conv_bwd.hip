@@ -9,13 +9,15 @@
 //    conv1 ReLU mask (stored bf16 a1 > 0, prefetched under the MFMA loop), and folds
 //    the conv1 weight/bias gradient into the epilogue as a second 16x16x16 MFMA fed straight
 //    from the masked accumulators (per-workgroup partials).
-//  * conv2_wgrad_kernel  (G persistent WGs, each looping over half-images): dW2 = dy^T (x) im2col(a1),
-//    contraction over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
+//  * conv2_wgrad_kernel  (G <= 256 WGs, each a contiguous range of dy rows of the whole batch, in
+//    8-row chunks through a double-buffered LDS pipeline): dW2 = dy^T (x) im2col(a1), contraction
+//    over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
 //    from ds_read_b64_tr_b16 with per-lane row addresses, so the im2col gather is free.
 //  * conv_grad_reduce_kernel: fixed-order (deterministic) sum of the partial slabs into the flat
 //    fp32 gradient buffer, scaled by 1/world_size (DDP averaging).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "conv_grad_reduce.h"
 
 namespace mnist {
 
@@ -29,11 +31,20 @@ constexpr int XS2_BYTES = DG_TROWS * IMG * 4;           // 1008 -> pad 1024
 constexpr int RED_BYTES = 4 * 32 * 10 * 4;              // 5120
 constexpr int DG_LDS = DYS_BYTES + W2DS_BYTES + 1024 + RED_BYTES;
 
-constexpr int WG_HALF_ROWS = 12;                        // dy rows per wgrad unit
-constexpr int WDYS_BYTES = WG_HALF_ROWS * H2 * C2 * 2;  // 36864
-constexpr int WA1S_BYTES = (WG_HALF_ROWS + 2) * H1 * C1 * 2;  // 23296
-constexpr int WG_LDS = WDYS_BYTES + WA1S_BYTES;
-constexpr int W2PART_STRIDE = 18432 + 64;
+// wgrad: every workgroup owns a contiguous range of dy rows of the whole batch (rows of
+// consecutive images are contiguous in both dy [B*24 rows] and a1 [B*26 rows]), processed in
+// chunks of up to 8 rows (192 px = 6 k-steps) through a double-buffered LDS pipeline.
+constexpr int WG_CH = 8;                                     // dy rows per chunk
+constexpr int WG_CHPX = WG_CH * H2;                          // 192 px
+constexpr int WG_A1ROWS = WG_CH + 4;                         // + 2 halo rows + 2 image-boundary rows
+constexpr int WDY_BYTES = WG_CHPX * C2 * 2;                  // 24576
+constexpr int WA1_BYTES = WG_A1ROWS * H1 * C1 * 2;           // 19968
+constexpr int WBUF_BYTES = WDY_BYTES + WA1_BYTES;            // 44544
+constexpr int WG_LDS = 2 * WBUF_BYTES;                       // 89088 (one workgroup per CU)
+constexpr int WG_THREADS = 512;                              // 8 waves: 2 per SIMD hide LDS latency
+constexpr int WDY_V = WDY_BYTES / 16 / WG_THREADS;           // 3 x 16 B per thread
+constexpr int WA1_V = (WA1_BYTES / 16 + WG_THREADS - 1) / WG_THREADS;   // 3 x 16 B (1248 used)
+static_assert(WDY_BYTES % (16 * WG_THREADS) == 0, "dy chunk staging");
 
 // 16-byte-chunk XOR swizzles against ds_read_b128 / ds_read_b64_tr_b16 bank conflicts (rows of
 // 128 B = 8 chunks, or 64 B = 4 chunks).  Chosen with tools/lds_banks.py (gfx950 lane-group model).
@@ -41,12 +52,12 @@ __device__ __forceinline__ int swz8(int row) { return row & 7; }
 __device__ __forceinline__ int swz_dy(int pix) { return (pix ^ (pix >> 1)) & 7; }
 }  // namespace
 
-// As few groups (= partial slabs for the reduce) as keep the per-group unit count minimal:
-// B=200 -> 400 units -> 200 groups x 2 units (not 256 groups doing 1 or 2).
+// One workgroup per CU, each owning >= 8 dy rows (B=200: 4800 rows -> 256 groups x 18-19 rows).
+// Monotonic in B, so a workspace sized for the largest batch fits every smaller one.
 int conv_wgrad_groups(int B) {
-  const int units = 2 * B;
-  const int per = (units + 255) / 256;
-  return (units + per - 1) / per;
+  const int rows = H2 * B;
+  const int g = (rows + WG_CH - 1) / WG_CH;
+  return g < 256 ? g : 256;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -211,25 +222,78 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
 }
 
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void conv2_wgrad_kernel(ConvBwdArgs a, int B) {
+namespace {
+// first a1 row (global, [B*26]) under dy row R (global, [B*24])
+__device__ __forceinline__ int a1_row_of(int R) { return R + 2 * (R / H2); }
+
+struct WgradChunk {
+  uint4 vd[WDY_V], va[WA1_V];
+};
+
+// Issue the global loads of chunk [c0, c1) into registers (zeros past the valid rows, so every LDS
+// byte of the buffer is rewritten and finite).
+__device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1, int tid, WgradChunk& k) {
+  const int ndy = (c1 - c0) * H2 * 8;                               // valid 16-B chunks of dy
+  const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
+  const int na1 = (A1 - A0) * H1 * 4;                               // valid 16-B chunks of a1
+  const uint4* dsrc = reinterpret_cast<const uint4*>(a.dy + (int64_t)c0 * H2 * C2);
+  const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
+  const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < WDY_V; ++i) {
+    const int c = tid + WG_THREADS * i;
+    k.vd[i] = (c < ndy) ? dsrc[c] : z;
+  }
+#pragma unroll
+  for (int i = 0; i < WA1_V; ++i) {
+    const int c = tid + WG_THREADS * i;
+    k.va[i] = (c < na1) ? asrc[c] : z;
+  }
+}
+
+__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, const WgradChunk& k, float* bsum) {
+  uint4* dys = reinterpret_cast<uint4*>(buf);
+  uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
+#pragma unroll
+  for (int i = 0; i < WDY_V; ++i) {
+    const int c = tid + WG_THREADS * i, pix = c >> 3;
+    dys[pix * 8 + ((c & 7) ^ swz_dy(pix))] = k.vd[i];
+    const uint32_t w4[4] = {k.vd[i].x, k.vd[i].y, k.vd[i].z, k.vd[i].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {          // conv2 bias gradient: this thread always holds channels 8*(tid&7)..
+      bsum[2 * j] += bf2f((uint16_t)(w4[j] & 0xFFFF));
+      bsum[2 * j + 1] += bf2f((uint16_t)(w4[j] >> 16));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < WA1_V; ++i) {
+    const int c = tid + WG_THREADS * i;
+    if (c < WA1_BYTES / 16) a1s[c] = k.va[i];
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
-  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);                // [12][24][64]
-  uint16_t* a1s = reinterpret_cast<uint16_t*>(smem + WDYS_BYTES);   // [14][26][32]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
-  const int G = gridDim.x;
-  floatx4 acc[2][9];
+  // 8 waves = 2 co-tile pairs x 4 groups of the 18 (tap, ci-half) n-tiles (5, 5, 4, 4)
+  const int mt0 = 2 * (wave & 1), ng = wave >> 1;
+  const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int rows = H2 * B;
+  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
+  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
+
+  floatx4 acc[2][5];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // conv2 bias partial: each thread always stages channels 8*(tid&7)..+7 of the dy tile
+    for (int j = 0; j < 5; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-  constexpr int DY_CH = WDYS_BYTES / 16;   // 2304 = 9 per thread
-  // per-lane fragment offsets (elements), hoisted out of the unit and k-step loops
+  // per-lane A (dy) fragment offsets: pixel rows 32ks + clo / + chi, swizzle independent of ks
   const int clo = 8 * gq + q, chi = clo + 4;
   int aoff_lo[2], aoff_hi[2];
 #pragma unroll
@@ -238,187 +302,89 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(ConvBwdArgs a, int B) 
     aoff_lo[i] = clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7));
     aoff_hi[i] = chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7));
   }
-  constexpr int A1_CH = WA1S_BYTES / 16;   // 1456
+  // per-lane B (a1) tap offsets of this wave's n-tiles
+  int toffs[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int nt = nt0 + (j < nn ? j : 0), t = nt >> 1, ci0 = 16 * (nt & 1);
+    toffs[j] = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
+  }
 
-  for (int u = blockIdx.x; u < 2 * B; u += G) {
-    const int b = u >> 1, h = u & 1;
-    {
-      const uint4* dsrc = reinterpret_cast<const uint4*>(a.dy + ((int64_t)b * H2 + WG_HALF_ROWS * h) * H2 * C2);
-      const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + ((int64_t)b * H1 + WG_HALF_ROWS * h) * H1 * C1);
-      uint4 vd[9], va[6];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) vd[k] = dsrc[tid + 256 * k];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int c = tid + 256 * k;
-        va[k] = asrc[c < A1_CH ? c : A1_CH - 1];   // clamped: no conditional load (keeps va in VGPRs)
-      }
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const int c = tid + 256 * k, pix = c >> 3;
-        reinterpret_cast<uint4*>(dys)[pix * 8 + ((c & 7) ^ swz_dy(pix))] = vd[k];
-        const uint32_t w4[4] = {vd[k].x, vd[k].y, vd[k].z, vd[k].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          bsum[2 * j] += bf2f((uint16_t)(w4[j] & 0xFFFF));
-          bsum[2 * j + 1] += bf2f((uint16_t)(w4[j] >> 16));
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int c = tid + 256 * k;
-        if (c < A1_CH) reinterpret_cast<uint4*>(a1s)[c] = va[k];
-      }
-      (void)DY_CH;
-    }
-    __syncthreads();
+  WgradChunk k;
+  if (nchunks > 0) {
+    wgrad_fetch(a, r0, min(r0 + WG_CH, r1), tid, k);
+    wgrad_store(smem, tid, k, bsum);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int c0 = r0 + ch * WG_CH, c1 = min(c0 + WG_CH, r1);
+    const bool more = ch + 1 < nchunks;
+    if (more) wgrad_fetch(a, c1, min(c1 + WG_CH, r1), tid, k);     // in flight under the MFMAs
+    const unsigned char* buf = smem + (ch & 1) * WBUF_BYTES;
+    const uint16_t* dys = reinterpret_cast<const uint16_t*>(buf);
+    const uint16_t* a1s = reinterpret_cast<const uint16_t*>(buf + WDY_BYTES);
+    const int A0 = a1_row_of(c0);
+    const int nks = ((c1 - c0) * H2 + 31) / 32;
 #pragma unroll 1
-    for (int ks = 0; ks < 9; ++ks) {
-      // A: dy rows (pixels) 32ks + c; the chunk swizzle (c ^ c>>1) & 7 does not depend on ks
+    for (int ks = 0; ks < nks; ++ks) {
       bf16x8 A[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) A[i] = tr_frag(dys + ks * 32 * C2 + aoff_lo[i], dys + ks * 32 * C2 + aoff_hi[i]);
-      // B: a1 pixel of dy pixel p = 32ks + c shifted by the tap = p + 2*(p/24) + (ky*26 + kx)
+      // B: a1 pixel under dy pixel p of the chunk (row c0 + p/24, col p%24), shifted by the tap
       const int plo = 32 * ks + clo, phi = plo + 4;
-      const uint16_t* blo = a1s + (plo + 2 * (plo / H2)) * C1 + 4 * pp;
-      const uint16_t* bhi = a1s + (phi + 2 * (phi / H2)) * C1 + 4 * pp;
+      const int rlo = plo / H2, rhi = phi / H2;
+      const int blo_px = (a1_row_of(c0 + rlo) - A0) * H1 + (plo - rlo * H2);
+      const int bhi_px = (a1_row_of(c0 + rhi) - A0) * H1 + (phi - rhi * H2);
+      const uint16_t* blo = a1s + blo_px * C1 + 4 * pp;
+      const uint16_t* bhi = a1s + bhi_px * C1 + 4 * pp;
 #pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const int nt = nt0 + j, t = nt >> 1, ci0 = 16 * (nt & 1);
-        const int toff = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
-        const bf16x8 Bf = tr_frag(blo + toff, bhi + toff);
+      for (int j = 0; j < 5; ++j) {
+        if (j < nn) {                                               // wave-uniform
+          const bf16x8 Bf = tr_frag(blo + toffs[j], bhi + toffs[j]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
+          for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
+        }
       }
     }
+    if (more) wgrad_store(smem + ((ch + 1) & 1) * WBUF_BYTES, tid, k, bsum);
     __syncthreads();
   }
   // slab layout = MFMA-native [co-tile 4][n-tile 18][lane 64][4]: one coalesced float4 per tile
-  float* out = a.w2part + (int64_t)blockIdx.x * W2PART_STRIDE;
+  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int tile = (mt0 + i) * 18 + nt0 + j;
-      *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
-    }
-  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 32 such threads via LDS
+    for (int j = 0; j < 5; ++j)
+      if (j < nn) {
+        const int tile = (mt0 + i) * 18 + nt0 + j;
+        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
+      }
+  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 64 such threads via LDS
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[j * 256 + tid] = bsum[j];
+  for (int j = 0; j < 8; ++j) red[j * WG_THREADS + tid] = bsum[j];
   __syncthreads();
   if (tid < 64) {
     const int c8 = tid >> 3, j = tid & 7;     // channel = 8*c8 + j
     float s = 0.f;
-    for (int k = 0; k < 32; ++k) s += red[j * 256 + k * 8 + c8];
+    for (int kk = 0; kk < WG_THREADS / 8; ++kk) s += red[j * WG_THREADS + kk * 8 + c8];
     out[18432 + 8 * c8 + j] = s;
   }
 }
 
 // --------------------------------------------------------------------------------------------
-// Deterministic fixed-order reduction of the partial slabs into the flat fp32 gradient buffer.
-// Latency-bound by construction (19 MB of partials at B=200, mostly MALL-resident), so every
-// thread issues all of its float4 loads before the first add:
-//   [0, 289): conv2 weight+bias slab columns, 16 float4 columns x 16 slab slices per WG
-//             (<= 16 loads in flight per thread for G <= 256), fixed-order LDS tree over slices
-//   [289, 309): conv1 weight+bias, 4 float4 columns x 64 slices of the 4*B dgrad partials
-namespace {
-constexpr int RED_W2_WGS = (W2PART_STRIDE / 4 + 15) / 16;   // 289
-constexpr int RED_C1_WGS = 320 / 16;                         // 20
-}  // namespace
-
+// Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
   __shared__ float4 red[256];
-  const int tid = threadIdx.x, bid = blockIdx.x;
-  const float sc = a.grad_scale;
-  if (bid < RED_W2_WGS) {
-    const int G = a.wgrad_groups;
-    const int col = bid * 16 + (tid & 15), sl = tid >> 4;          // float4 column, slab slice
-    const float4* src = reinterpret_cast<const float4*>(a.w2part) + col;
-    constexpr int S4 = W2PART_STRIDE / 4;
-    float4 v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int g = sl + 16 * k;
-      v[k] = (g < G) ? src[(int64_t)g * S4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float4 t = v[0];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
-    for (int g = sl + 256; g < G; g += 16) {          // G > 256 never happens today; kept general
-      const float4 u = src[(int64_t)g * S4];
-      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-    }
-    red[tid] = t;
-    __syncthreads();
-#pragma unroll
-    for (int w = 8; w >= 1; w >>= 1) {                 // fixed-order tree over the 16 slices
-      if (sl < w) {
-        const float4 u = red[tid + 16 * w];
-        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-        red[tid] = t;
-      }
-      __syncthreads();
-    }
-    if (sl == 0) {
-      const int e = 4 * col;
-      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
-      if (e < 18432) {
-        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
-        const int ln = (e >> 2) & 63, tile = e >> 8;
-        const int mtile = tile / 18, ntile = tile - mtile * 18;
-        const int co0 = 16 * mtile + 4 * (ln >> 4);
-        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a.grad[OFF_CONV2_W + (co0 + r) * 288 + ci * 9 + tap] = o[r];
-      } else if (e < 18432 + C2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a.grad[OFF_CONV2_B + (e - 18432) + r] = o[r];
-      }
-    }
-  } else {
-    const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
-    const int nslab = 4 * B;
-    const float4* src = reinterpret_cast<const float4*>(a.c1part) + col;
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {
-      float4 v[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int r = k0 + 64 * k;
-        v[k] = (r < nslab) ? src[(int64_t)r * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
-    }
-    red[tid] = t;
-    __syncthreads();
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-      if (sl < w) {
-        const float4 u = red[tid + 4 * w];
-        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-        red[tid] = t;
-      }
-      __syncthreads();
-    }
-    if (sl == 0) {
-      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
-        if (kk < 9) a.grad[OFF_CONV1_W + ci * 9 + kk] = o[r];
-        else a.grad[OFF_CONV1_B + ci] = o[r];
-      }
-    }
-  }
+  float* grad = a.grad;
+  reduce_conv_grads(a, B, blockIdx.x, red, [grad](int64_t e, float v) { grad[e] = v; });
 }
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
 }
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
 }
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
   launch_conv_dgrad(a, B, s);
@@ -426,7 +392,7 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
 }
 
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_W2_WGS + RED_C1_WGS), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_WGS), dim3(256), 0, s, a, B);
 }
 
 }  // namespace mnist

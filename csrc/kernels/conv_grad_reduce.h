@@ -1,0 +1,106 @@
+// Deterministic fixed-order reduction of the conv gradient partial slabs (shared by the stand-alone
+// reduce kernel in conv_bwd.hip and the fused reduce+Adadelta launch in adadelta.hip).
+// Latency-bound by construction (19 MB of partials at B=200, mostly MALL-resident), so every
+// thread issues all of its float4 loads before the first add:
+//   [0, 289): conv2 weight+bias slab columns, 16 float4 columns x 16 slab slices per WG
+//             (<= 16 loads in flight per thread for G <= 256), fixed-order LDS tree over slices
+//   [289, 309): conv1 weight+bias, 4 float4 columns x 64 slices of the 4*B dgrad partials
+// Each final (scaled) value is handed to sink(flat_element_index, value).
+#pragma once
+#include "../include/device_utils.h"
+#include "../include/kernels.h"
+
+namespace mnist {
+
+constexpr int W2PART_STRIDE = 18432 + 64;
+constexpr int RED_W2_WGS = (W2PART_STRIDE / 4 + 15) / 16;   // 289
+constexpr int RED_C1_WGS = 320 / 16;                         // 20
+constexpr int RED_WGS = RED_W2_WGS + RED_C1_WGS;             // 309
+
+template <class Sink>
+__device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Sink&& sink) {
+  const int tid = threadIdx.x;
+  const float sc = a.grad_scale;
+  if (bid < RED_W2_WGS) {
+    const int G = a.wgrad_groups;
+    const int col = bid * 16 + (tid & 15), sl = tid >> 4;          // float4 column, slab slice
+    const float4* src = reinterpret_cast<const float4*>(a.w2part) + col;
+    constexpr int S4 = W2PART_STRIDE / 4;
+    float4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int g = sl + 16 * k;
+      v[k] = (g < G) ? src[(int64_t)g * S4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 t = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+    for (int g = sl + 256; g < G; g += 16) {          // G > 256 never happens today; kept general
+      const float4 u = src[(int64_t)g * S4];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    red[tid] = t;
+    __syncthreads();
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) {                 // fixed-order tree over the 16 slices
+      if (sl < w) {
+        const float4 u = red[tid + 16 * w];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        red[tid] = t;
+      }
+      __syncthreads();
+    }
+    if (sl == 0) {
+      const int e = 4 * col;
+      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+      if (e < 18432) {
+        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
+        const int ln = (e >> 2) & 63, tile = e >> 8;
+        const int mtile = tile / 18, ntile = tile - mtile * 18;
+        const int co0 = 16 * mtile + 4 * (ln >> 4);
+        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sink((int64_t)OFF_CONV2_W + (co0 + r) * 288 + ci * 9 + tap, o[r]);
+      } else if (e < 18432 + C2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sink((int64_t)OFF_CONV2_B + (e - 18432) + r, o[r]);
+      }
+    }
+  } else {
+    const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
+    const int nslab = 4 * B;
+    const float4* src = reinterpret_cast<const float4*>(a.c1part) + col;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {
+      float4 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int r = k0 + 64 * k;
+        v[k] = (r < nslab) ? src[(int64_t)r * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+    }
+    red[tid] = t;
+    __syncthreads();
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+      if (sl < w) {
+        const float4 u = red[tid + 4 * w];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        red[tid] = t;
+      }
+      __syncthreads();
+    }
+    if (sl == 0) {
+      const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
+        sink(kk < 9 ? (int64_t)OFF_CONV1_W + ci * 9 + kk : (int64_t)OFF_CONV1_B + ci, o[r]);
+      }
+    }
+  }
+}
+
+}  // namespace mnist

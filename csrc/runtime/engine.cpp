@@ -44,8 +44,7 @@ Engine::~Engine() {
 void Engine::alloc_workspace() {
   const int M = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
   const int Mp = round_up(M, 64);
-  // conv_wgrad_groups is not monotonic in B (a smaller last batch can use more groups): size for the max
-  const int G = 2 * max_batch_ < 256 ? 2 * max_batch_ : 256;
+  const int G = conv_wgrad_groups(max_batch_);   // monotonic in B
   int64_t off = 0;
   auto carve = [&](int64_t bytes) { int64_t o = off; off += align256(bytes); return o; };
   const int64_t o_a1 = carve((int64_t)M * H1 * H1 * C1 * 2);
@@ -152,12 +151,14 @@ void Engine::enqueue_step(int batch) {
   if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
   launch_conv_dgrad(cb, B, compute_);
   if (ws != compute_) HIP_OK(hipStreamWaitEvent(compute_, ev_w_, 0));
+  if (one_update) {                     // single GPU: slab reduce + full Adadelta in one launch
+    launch_adadelta_reduce(adc, cb, B, compute_);
+    return;
+  }
   launch_conv_grad_reduce(cb, B, compute_);
   HIP_OK(hipEventRecord(ev_conv_, compute_));
   if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_conv_, 0));
-  if (one_update) {
-    launch_adadelta(adc, ADA_ALL, ms);
-  } else if (dist && !two_buckets_) {
+  if (dist && !two_buckets_) {
     comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, ms);
     launch_adadelta(adc, ADA_ALL, ms);
   } else {
