@@ -40,7 +40,7 @@ from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream  # noqa: 
 from pytorch_mnist_ddp_amd.engine.state import ModelState  # noqa: E402
 from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer  # noqa: E402
 from pytorch_mnist_ddp_amd.models.net import Net  # noqa: E402
-from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comm  # noqa: E402
+from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comms  # noqa: E402
 
 METRIC = "images/sec + 20-epoch wallclock, MNIST CNN DDP at 1/2/4/8 MI355X"
 # reference README.md:55-59 (20-epoch wallclock at B=200/GPU) -> images/s = 20*60000/t
@@ -88,10 +88,10 @@ def main() -> int:
     steps_per_epoch = math.ceil(len(sampler) / B)
     num_samples = max(total * B, steps_per_epoch * B)
     ms = ModelState(net, dev, lr=1.0)
-    comm = create_rccl_comm(world, rank, local) if use_pg else None
+    comm, comm2 = create_rccl_comms(world, rank, local) if use_pg else (None, None)
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                      two_buckets=not args.single_bucket)
+                      two_buckets=not args.single_bucket, comm2=comm2)
     if comm is not None:
         tr.engine.broadcast_params(0)     # DDP construction semantics: rank-0 weights everywhere
 
@@ -137,7 +137,7 @@ def main() -> int:
         ms2 = ModelState(net2, dev, lr=1.0)
         tr2 = FusedTrainer(ms2, train, test, B, 1000, num_samples=len(sampler), world_size=world, rank=rank,
                            comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                           two_buckets=not args.single_bucket)
+                           two_buckets=not args.single_bucket, comm2=comm2)
         if comm is not None:
             tr2.engine.broadcast_params(0)
         if use_pg:

@@ -203,6 +203,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("buffers"), py::arg("max_batch"), py::arg("max_test_batch"), py::arg("compute_stream"),
            py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
       .def("attach_comm", &Engine::attach_comm)
+      .def("attach_comm2", &Engine::attach_comm2)
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_concurrent", &Engine::set_concurrent)
       .def("set_dist_schedule", &Engine::set_dist_schedule)

@@ -24,18 +24,21 @@ constexpr int64_t FC_TAIL_N = OFF_CONV1_W - OFF_FC1_B;            // 1472 (fc1.b
 constexpr int64_t CONV_N = PARAM_TOTAL - OFF_CONV1_W;             // 18880
 constexpr int CONV_WGS = (int)((CONV_N / 4 + 255) / 256);         // 19
 
+// Every operation individually rounded (FMA contraction off), in torch's order
+// (optim/adadelta.py: mul_, addcmul_, add+sqrt, add+sqrt, div_, mul_, mul_, addcmul_, add_), so
+// the result is a pure function of the inputs - identical in every kernel / inlining context
+// (with contraction on, the same source fused differently in the fused reduce+update launch).
 struct Ada {
   float rho, eps, wd, lr;
   __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {
+#pragma clang fp contract(off)
     if (wd != 0.0f) g = g + wd * p;
-    sq = sq * rho;
-    sq = sq + (1.0f - rho) * g * g;
+    const float c = 1.0f - rho;
+    sq = sq * rho + (c * g) * g;
     const float sd = sqrtf(sq + eps);
     float d = sqrtf(acc + eps);
-    d = d / sd;
-    d = d * g;
-    acc = acc * rho;
-    acc = acc + (1.0f - rho) * d * d;
+    d = (d / sd) * g;
+    acc = acc * rho + (c * d) * d;
     p = p + (-lr) * d;
     return p;
   }

@@ -80,6 +80,11 @@ void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
   comm_ = std::move(comm);
 }
 
+void Engine::attach_comm2(std::shared_ptr<RcclComm> comm) {
+  if (comm && comm->world_size() != world_) throw std::runtime_error("comm world size mismatch");
+  comm2_ = std::move(comm);
+}
+
 void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags) {
   StepState host{step0, flags, seed, rng_base};
   // tiny H2D of 24 bytes, ordered on the compute stream (never inside a captured graph)
@@ -87,7 +92,7 @@ void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags)
   HIP_OK(hipStreamSynchronize(compute_));   // `host` lives on this stack frame
 }
 
-void Engine::enqueue_step(int batch) {
+void Engine::enqueue_step(int batch, bool last) {
   const int B = batch, Bp = round_up(B, 32);
   const int stride = idx_stride_;
   float* P = buf_.param;
@@ -96,6 +101,10 @@ void Engine::enqueue_step(int batch) {
   TrunkFwdArgs tf{buf_.train_u8, buf_.train_idx, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
   launch_trunk_fwd(tf, B, true, compute_);
+  if (side_pending_) {                 // schedule 2: previous step's fc all-reduce + fc update
+    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+    side_pending_ = false;
+  }
   launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
@@ -115,7 +124,31 @@ void Engine::enqueue_step(int batch) {
                  conv_wgrad_groups(B), nullptr};
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
-  if (dist && two_buckets_ && !concurrent_ && dist_sched_ == 1) {
+  if (dist && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 2) {
+    // Cross-step overlap: the fc bucket (fc1.w/b, fc2.w/b = 98.4 % of the bytes) is all-reduced on
+    // its own communicator and updated on the comm stream while the compute stream runs the conv
+    // backward, the conv-bucket all-reduce (first communicator) + conv update, and the next step's
+    // trunk_fwd - which reads only conv weights.  The join sits right before the next fc1_fwd (or
+    // at the end of the captured chunk).  Two communicators because RCCL ops of one communicator
+    // must not be in flight concurrently on two streams.
+    HIP_OK(hipEventRecord(ev_fc_, compute_));
+    launch_conv_wgrad(cb, B, compute_);                 // first-captured child stays on this queue
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    side_pending_ = true;
+    launch_conv_dgrad(cb, B, compute_);
+    launch_conv_grad_reduce(cb, B, compute_);
+    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+    launch_adadelta(adc, ADA_CONV, compute_);
+    if (last) {
+      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      side_pending_ = false;
+    }
+    return;
+  }
+  if (dist && two_buckets_ && !concurrent_ && dist_sched_ >= 1) {
     // Every cross-queue edge costs ~5-10 us of signal latency, so the critical path (conv backward,
     // conv bucket, conv update) never leaves the compute queue; only the fc bucket (98.4 % of the
     // bytes) forks onto the comm stream, and the join is on an edge that has long completed.
@@ -174,7 +207,7 @@ void Engine::enqueue_step(int batch) {
 void Engine::train_steps(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
-  for (int i = 0; i < n; ++i) enqueue_step(batch);
+  for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
   HIP_OK(hipGetLastError());
 }
 
@@ -184,8 +217,9 @@ int Engine::capture_train(int n, int batch, int stride) {
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
   try {
-    for (int i = 0; i < n; ++i) enqueue_step(batch);
+    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
   } catch (...) {
+    side_pending_ = false;
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
     throw;

@@ -58,11 +58,16 @@ class Engine {
   ~Engine();
 
   void attach_comm(std::shared_ptr<RcclComm> comm);   // enables the overlapped DDP path
+  // second communicator for the fc bucket: lets it stay in flight across the step boundary
+  // (joined only before the next step's fc1) while the conv bucket reduces on the first
+  void attach_comm2(std::shared_ptr<RcclComm> comm);
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
   void set_concurrent(bool on) { concurrent_ = on; }
   // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
-  // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute
-  void set_dist_schedule(int s) { dist_sched_ = s; }   // parallel graph branches (wgrad || dgrad, fc optimizer || conv bwd)
+  // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute;
+  // 2 (needs attach_comm2) = as 1, but the fc branch is joined just before the next step's fc1,
+  //   so it overlaps the conv backward, the conv bucket, the conv update AND the next trunk_fwd
+  void set_dist_schedule(int s) { dist_sched_ = s; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -83,7 +88,7 @@ class Engine {
   const EngineBuffers& buffers() const { return buf_; }
 
  private:
-  void enqueue_step(int batch);
+  void enqueue_step(int batch, bool last);
   void enqueue_eval(int n_total, int batch);
   void alloc_workspace();
 
@@ -96,7 +101,8 @@ class Engine {
   int idx_stride_ = 0;
   bool concurrent_ = false;
   int dist_sched_ = 1;
-  std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<RcclComm> comm_, comm2_;
+  bool side_pending_ = false;       // schedule 2: the previous step's fc branch is not joined yet
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;
   hipStream_t wgrad_stream_ = nullptr;
   // workspace

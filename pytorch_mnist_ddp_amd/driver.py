@@ -163,20 +163,21 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     from .utils.profiling import roctx_range
     ms = ModelState(model, device, lr=args.lr)
     model_for_save = model
-    comm = None
+    comm = comm2 = None
     if distributed:
         from .parallel.ddp import DistributedDataParallel
-        from .parallel.distributed import create_rccl_comm
+        from .parallel.distributed import create_rccl_comms
         ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
                                       bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
         model_for_save = ddp
-        comm = create_rccl_comm(world, rank, gpu)
+        comm, comm2 = create_rccl_comms(world, rank, gpu)
     optimizer = Adadelta(model.parameters(), lr=args.lr, model_state=ms)
     scheduler = StepLR(optimizer, step_size=1, gamma=args.gamma)
     graph_steps = args.log_interval if args.graph_steps is None else args.graph_steps
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
-                           world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps)
+                           world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
+                           comm2=comm2)
     trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper
     n_train = len(train_data)
     n_batches = num_batches(len(train_stream), args.batch_size)

@@ -43,7 +43,7 @@ class FusedTrainer:
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
-                 two_buckets: bool = True, concurrent: bool | None = None):
+                 two_buckets: bool = True, concurrent: bool | None = None, comm2=None):
         C = native.load()
         self.C, self.ms = C, mstate
         dev = mstate.device
@@ -85,10 +85,15 @@ class FusedTrainer:
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
-        self.engine.set_dist_schedule(int(os.environ.get("MNIST_AMD_DIST_SCHED", "1")))
+        # DDP schedule: 2 (fc bucket on its own communicator, overlapping across the step boundary)
+        # when a second communicator is given, else 1 (see csrc/runtime/engine.h)
+        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "2" if comm2 is not None else "1"))
+        self.engine.set_dist_schedule(sched)
         if comm is not None:
             self.engine.attach_comm(comm)
-        self.comm = comm
+        if comm2 is not None:
+            self.engine.attach_comm2(comm2)
+        self.comm, self.comm2 = comm, comm2
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None
         self.use_graphs = self.graph_steps > 0

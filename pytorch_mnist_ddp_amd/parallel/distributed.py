@@ -86,3 +86,10 @@ def get_world_size() -> int:
 def barrier() -> None:
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
+
+
+def create_rccl_comms(world_size: int, rank: int, device: int, n: int = 2):
+    """``n`` independent framework communicators (the fused engine's DDP schedule 2 reduces the
+    conv bucket on the first and the fc bucket on the second, concurrently)."""
+    return [create_rccl_comm(world_size, rank, device, tag=str(i)) for i in range(n)]
+

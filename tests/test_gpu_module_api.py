@@ -137,17 +137,20 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         # stream overlapped with the conv backward, captured into graphs; must equal no-comm run
         C = native.load()
         comm = C.RcclComm(C.RcclComm.unique_id(), 1, 0, 0)
+        comm2 = C.RcclComm(C.RcclComm.unique_id(), 1, 0, 0)
         tr = load_mnist(synthetic_data=True, train=True, synthetic_size=1024, verbose=False)
         idx = torch.randperm(1024, generator=torch.Generator().manual_seed(0))
         res = []
-        for c in (comm, None):
+        # schedule 1 (one comm), schedule 2 (cross-step fc branch, two comms), eager schedule 2, no comm
+        for c, c2, gs in ((comm, None, 4), (comm, comm2, 4), (comm, comm2, 0), (None, None, 4)):
             torch.manual_seed(5)
             ms = ModelState(Net(), cuda_device)
-            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=4)
+            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=gs, comm2=c2)
             t.train_epoch(1, idx)
             t.synchronize()
             res.append(ms.param.clone())
-        assert torch.equal(res[0], res[1])
+        diffs = [(r - res[-1]).abs().max().item() for r in res]
+        assert all(d == 0 for d in diffs), diffs
     finally:
         dist.destroy_process_group()
 
