@@ -56,6 +56,12 @@ void launch_head_eval(const HeadArgs& a, int B, hipStream_t s);
 void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
 
 // ---------------- backward ----------------
+// Compact gradient wrt the conv2 output (the max-pool backward input): one record per (image,
+// pooled position) = 64 bf16 pooled gradients (already dropout-scaled, ReLU-masked) followed by
+// 64 argmax codes (2x2 window position, 0..3).  Dense dy[y][x][c] = (code == 2(y&1)+(x&1)) ? g : 0.
+constexpr int DYC_REC = 192, DYC_ROUTE = 128;
+constexpr int64_t DYC_BYTES_PER_IMAGE = (int64_t)NPOOL * DYC_REC;   // 27648
+
 struct FcBwdArgs {
   const uint16_t* dz1;        // bf16 [Bp][128]
   const uint16_t* p;          // bf16 [Bp][9216] (rows >= B are masked)
@@ -66,15 +72,16 @@ struct FcBwdArgs {
   const float* loss_rows;     // [B]
   const StepState* state;
   float* grad;                // flat fp32 grad buffer (writes fc1.w, fc1.b, fc2.w, fc2.b)
-  uint16_t* dy;               // bf16 [B][24][24][64] NHWC grad wrt conv2 output (dense, un-pooled)
+  uint8_t* dyc;               // compact grad wrt conv2 output: [B][144] records (see DYC_REC)
   float* loss_log;            // [steps] mean loss per step (indexed by state->step)
   float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
   float inv_batch;
 };
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
+void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s);   // profiling aid
 
 struct ConvBwdArgs {
-  const uint16_t* dy;         // bf16 [B][24][24][64] NHWC (written by fc_bwd)
+  const uint8_t* dyc;         // compact un-pooled gradient (written by fc_bwd role B)
   const uint16_t* a1;         // bf16 [B][26][26][32]
   const uint16_t* w2d;        // bf16 [9][32][64]
   const float* w1c;           // conv1 fp32 [32][9]

@@ -3,8 +3,8 @@
 // Replaces the autograd backward of reference mnist_ddp.py:50-55 (dropout1, max_pool2d, relu, conv2,
 // relu, conv1): max_pool2d_with_indices_backward, threshold_backward x2, convolution_backward x2.
 //
-//  * conv2_dgrad_kernel  (WG = image x strip of 7 conv1 rows): stages the dense un-pooled gradient dy
-//    (written by fc_bwd) into a zero-padded NHWC LDS tile with 16-B copies, runs the transposed
+//  * conv2_dgrad_kernel  (WG = image x strip of 7 conv1 rows): expands the compact un-pooled gradient
+//    (pooled grads + argmax codes written by fc_bwd) into a zero-padded NHWC LDS tile, runs the transposed
 //    convolution as an MFMA implicit GEMM (M = pixels, N = 32 ci, K = 9 taps x 64 co), applies the
 //    conv1 ReLU mask (stored bf16 a1 > 0, prefetched under the MFMA loop), and folds
 //    the conv1 weight/bias gradient into the epilogue as a second 16x16x16 MFMA fed straight
@@ -52,6 +52,30 @@ __device__ __forceinline__ int swz8(int row) { return row & 7; }
 __device__ __forceinline__ int swz_dy(int pix) { return (pix ^ (pix >> 1)) & 7; }
 }  // namespace
 
+// Expand one 16-B chunk of the compact un-pooled gradient (8 channels of one pooled position) to
+// the dense chunk of window pixel q (0..3): channel j keeps its value iff its argmax code == q.
+__device__ __forceinline__ uint4 dyc_expand(uint4 g, uint2 route, int q) {
+  // per route word (4 channels): 0xFF in the bytes whose code == q (SWAR zero-byte test), then
+  // v_perm_b32 doubles each byte into the 16-bit lane of its bf16
+  const uint32_t rep = (uint32_t)q * 0x01010101u;
+  uint32_t keep[2];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const uint32_t x = (w ? route.y : route.x) ^ rep;                        // 0 byte <=> match
+    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 <=> no match
+    keep[w] = ~((nz >> 7) * 0xFFu);                                            // 0xFF <=> match
+  }
+  uint4 o;
+  o.x = g.x & __builtin_amdgcn_perm(0u, keep[0], 0x01010000u);
+  o.y = g.y & __builtin_amdgcn_perm(0u, keep[0], 0x03030202u);
+  o.z = g.z & __builtin_amdgcn_perm(0u, keep[1], 0x01010000u);
+  o.w = g.w & __builtin_amdgcn_perm(0u, keep[1], 0x03030202u);
+  return o;
+}
+__device__ __forceinline__ const uint8_t* dyc_record(const uint8_t* dyc, int b, int y, int x) {
+  return dyc + (int64_t)b * DYC_BYTES_PER_IMAGE + ((y >> 1) * HP + (x >> 1)) * DYC_REC;
+}
+
 // One workgroup per CU, each owning >= 8 dy rows (B=200: 4800 rows -> 256 groups x 18-19 rows).
 // Monotonic in B, so a workspace sized for the largest batch fits every smaller one.
 int conv_wgrad_groups(int B) {
@@ -80,16 +104,22 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
   {
     constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
     uint4 v[8];
+    uint2 rt[8];
+    int qv[8];
     const uint4 z = {0u, 0u, 0u, 0u};
-    const uint16_t* dyb = a.dy + (int64_t)b * H2 * H2 * C2;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int c = tid + 256 * k;
       const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
       const int y = r0 - 2 + ly, x = col - 2;
       v[k] = z;
-      if (c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2)
-        v[k] = *reinterpret_cast<const uint4*>(dyb + (y * H2 + x) * C2 + c8 * 8);
+      rt[k] = uint2{0xFFFFFFFFu, 0xFFFFFFFFu};                    // no channel matches -> zero chunk
+      qv[k] = ((y & 1) << 1) | (x & 1);
+      if (c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2) {
+        const uint8_t* rec = dyc_record(a.dyc, b, y, x);
+        v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
+        rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
+      }
     }
     uint4 w[9];
     const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
@@ -114,7 +144,7 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
       const int c = tid + 256 * k;
       if (c < NCH) {
         const int row = c >> 3, c8 = c & 7;
-        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = v[k];
+        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = dyc_expand(v[k], rt[k], qv[k]);
       }
     }
 #pragma unroll
@@ -228,6 +258,7 @@ __device__ __forceinline__ int a1_row_of(int R) { return R + 2 * (R / H2); }
 
 struct WgradChunk {
   uint4 vd[WDY_V], va[WA1_V];
+  uint2 rt[WDY_V];
 };
 
 // Issue the global loads of chunk [c0, c1) into registers (zeros past the valid rows, so every LDS
@@ -236,13 +267,20 @@ __device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1
   const int ndy = (c1 - c0) * H2 * 8;                               // valid 16-B chunks of dy
   const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
   const int na1 = (A1 - A0) * H1 * 4;                               // valid 16-B chunks of a1
-  const uint4* dsrc = reinterpret_cast<const uint4*>(a.dy + (int64_t)c0 * H2 * C2);
   const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
   const uint4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int i = 0; i < WDY_V; ++i) {
     const int c = tid + WG_THREADS * i;
-    k.vd[i] = (c < ndy) ? dsrc[c] : z;
+    k.vd[i] = z;
+    k.rt[i] = uint2{0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (c < ndy) {                                  // dense chunk (pixel c>>3, channels 8(c&7)..)
+      const int pix = c >> 3, R = c0 + pix / H2, x = pix - (pix / H2) * H2;
+      const int bimg = R / H2, y = R - bimg * H2;
+      const uint8_t* rec = dyc_record(a.dyc, bimg, y, x);
+      k.vd[i] = *reinterpret_cast<const uint4*>(rec + (c & 7) * 16);
+      k.rt[i] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + (c & 7) * 8);
+    }
   }
 #pragma unroll
   for (int i = 0; i < WA1_V; ++i) {
@@ -251,14 +289,16 @@ __device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1
   }
 }
 
-__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, const WgradChunk& k, float* bsum) {
+__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0, const WgradChunk& k, float* bsum) {
   uint4* dys = reinterpret_cast<uint4*>(buf);
   uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
 #pragma unroll
   for (int i = 0; i < WDY_V; ++i) {
     const int c = tid + WG_THREADS * i, pix = c >> 3;
-    dys[pix * 8 + ((c & 7) ^ swz_dy(pix))] = k.vd[i];
-    const uint32_t w4[4] = {k.vd[i].x, k.vd[i].y, k.vd[i].z, k.vd[i].w};
+    const int R = c0 + pix / H2, x = pix - (pix / H2) * H2;
+    const uint4 d = dyc_expand(k.vd[i], k.rt[i], ((R & 1) << 1) | (x & 1));   // H2 even: y&1 == R&1
+    dys[pix * 8 + ((c & 7) ^ swz_dy(pix))] = d;
+    const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {          // conv2 bias gradient: this thread always holds channels 8*(tid&7)..
       bsum[2 * j] += bf2f((uint16_t)(w4[j] & 0xFFFF));
@@ -313,7 +353,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
   WgradChunk k;
   if (nchunks > 0) {
     wgrad_fetch(a, r0, min(r0 + WG_CH, r1), tid, k);
-    wgrad_store(smem, tid, k, bsum);
+    wgrad_store(smem, tid, r0, k, bsum);
   }
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -346,7 +386,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
         }
       }
     }
-    if (more) wgrad_store(smem + ((ch + 1) & 1) * WBUF_BYTES, tid, k, bsum);
+    if (more) wgrad_store(smem + ((ch + 1) & 1) * WBUF_BYTES, tid, c1, k, bsum);
     __syncthreads();
   }
   // slab layout = MFMA-native [co-tile 4][n-tile 18][lane 64][4]: one coalesced float4 per tile

@@ -127,6 +127,9 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   const uint64_t seed = a.state->seed;
   const uint64_t off = a.state->rng_base + 2ull * (uint64_t)step + 1ull;
   const bool no_drop = (a.state->flags & STEP_FLAG_NO_DROPOUT) != 0;
+  // the label is two dependent loads (index -> label): issue them before the row's 64 partial-sum
+  // loads so their latency overlaps instead of trailing the softmax
+  const int y = a.dlogp ? 0 : a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
   HeadRow r;
   head_forward_row(a, B, b, lane, true, no_drop, seed, off, r);
   float lp[NCLS];
@@ -140,7 +143,6 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) dl[c] = go[c] - expf(lp[c]) * sg;
   } else {
-    const int y = a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
     if (lane == 0) a.loss_rows[b] = -lp[y];
     // nll(mean) backward: go[c] = -[c==y]/B; log_softmax backward: go - exp(lp) * sum(go)
 #pragma unroll
@@ -171,12 +173,12 @@ __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + wave;
   if (b >= B) return;
+  const int y = a.labels ? a.labels[a.idx ? a.idx[b] : b] : -1;   // issued before the partial sums
   HeadRow r;
   head_forward_row(a, B, b, lane, false, true, 0, 0, r);
   float lp[NCLS];
   log_softmax10(r.logit, lp);
   if (lane == 0) {
-    const int y = a.labels ? a.labels[a.idx ? a.idx[b] : b] : -1;
     int am = 0;
 #pragma unroll
     for (int c = 1; c < NCLS; ++c) am = (lp[c] > lp[am]) ? c : am;
@@ -232,6 +234,19 @@ void launch_head_eval(const HeadArgs& a, int B, hipStream_t s) {
 // ============================================================================================
 namespace {
 constexpr int ROLE_A_WGS = NFLAT / 64 + 1;   // 145
+// k(=batch)-major LDS tiles read with ds_read_b64_tr_b16: one instruction touches rows
+// {8g+q (+4)} x one 32-B column segment per row, so without a swizzle every row of a 256-B
+// (128-B) row pitch lands on the same banks (8-way / 4-way).  XOR the 32-B segment index
+// (16 bf16) with a row code that is distinct over those 8 rows (gfx950: 2 x 32-lane groups,
+// bank = dword mod 64).  Writes (16-B chunks) apply the same map.
+__device__ __forceinline__ int swz_row256(int row, int col) {   // 128 bf16 per row, 8 segments
+  const int code = (row & 3) | (((row >> 3) & 1) << 2);
+  return (((col >> 4) ^ code) << 4) | (col & 15);
+}
+__device__ __forceinline__ int swz_row128(int row, int col) {   // 64 bf16 per row, 4 segments x 2 halves
+  const int code = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return (((col >> 4) ^ code) << 4) | (col & 15);
+}
 constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
 
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
@@ -267,23 +282,26 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
   for (int kb = 0; kb < nkb; ++kb) {
     uint16_t* dzs = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288);          // [32][128]
     uint16_t* ps = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288 + 8192);    // [32][64]
-    *reinterpret_cast<uint4*>(dzs + (tid >> 4) * 128 + (tid & 15) * 8) = rz0;
-    *reinterpret_cast<uint4*>(dzs + (16 + (tid >> 4)) * 128 + (tid & 15) * 8) = rz1;
-    *reinterpret_cast<uint4*>(ps + prow * 64 + pc8 * 8) = rp;
+    {
+      const int r0 = tid >> 4, r1 = 16 + (tid >> 4), c = (tid & 15) * 8;
+      *reinterpret_cast<uint4*>(dzs + r0 * 128 + swz_row256(r0, c)) = rz0;
+      *reinterpret_cast<uint4*>(dzs + r1 * 128 + swz_row256(r1, c)) = rz1;
+      *reinterpret_cast<uint4*>(ps + prow * 64 + swz_row128(prow, pc8 * 8)) = rp;
+    }
     if (kb + 1 < nkb) fetch(kb + 1);
     __syncthreads();
     const int rlo = 8 * g + q, rhi = rlo + 4;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int ob = 32 * wave + 16 * mt + 4 * pp;
-      const bf16x8 A = tr_frag(dzs + rlo * 128 + ob, dzs + rhi * 128 + ob);
+      const bf16x8 A = tr_frag(dzs + rlo * 128 + swz_row256(rlo, ob), dzs + rhi * 128 + swz_row256(rhi, ob));
       if (ones) {
         acc[mt][0] = mfma16x16x32(A, onesfrag, acc[mt][0]);
       } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int nb = 16 * nt + 4 * pp;
-          const bf16x8 Bf = tr_frag(ps + rlo * 64 + nb, ps + rhi * 64 + nb);
+          const bf16x8 Bf = tr_frag(ps + rlo * 64 + swz_row128(rlo, nb), ps + rhi * 64 + swz_row128(rhi, nb));
           acc[mt][nt] = mfma16x16x32(A, Bf, acc[mt][nt]);
         }
       }
@@ -305,32 +323,26 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
 }
 
 // B: gradient into the conv trunk.  WG = 16 batch rows x 4 consecutive pooled positions x 64 channels
-// (N = 256 columns of dz1 . w1).  The epilogue applies dropout-1 scale/keep, the ReLU (pooled > 0)
-// and max-pool routing (argmax) and writes the *dense* NHWC conv2-output gradient dy for the 2x8-pixel
-// footprint through LDS, so every global store is a full 1 KB row segment and the conv backward
-// kernels stage dy with plain 16-byte copies.
+// (N = 256 columns of dz1 . w1).  The epilogue applies dropout-1 scale/keep and the ReLU (pooled > 0)
+// and writes the *compact* un-pooled gradient: one 192-B record per (image, pooled position) =
+// 64 bf16 pooled gradients + 64 argmax codes (DYC_* in kernels.h).  The conv backward kernels expand
+// it into the dense NHWC tile while staging, so the 75 %-zero dense map never touches HBM.
 __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb, unsigned char* smem) {
-  uint8_t* pms = smem;                                          // [16 b][64 c][4 j]
-  uint16_t* dyst = reinterpret_cast<uint16_t*>(smem + 4096);    // [16 b][2 y][8 x][64 c]
+  uint8_t* pms = smem;                                 // [16 b][64 c][4 j]
+  unsigned char* recs = smem + 4096;                   // [16 b][4 j] records of DYC_REC bytes
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m = lane & 15, kg = lane >> 4;
   const int bb = rb / ROLE_B_SBLOCKS, sb = rb - bb * ROLE_B_SBLOCKS;
-  const int py = sb / 3, px0 = (sb - py * 3) * 4;
-  const int s0 = py * HP + px0;
+  const int s0 = sb * 4;                               // 4 consecutive pooled positions (row-major 12x12)
   const int b0 = bb * 16;
   const float dscale = (a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT)) ? 1.0f : (1.0f / KEEP1);
-  // pmask tile (4 consecutive pooled positions per (b, c) = one u32) + zero the dy staging tile
+  // pmask tile (4 consecutive pooled positions per (b, c) = one u32)
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
     uint32_t v = 0;
     if (b0 + bl < B) v = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)(b0 + bl) * NFLAT + c * NPOOL + s0);
     reinterpret_cast<uint32_t*>(pms)[idx] = v;
-  }
-  {
-    const uint4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) reinterpret_cast<uint4*>(dyst)[tid + 256 * k] = z;
   }
   // MFMA: wave w owns pooled position s0 + w, 4 N-tiles = 64 channels; K = 128
   floatx4 acc[4];
@@ -354,18 +366,20 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
     for (int r = 0; r < 4; ++r) {
       const int bl = 4 * kg + r, c = 16 * nt + m;
       const int mk = pms[(bl * 64 + c) * 4 + wave];
-      if ((mk & 12) == 12) {
-        const int yl = (mk >> 1) & 1, xl = 2 * wave + (mk & 1);
-        dyst[((bl * 2 + yl) * 8 + xl) * 64 + c] = f2bf(acc[nt][r] * dscale);
-      }
+      const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;   // kept by dropout and ReLU alive
+      unsigned char* rec = recs + (bl * 4 + wave) * DYC_REC;
+      reinterpret_cast<uint16_t*>(rec)[c] = f2bf(v);
+      rec[DYC_ROUTE + c] = (uint8_t)(mk & 3);
     }
   __syncthreads();
+  // 16 runs of 4 contiguous records (768 B) -> 48 x 16 B per image row, 3 per thread
+  constexpr int RUN16 = 4 * DYC_REC / 16;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int cidx = tid + 256 * k, bl = cidx >> 7, yl = (cidx >> 6) & 1, off = cidx & 63;
+  for (int k = 0; k < 3; ++k) {
+    const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
     if (b0 + bl < B) {
-      uint4* dst = reinterpret_cast<uint4*>(a.dy + (((int64_t)(b0 + bl) * H2 + 2 * py + yl) * H2 + 2 * px0) * C2);
-      dst[off] = reinterpret_cast<const uint4*>(dyst)[cidx];
+      uint4* dst = reinterpret_cast<uint4*>(a.dyc + ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC);
+      dst[off] = reinterpret_cast<const uint4*>(recs)[cidx];
     }
   }
 }
@@ -395,7 +409,7 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
       const int c = lane + 64 * j, row = c >> 4, c16 = c & 15;
       uint4 v = {0u, 0u, 0u, 0u};
       if (active) v = *reinterpret_cast<const uint4*>(a.h_bf + (int64_t)(kb * 32 + row) * NH + c16 * 8);
-      *reinterpret_cast<uint4*>(hs + row * 128 + c16 * 8) = v;
+      *reinterpret_cast<uint4*>(hs + row * 128 + swz_row256(row, c16 * 8)) = v;
     }
     {
       const int row = lane >> 1, c8 = lane & 1;
@@ -409,7 +423,7 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       const int nb = 16 * nt + 4 * pp;
-      const bf16x8 Bf = tr_frag(hs + rlo * 128 + nb, hs + rhi * 128 + nb);
+      const bf16x8 Bf = tr_frag(hs + rlo * 128 + swz_row256(rlo, nb), hs + rhi * 128 + swz_row256(rhi, nb));
       acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
     }
     acc[8] = mfma16x16x32(A, onesfrag, acc[8]);
@@ -441,9 +455,9 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp) {
+__global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
-  const int bid = blockIdx.x;
+  const int bid = blockIdx.x + bid0;
   const int nb_roles = 0;
   // role C (one long-running WG) first so it is dispatched before the short role-B tiles
   if (bid == 0) {
@@ -458,7 +472,15 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp)
 
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
   const int grid = 1 + ROLE_A_WGS + ((B + 15) / 16) * ROLE_B_SBLOCKS;
-  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp);
+  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+}
+
+// profiling aid: one role of fc_bwd on its own (0 = C, 1 = A, 2 = B)
+void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s) {
+  const int nb = ((B + 15) / 16) * ROLE_B_SBLOCKS;
+  const int grid = role == 0 ? 1 : role == 1 ? ROLE_A_WGS : nb;
+  const int bid0 = role == 0 ? 0 : role == 1 ? 1 : 1 + ROLE_A_WGS;
+  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
 }
 
 }  // namespace mnist

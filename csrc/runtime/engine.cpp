@@ -55,7 +55,7 @@ void Engine::alloc_workspace() {
   const int64_t o_dz = carve((int64_t)Mp * NH * 2);
   const int64_t o_h = carve((int64_t)Mp * NH * 2);
   const int64_t o_dl = carve((int64_t)Mp * 16 * 2);
-  const int64_t o_g = carve((int64_t)M * H2 * H2 * C2 * 2);   // dense dy
+  const int64_t o_g = carve((int64_t)M * DYC_BYTES_PER_IMAGE);   // compact dy records
   const int64_t o_c1 = carve((int64_t)4 * M * 320 * 4);
   const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
   ws_bytes_ = off;
@@ -70,7 +70,7 @@ void Engine::alloc_workspace() {
   dz1_ = reinterpret_cast<uint16_t*>(base + o_dz);
   h_bf_ = reinterpret_cast<uint16_t*>(base + o_h);
   dl_bf_ = reinterpret_cast<uint16_t*>(base + o_dl);
-  dy_ = reinterpret_cast<uint16_t*>(base + o_g);
+  dyc_ = reinterpret_cast<uint8_t*>(base + o_g);
   c1part_ = reinterpret_cast<float*>(base + o_c1);
   w2part_ = reinterpret_cast<float*>(base + o_w2);
 }
@@ -112,14 +112,14 @@ void Engine::enqueue_step(int batch, bool last) {
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
-  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, dy_,
+  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, dyc_,
                buf_.loss_log, gscale, 1.0f / (float)B};
   launch_fc_bwd(fb, B, Bp, compute_);
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
   const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
-  ConvBwdArgs cb{dy_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
+  ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
                  buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
   AdadeltaArgs adc = ad;

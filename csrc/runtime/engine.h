@@ -108,7 +108,8 @@ class Engine {
   // workspace
   int64_t ws_bytes_ = 0;
   void* ws_ = nullptr;
-  uint16_t *a1_, *p_, *dz1_, *h_bf_, *dl_bf_, *dy_;
+  uint16_t *a1_, *p_, *dz1_, *h_bf_, *dl_bf_;
+  uint8_t* dyc_;                     // compact un-pooled gradient records (DYC_REC per pooled position)
   uint8_t* pmask_;
   float *z1part_, *loss_rows_, *c1part_, *w2part_;
   std::vector<hipGraphExec_t> graphs_;

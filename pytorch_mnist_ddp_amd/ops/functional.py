@@ -39,7 +39,7 @@ class StepBuffers:
     dz1: torch.Tensor         # bf16 [Bp64, 128]
     h_bf: torch.Tensor        # bf16 [Bp64, 128]
     dl_bf: torch.Tensor       # bf16 [Bp64, 16]
-    dy: torch.Tensor          # bf16 [B,24,24,64] dense NHWC grad wrt conv2 output
+    dyc: torch.Tensor         # uint8 [B, 144*192] compact grad wrt conv2 output (pooled grads + argmax)
     c1part: torch.Tensor      # f32 [4B, 320]
     w2part: torch.Tensor      # f32 [G, 18496]
     correct: torch.Tensor     # i32 [B]
@@ -62,7 +62,7 @@ class StepBuffers:
             dz1=torch.zeros(Bp, NH, **bf),
             h_bf=torch.zeros(Bp, NH, **bf),
             dl_bf=torch.zeros(Bp, 16, **bf),
-            dy=torch.zeros(B, 24, 24, 64, **bf),
+            dyc=torch.zeros(B, 144 * 192, dtype=torch.uint8, device=device),
             c1part=torch.zeros(4 * B, 320, dtype=torch.float32, **z),
             w2part=torch.zeros(G, 18432 + 64, dtype=torch.float32, **z),
             correct=torch.zeros(B, dtype=torch.int32, **z),
@@ -103,13 +103,13 @@ def fc_bwd(ms, buf: StepBuffers, grad_scale: float = 1.0, loss_log: torch.Tensor
     p = native.ptr
     B = buf.B
     _C().fc_bwd(p(buf.dz1), p(buf.p), p(buf.pmask), p(ms.w1t), p(buf.h_bf), p(buf.dl_bf), p(buf.loss_rows),
-                p(ms.state), p(ms.grad), p(buf.dy), p(loss_log), grad_scale, 1.0 / B, B, round_up(B, 32), _s())
+                p(ms.state), p(ms.grad), p(buf.dyc), p(loss_log), grad_scale, 1.0 / B, B, round_up(B, 32), _s())
 
 
 def conv_bwd(ms, data_u8: torch.Tensor, idx: torch.Tensor, buf: StepBuffers, grad_scale: float = 1.0,
              idx_stride: int = 0) -> None:
     p, o = native.ptr, ms.offsets
-    _C().conv_bwd(p(buf.dy), p(buf.a1), p(ms.w2d), p(ms.param) + 4 * o["conv1.weight"],
+    _C().conv_bwd(p(buf.dyc), p(buf.a1), p(ms.w2d), p(ms.param) + 4 * o["conv1.weight"],
                   p(ms.param) + 4 * o["conv1.bias"], p(data_u8), p(idx), idx_stride, p(ms.state),
                   p(buf.c1part), p(buf.w2part), p(ms.grad), grad_scale, buf.B, _s())
 
@@ -137,3 +137,18 @@ def eval_forward(ms, data_u8, labels, idx, buf: StepBuffers) -> None:
     trunk_fwd(ms, data_u8, idx, buf, False)
     fc1_fwd(ms, buf)
     head_eval(ms, labels, idx, buf)
+
+
+def dense_dy(buf: StepBuffers) -> torch.Tensor:
+    """Expand the compact un-pooled gradient records to the dense NHWC bf16 [B,24,24,64] map
+    (what the conv backward kernels stage in LDS); for tests and tools."""
+    B = buf.B
+    rec = buf.dyc.view(B, 12, 12, 192)
+    g = rec[..., :128].contiguous().view(torch.bfloat16).view(B, 12, 12, 64)
+    code = rec[..., 128:].long()                                    # [B,12,12,64] window position
+    dense = torch.zeros(B, 12, 2, 12, 2, 64, dtype=torch.bfloat16, device=g.device)
+    for q in range(4):
+        sel = (code == q)
+        dense[:, :, q >> 1, :, q & 1, :] = torch.where(sel, g, torch.zeros_like(g))
+    return dense.view(B, 24, 24, 64)
+

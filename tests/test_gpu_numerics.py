@@ -163,7 +163,7 @@ def test_backward_kernels_stagewise_exact(cuda_device, B):
     bi = torch.arange(B).view(B, 1, 1, 1).expand(B, 64, 12, 12)
     ci = torch.arange(64).view(1, 64, 1, 1).expand(B, 64, 12, 12)
     dy_ref[bi, ci, py, px] = g_ref
-    dy = buf.dy.cpu().double().permute(0, 3, 1, 2)          # NHWC -> NCHW
+    dy = Fk.dense_dy(buf).cpu().double().permute(0, 3, 1, 2)   # compact records -> dense NCHW
     mism = (dy != dy_ref).double().mean().item()
     assert mism < 1e-3 and rel_err(dy, dy_ref) < 1e-3, mism
     a1 = buf.a1.cpu().double().permute(0, 3, 1, 2)          # NHWC -> NCHW
