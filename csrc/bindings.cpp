@@ -122,18 +122,21 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("fc_bwd", [](uintptr_t dz1, uintptr_t p, uintptr_t pmask, uintptr_t w1t, uintptr_t h_bf, uintptr_t dl_bf,
                      uintptr_t loss_rows, uintptr_t state, uintptr_t grad, uintptr_t dyc, uintptr_t loss_log,
-                     float grad_scale, float inv_batch, int B, int Bp, uintptr_t stream, int role) {
+                     float grad_scale, float inv_batch, int B, int Bp, uintptr_t stream, int role,
+                     uintptr_t part) {
     FcBwdArgs a{P<const uint16_t>(dz1), P<const uint16_t>(p), P<const uint8_t>(pmask), P<const uint16_t>(w1t),
                 P<const uint16_t>(h_bf), P<const uint16_t>(dl_bf), P<const float>(loss_rows),
                 P<const StepState>(state), P<float>(grad), P<uint8_t>(dyc), P<float>(loss_log), grad_scale,
-                inv_batch};
+                inv_batch, P<float>(part)};
     if (role < 0) launch_fc_bwd(a, B, Bp, S(stream));
     else launch_fc_bwd_role(a, B, Bp, role, S(stream));
     check_launch();
   }, py::arg("dz1"), py::arg("p"), py::arg("pmask"), py::arg("w1t"), py::arg("h_bf"), py::arg("dl_bf"),
      py::arg("loss_rows"), py::arg("state"), py::arg("grad"), py::arg("dyc"), py::arg("loss_log"),
      py::arg("grad_scale"), py::arg("inv_batch"), py::arg("B"), py::arg("Bp"), py::arg("stream"),
-     py::arg("role") = -1);
+     py::arg("role") = -1, py::arg("part") = 0);
+  m.def("fc_bwd_splits", &fc_bwd_splits);
+  m.attr("FCB_PART_STRIDE") = FCB_PART_STRIDE;
   m.def("conv_bwd", [](uintptr_t dyc, uintptr_t a1, uintptr_t w2d, uintptr_t w1c, uintptr_t b1c,
                        uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t c1part,
                        uintptr_t w2part, uintptr_t grad, float grad_scale, int B, uintptr_t stream,

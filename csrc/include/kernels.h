@@ -26,12 +26,15 @@ struct TrunkFwdArgs {
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
 
 // fc1 split-K partial GEMM: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
-constexpr int FC1_KSPLIT = 32;
+constexpr int FC1_KSPLIT = 32;            // small batches: 16-row tiles, fragments straight from HBM/L2
+constexpr int FC1_KSPLIT_BIG = 4;         // B >= FC1_BIG_MIN_B: 64x128 LDS-staged tiles, K/4 each
+constexpr int FC1_BIG_MIN_B = 512;
+__host__ __device__ inline int fc1_ksplit(int B) { return B >= FC1_BIG_MIN_B ? FC1_KSPLIT_BIG : FC1_KSPLIT; }
 void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s);
 
 // Head: reduce fc1 partials + bias -> ReLU -> dropout(0.5) -> fc2 -> log_softmax (+ NLL + backward)
 struct HeadArgs {
-  const float* z1part;        // [FC1_KSPLIT][B][128]
+  const float* z1part;        // [fc1_ksplit(B)][B][128]
   const float* b_fc1;         // [128]
   const float* w_fc2;         // [10][128] fp32
   const float* b_fc2;         // [10]
@@ -76,7 +79,18 @@ struct FcBwdArgs {
   float* loss_log;            // [steps] mean loss per step (indexed by state->step)
   float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
   float inv_batch;
+  float* part;                // B > FC_BWD_SPLIT_ROWS: [fc_bwd_splits(B)][FCB_PART_STRIDE] partial fc grads
 };
+// Large batches split the batch (= K of the fc weight gradients) over fc_bwd_splits(B) groups of
+// workgroups writing fp32 partials that fc_grad_reduce sums in fixed order; B <= 1024 writes the
+// gradients directly.  Role B processes FCB_MR(B) 16-row tiles per workgroup (w1 slice kept in VGPRs).
+constexpr int FC_BWD_SPLIT_ROWS = 1024;
+__host__ __device__ inline int fc_bwd_splits(int B) { return (B + FC_BWD_SPLIT_ROWS - 1) / FC_BWD_SPLIT_ROWS; }
+__host__ __device__ inline int fcb_mr(int B) { return B >= 2048 ? 8 : B >= 512 ? 2 : 1; }
+// partial layout per split: fc1.w [128][9216], fc1.b [128], fc2.w [10][128], fc2.b [10], loss sum, pad
+constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_PART_B1 + 128,
+                  FCB_PART_B2 = FCB_PART_W2 + 1280, FCB_PART_LOSS = FCB_PART_B2 + 10,
+                  FCB_PART_STRIDE = (FCB_PART_LOSS + 1 + 63) / 64 * 64;
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s);   // profiling aid
 

@@ -6,6 +6,8 @@
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
+#include <stdexcept>
+
 namespace mnist {
 
 // ============================================================================================
@@ -52,7 +54,117 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
   }
 }
 
+// Large batches: 64 rows x 128 columns per workgroup, K split 4 ways (2304 = 36 stages of 64),
+// A [64][64] and B [128][64] bf16 stages double-buffered in LDS (128-B rows, chunk ^ (row>>1 & 7)
+// swizzle: conflict-free ds_read_b128 fragment reads), next stage prefetched into VGPRs.  Each wave
+// owns 32 rows x 64 columns (2 x 4 MFMA tiles): w1 is read from L2 once per 64 rows, not per 16.
+namespace {
+constexpr int F1B_ROWS = 64, F1B_KS = 64;
+constexpr int F1B_KC = NFLAT / FC1_KSPLIT_BIG;            // 2304
+constexpr int F1B_STAGES = F1B_KC / F1B_KS;               // 36
+constexpr int F1B_ABYTES = F1B_ROWS * F1B_KS * 2;         // 8192
+constexpr int F1B_BBYTES = NH * F1B_KS * 2;               // 16384
+constexpr int F1B_STAGE = F1B_ABYTES + F1B_BBYTES;        // 24576
+__device__ __forceinline__ int f1b_swz(int row) { return (row >> 1) & 7; }
+}  // namespace
+
+__global__ __launch_bounds__(256) void fc1_fwd_big_kernel(const uint16_t* __restrict__ p,
+                                                          const uint16_t* __restrict__ w1,
+                                                          float* __restrict__ z1part, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * F1B_STAGE];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m = lane & 15, kg = lane >> 4;
+  const int r0 = blockIdx.x * F1B_ROWS, split = blockIdx.y;
+  const int kbase = split * F1B_KC;
+  const int wr = 32 * (wave & 1), wc = 64 * (wave >> 1);
+  // staging map: A 512 chunks (2/thread), B 1024 chunks (4/thread); chunk = (row, 16-B column)
+  uint4 ra0, ra1, rb0, rb1, rb2, rb3;
+#define F1B_FETCH(st)                                                                             \
+  {                                                                                               \
+    const int k0 = kbase + (st) * F1B_KS;                                                         \
+    const int ar0 = tid >> 3, ar1 = (tid + 256) >> 3, cc = tid & 7;                               \
+    ra0 = (r0 + ar0 < B) ? *reinterpret_cast<const uint4*>(p + (int64_t)(r0 + ar0) * NFLAT + k0 + cc * 8) \
+                         : uint4{0u, 0u, 0u, 0u};                                                 \
+    ra1 = (r0 + ar1 < B) ? *reinterpret_cast<const uint4*>(p + (int64_t)(r0 + ar1) * NFLAT + k0 + cc * 8) \
+                         : uint4{0u, 0u, 0u, 0u};                                                 \
+    rb0 = *reinterpret_cast<const uint4*>(w1 + (int64_t)(tid >> 3) * NFLAT + k0 + cc * 8);          \
+    rb1 = *reinterpret_cast<const uint4*>(w1 + (int64_t)((tid + 256) >> 3) * NFLAT + k0 + cc * 8);  \
+    rb2 = *reinterpret_cast<const uint4*>(w1 + (int64_t)((tid + 512) >> 3) * NFLAT + k0 + cc * 8);  \
+    rb3 = *reinterpret_cast<const uint4*>(w1 + (int64_t)((tid + 768) >> 3) * NFLAT + k0 + cc * 8);  \
+  }
+#define F1B_STORE(buf)                                                                            \
+  {                                                                                               \
+    uint4* as_ = reinterpret_cast<uint4*>(smem + (buf) * F1B_STAGE);                              \
+    uint4* bs_ = reinterpret_cast<uint4*>(smem + (buf) * F1B_STAGE + F1B_ABYTES);                 \
+    const int cc = tid & 7;                                                                       \
+    int row = tid >> 3;                                                                           \
+    as_[row * 8 + (cc ^ f1b_swz(row))] = ra0;                                                     \
+    bs_[row * 8 + (cc ^ f1b_swz(row))] = rb0;                                                     \
+    row += 32;                                                                                    \
+    as_[row * 8 + (cc ^ f1b_swz(row))] = ra1;                                                     \
+    bs_[row * 8 + (cc ^ f1b_swz(row))] = rb1;                                                     \
+    row += 32;                                                                                    \
+    bs_[row * 8 + (cc ^ f1b_swz(row))] = rb2;                                                     \
+    row += 32;                                                                                    \
+    bs_[row * 8 + (cc ^ f1b_swz(row))] = rb3;                                                     \
+  }
+  floatx4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  F1B_FETCH(0);
+  F1B_STORE(0);
+  __syncthreads();
+  for (int st = 0; st < F1B_STAGES; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < F1B_STAGES) F1B_FETCH(st + 1);               // in flight under this stage's MFMAs
+    const uint16_t* as = reinterpret_cast<const uint16_t*>(smem + buf * F1B_STAGE);
+    const uint16_t* bs = reinterpret_cast<const uint16_t*>(smem + buf * F1B_STAGE + F1B_ABYTES);
+#pragma unroll
+    for (int t = 0; t < F1B_KS / 32; ++t) {
+      const int ch = 4 * t + kg;
+      bf16x8 A[2], Bf[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr + 16 * i + m;
+        A[i] = ld16(as + row * F1B_KS + ((ch ^ f1b_swz(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wc + 16 * j + m;
+        Bf[j] = ld16(bs + row * F1B_KS + ((ch ^ f1b_swz(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(A[i], Bf[j], acc[i][j]);
+    }
+    if (st + 1 < F1B_STAGES) F1B_STORE(buf ^ 1);
+    __syncthreads();
+  }
+#undef F1B_FETCH
+#undef F1B_STORE
+  // C fragment: row = 4*(lane>>4) + r, col = lane & 15
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = r0 + wr + 16 * i + 4 * kg + r;
+      if (b < B) {
+        float* dst = z1part + ((int64_t)split * B + b) * NH + wc + m;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[16 * j] = acc[i][j][r];
+      }
+    }
+}
+
 void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s) {
+  if (fc1_ksplit(B) == FC1_KSPLIT_BIG) {
+    hipLaunchKernelGGL(fc1_fwd_big_kernel, dim3((B + F1B_ROWS - 1) / F1B_ROWS, FC1_KSPLIT_BIG), dim3(256), 0, s,
+                       p, w1, z1part, B);
+    return;
+  }
   dim3 grid((B + 15) / 16, FC1_KSPLIT);
   hipLaunchKernelGGL(fc1_fwd_kernel, grid, dim3(256), 0, s, p, w1, z1part, B);
 }
@@ -75,8 +187,13 @@ __device__ __forceinline__ void head_forward_row(const HeadArgs& a, int B, int b
     float z = a.b_fc1[o];
     // torch adds the bias after the GEMM; the partial sums are accumulated in fixed chunk order
     float s = 0.f;
+    if (fc1_ksplit(B) == FC1_KSPLIT) {
 #pragma unroll
-    for (int c = 0; c < FC1_KSPLIT; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
+      for (int c = 0; c < FC1_KSPLIT; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
+    } else {
+#pragma unroll
+      for (int c = 0; c < FC1_KSPLIT_BIG; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
+    }
     z += s;
     r.z[j] = z;
     float h = fmaxf(z, 0.0f);
@@ -251,7 +368,8 @@ constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions 
 
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
 // loaded into VGPRs while the current one (double-buffered LDS) feeds the MFMAs; one barrier per slab.
-__device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, unsigned char* smem) {
+__device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, int sp, int S,
+                                              unsigned char* smem) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const bool ones = (ib == NFLAT / 64);
@@ -268,7 +386,9 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
     us8 v = {one, one, one, one, one, one, one, one};
     onesfrag = __builtin_bit_cast(bf16x8, v);
   }
-  const int nkb = Bp / 32;
+  // this split's k(=batch) blocks of 32 rows
+  const int kb0 = sp * (FC_BWD_SPLIT_ROWS / 32);
+  const int kb1 = min(Bp / 32, kb0 + FC_BWD_SPLIT_ROWS / 32);
   const int prow = tid >> 3, pc8 = tid & 7;
   uint4 rz0, rz1, rp = {0u, 0u, 0u, 0u};
   auto fetch = [&](int kb) {
@@ -278,8 +398,8 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
     rp = uint4{0u, 0u, 0u, 0u};
     if (!ones && b < B) rp = *reinterpret_cast<const uint4*>(a.p + (int64_t)b * NFLAT + i0 + pc8 * 8);
   };
-  fetch(0);
-  for (int kb = 0; kb < nkb; ++kb) {
+  fetch(kb0);
+  for (int kb = kb0; kb < kb1; ++kb) {
     uint16_t* dzs = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288);          // [32][128]
     uint16_t* ps = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288 + 8192);    // [32][64]
     {
@@ -288,7 +408,7 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
       *reinterpret_cast<uint4*>(dzs + r1 * 128 + swz_row256(r1, c)) = rz1;
       *reinterpret_cast<uint4*>(ps + prow * 64 + swz_row128(prow, pc8 * 8)) = rp;
     }
-    if (kb + 1 < nkb) fetch(kb + 1);
+    if (kb + 1 < kb1) fetch(kb + 1);
     __syncthreads();
     const int rlo = 8 * g + q, rhi = rlo + 4;
 #pragma unroll
@@ -312,12 +432,15 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = 32 * wave + 16 * mt + 4 * g + r;
+      // S == 1: final (scaled) gradient; S > 1: unscaled partial in the same layout (fc_grad_reduce)
+      float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
+      const float sc = (S == 1) ? a.grad_scale : 1.0f;
       if (ones) {
-        if ((lane & 15) == 0) a.grad[OFF_FC1_B + o] = acc[mt][0][r] * a.grad_scale;
+        if ((lane & 15) == 0) dst[OFF_FC1_B + o] = acc[mt][0][r] * sc;
       } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
-          a.grad[OFF_FC1_W + (int64_t)o * NFLAT + i0 + 16 * nt + (lane & 15)] = acc[mt][nt][r] * a.grad_scale;
+          dst[OFF_FC1_W + (int64_t)o * NFLAT + i0 + 16 * nt + (lane & 15)] = acc[mt][nt][r] * sc;
       }
     }
 }
@@ -327,64 +450,81 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
 // and writes the *compact* un-pooled gradient: one 192-B record per (image, pooled position) =
 // 64 bf16 pooled gradients + 64 argmax codes (DYC_* in kernels.h).  The conv backward kernels expand
 // it into the dense NHWC tile while staging, so the 75 %-zero dense map never touches HBM.
-__device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb, unsigned char* smem) {
+template <bool CACHE_W>
+__device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb, int MR,
+                                              unsigned char* smem) {
   uint8_t* pms = smem;                                 // [16 b][64 c][4 j]
   unsigned char* recs = smem + 4096;                   // [16 b][4 j] records of DYC_REC bytes
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m = lane & 15, kg = lane >> 4;
   const int bb = rb / ROLE_B_SBLOCKS, sb = rb - bb * ROLE_B_SBLOCKS;
   const int s0 = sb * 4;                               // 4 consecutive pooled positions (row-major 12x12)
-  const int b0 = bb * 16;
   const float dscale = (a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT)) ? 1.0f : (1.0f / KEEP1);
-  // pmask tile (4 consecutive pooled positions per (b, c) = one u32)
+  // large batches (CACHE_W): this wave's w1 slice (pooled position s0 + wave, 64 channels, K = 128)
+  // stays in VGPRs for all MR row tiles of the workgroup; small batches (MR = 1) stream it, which
+  // keeps the kernel at 3 workgroups per CU
+  bf16x8 Bw[CACHE_W ? NH / 32 : 1][4];
+  if (CACHE_W) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
-    uint32_t v = 0;
-    if (b0 + bl < B) v = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)(b0 + bl) * NFLAT + c * NPOOL + s0);
-    reinterpret_cast<uint32_t*>(pms)[idx] = v;
+    for (int ks = 0; ks < (CACHE_W ? NH / 32 : 1); ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        Bw[ks][nt] = ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
   }
-  // MFMA: wave w owns pooled position s0 + w, 4 N-tiles = 64 channels; K = 128
-  floatx4 acc[4];
+  for (int t = 0; t < MR; ++t) {
+    const int b0 = (bb * MR + t) * 16;
+    if (b0 >= B) break;                                // workgroup-uniform
+    // pmask tile (4 consecutive pooled positions per (b, c) = one u32)
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;
-#pragma unroll
-  for (int ks = 0; ks < NH / 32; ++ks) {
-    const bf16x8 A = ld16(arow + ks * 32);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int c = 16 * nt + m;
-      const bf16x8 Bf = ld16(a.w1t + (int64_t)(c * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
-      acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
+    for (int k = 0; k < 4; ++k) {
+      const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
+      uint32_t v = 0;
+      if (b0 + bl < B) v = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)(b0 + bl) * NFLAT + c * NPOOL + s0);
+      reinterpret_cast<uint32_t*>(pms)[idx] = v;
     }
-  }
-  __syncthreads();
+    floatx4 acc[4];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int bl = 4 * kg + r, c = 16 * nt + m;
-      const int mk = pms[(bl * 64 + c) * 4 + wave];
-      const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;   // kept by dropout and ReLU alive
-      unsigned char* rec = recs + (bl * 4 + wave) * DYC_REC;
-      reinterpret_cast<uint16_t*>(rec)[c] = f2bf(v);
-      rec[DYC_ROUTE + c] = (uint8_t)(mk & 3);
+    for (int ks = 0; ks < NH / 32; ++ks) {
+      const bf16x8 A = ld16(arow + ks * 32);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 Bf = CACHE_W ? Bw[CACHE_W ? ks : 0][nt]
+                                  : ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
+        acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
+      }
     }
-  __syncthreads();
-  // 16 runs of 4 contiguous records (768 B) -> 48 x 16 B per image row, 3 per thread
-  constexpr int RUN16 = 4 * DYC_REC / 16;
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
-    if (b0 + bl < B) {
-      uint4* dst = reinterpret_cast<uint4*>(a.dyc + ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC);
-      dst[off] = reinterpret_cast<const uint4*>(recs)[cidx];
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int bl = 4 * kg + r, c = 16 * nt + m;
+        const int mk = pms[(bl * 64 + c) * 4 + wave];
+        const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;   // kept by dropout, ReLU alive
+        unsigned char* rec = recs + (bl * 4 + wave) * DYC_REC;
+        reinterpret_cast<uint16_t*>(rec)[c] = f2bf(v);
+        rec[DYC_ROUTE + c] = (uint8_t)(mk & 3);
+      }
+    __syncthreads();
+    // 16 runs of 4 contiguous records (768 B) -> 48 x 16 B per image row, 3 per thread
+    constexpr int RUN16 = 4 * DYC_REC / 16;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
+      if (b0 + bl < B) {
+        uint4* dst = reinterpret_cast<uint4*>(a.dyc + ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC);
+        dst[off] = reinterpret_cast<const uint4*>(recs)[cidx];
+      }
     }
+    if (t + 1 < MR) __syncthreads();                   // pms / recs are rewritten by the next tile
   }
 }
 
-__device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp, unsigned char* smem) {
+__device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp, int sp, int S,
+                                              unsigned char* smem) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem + wave * 9216);          // [32][128]
@@ -399,11 +539,12 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
     us8 v = {one, one, one, one, one, one, one, one};
     onesfrag = __builtin_bit_cast(bf16x8, v);
   }
-  const int nkb = Bp / 32;
-  const int iters = (nkb + 3) / 4;
+  const int kb0 = sp * (FC_BWD_SPLIT_ROWS / 32);
+  const int kb1 = min(Bp / 32, kb0 + FC_BWD_SPLIT_ROWS / 32);
+  const int iters = (kb1 - kb0 + 3) / 4;
   for (int it = 0; it < iters; ++it) {
-    const int kb = it * 4 + wave;
-    const bool active = kb < nkb;
+    const int kb = kb0 + it * 4 + wave;
+    const bool active = kb < kb1;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = lane + 64 * j, row = c >> 4, c16 = c & 15;
@@ -441,46 +582,95 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
     const int ln = e & 63, r = (e >> 6) & 3, nt = e >> 8;
     const int c = 4 * (ln >> 4) + r;        // row of the 16x16 output = class
     const int col = ln & 15;
+    float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
+    const float sc = (S == 1) ? a.grad_scale : 1.0f;
     if (c < NCLS) {
-      if (nt < 8) a.grad[OFF_FC2_W + c * NH + 16 * nt + col] = s * a.grad_scale;
-      else if (col == 0) a.grad[OFF_FC2_B + c] = s * a.grad_scale;
+      if (nt < 8) dst[OFF_FC2_W + c * NH + 16 * nt + col] = s * sc;
+      else if (col == 0) dst[OFF_FC2_B + c] = s * sc;
     }
   }
   if (wave == 0) {
+    const int b_lo = sp * FC_BWD_SPLIT_ROWS, b_hi = min(B, b_lo + FC_BWD_SPLIT_ROWS);
     float s = 0.f;
-    for (int b = lane; b < B; b += 64) s += a.loss_rows[b];
+    for (int b = b_lo + lane; b < b_hi; b += 64) s += a.loss_rows[b];
     s = wave_sum(s);
-    if (lane == 0 && a.loss_log) a.loss_log[a.state->step] = s / (float)B;
+    if (lane == 0) {
+      if (S == 1) {
+        if (a.loss_log) a.loss_log[a.state->step] = s / (float)B;
+      } else {
+        a.part[(int64_t)sp * FCB_PART_STRIDE + FCB_PART_LOSS] = s;
+      }
+    }
   }
 }
 }  // namespace
 
+template <bool BIG>
 __global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   const int bid = blockIdx.x + bid0;
-  const int nb_roles = 0;
-  // role C (one long-running WG) first so it is dispatched before the short role-B tiles
-  if (bid == 0) {
-    fc_bwd_role_c(a, B, Bp, smem);
-  } else if (bid <= ROLE_A_WGS) {
-    fc_bwd_role_a(a, B, Bp, bid - 1, smem);
+  const int S = fc_bwd_splits(B);
+  // role C (long-running, one per split) first so it is dispatched before the short role-B tiles
+  if (bid < S) {
+    fc_bwd_role_c(a, B, Bp, bid, S, smem);
+  } else if (bid < S + S * ROLE_A_WGS) {
+    const int r = bid - S;
+    fc_bwd_role_a(a, B, Bp, r % ROLE_A_WGS, r / ROLE_A_WGS, S, smem);
   } else {
-    fc_bwd_role_b(a, B, Bp, bid - 1 - ROLE_A_WGS, smem);
+    fc_bwd_role_b<BIG>(a, B, Bp, bid - S - S * ROLE_A_WGS, fcb_mr(B), smem);
   }
-  (void)nb_roles;
+}
+
+// S > 1: fixed-order sum of the split partials (fc1.w, fc1.b, fc2.w, fc2.b share the grad layout
+// [0, OFF_FC2_B + 10)), scaled by 1/world_size, plus the mean loss.
+__global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B, int S) {
+  constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;   // float4 columns (the tail pads into fc2.b's pad)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < N4) {
+    float4 t = reinterpret_cast<const float4*>(a.part)[i];
+    for (int sp = 1; sp < S; ++sp) {
+      const float4 u = reinterpret_cast<const float4*>(a.part + (int64_t)sp * FCB_PART_STRIDE)[i];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const float sc = a.grad_scale;
+    const int64_t e = 4 * i;
+    const float v[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e + k < OFF_FC2_B + NCLS) a.grad[e + k] = v[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.loss_log) {
+    float s = 0.f;
+    for (int sp = 0; sp < S; ++sp) s += a.part[(int64_t)sp * FCB_PART_STRIDE + FCB_PART_LOSS];
+    a.loss_log[a.state->step] = s / (float)B;
+  }
+}
+
+static int fc_bwd_role_b_wgs(int B) {
+  const int rows16 = (B + 15) / 16, mr = fcb_mr(B);
+  return ((rows16 + mr - 1) / mr) * ROLE_B_SBLOCKS;
 }
 
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
-  const int grid = 1 + ROLE_A_WGS + ((B + 15) / 16) * ROLE_B_SBLOCKS;
-  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  const int S = fc_bwd_splits(B);
+  if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
+  const int grid = S + S * ROLE_A_WGS + fc_bwd_role_b_wgs(B);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  if (S > 1) {
+    constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;
+    hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
+  }
 }
 
 // profiling aid: one role of fc_bwd on its own (0 = C, 1 = A, 2 = B)
 void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s) {
-  const int nb = ((B + 15) / 16) * ROLE_B_SBLOCKS;
-  const int grid = role == 0 ? 1 : role == 1 ? ROLE_A_WGS : nb;
-  const int bid0 = role == 0 ? 0 : role == 1 ? 1 : 1 + ROLE_A_WGS;
-  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
+  const int S = fc_bwd_splits(B);
+  const int nb = fc_bwd_role_b_wgs(B);
+  const int grid = role == 0 ? S : role == 1 ? S * ROLE_A_WGS : nb;
+  const int bid0 = role == 0 ? 0 : role == 1 ? S : S + S * ROLE_A_WGS;
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
 }
 
 }  // namespace mnist

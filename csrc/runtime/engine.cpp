@@ -58,6 +58,8 @@ void Engine::alloc_workspace() {
   const int64_t o_g = carve((int64_t)M * DYC_BYTES_PER_IMAGE);   // compact dy records
   const int64_t o_c1 = carve((int64_t)4 * M * 320 * 4);
   const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
+  const int S = fc_bwd_splits(max_batch_);
+  const int64_t o_fp = carve(S > 1 ? (int64_t)S * FCB_PART_STRIDE * 4 : 256);   // large-batch fc partials
   ws_bytes_ = off;
   HIP_OK(hipMalloc(&ws_, ws_bytes_));
   HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
@@ -73,6 +75,7 @@ void Engine::alloc_workspace() {
   dyc_ = reinterpret_cast<uint8_t*>(base + o_g);
   c1part_ = reinterpret_cast<float*>(base + o_c1);
   w2part_ = reinterpret_cast<float*>(base + o_w2);
+  fcpart_ = reinterpret_cast<float*>(base + o_fp);
 }
 
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
@@ -113,7 +116,7 @@ void Engine::enqueue_step(int batch, bool last) {
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
   FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, dyc_,
-               buf_.loss_log, gscale, 1.0f / (float)B};
+               buf_.loss_log, gscale, 1.0f / (float)B, fcpart_};
   launch_fc_bwd(fb, B, Bp, compute_);
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,

@@ -111,7 +111,7 @@ class Engine {
   uint16_t *a1_, *p_, *dz1_, *h_bf_, *dl_bf_;
   uint8_t* dyc_;                     // compact un-pooled gradient records (DYC_REC per pooled position)
   uint8_t* pmask_;
-  float *z1part_, *loss_rows_, *c1part_, *w2part_;
+  float *z1part_, *loss_rows_, *c1part_, *w2part_, *fcpart_;
   std::vector<hipGraphExec_t> graphs_;
   std::vector<hipGraph_t> graph_defs_;
 };

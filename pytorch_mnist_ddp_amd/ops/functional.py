@@ -40,6 +40,7 @@ class StepBuffers:
     h_bf: torch.Tensor        # bf16 [Bp64, 128]
     dl_bf: torch.Tensor       # bf16 [Bp64, 16]
     dyc: torch.Tensor         # uint8 [B, 144*192] compact grad wrt conv2 output (pooled grads + argmax)
+    fcpart: torch.Tensor      # f32 fc-gradient split partials (B > 1024), else a 1-element placeholder
     c1part: torch.Tensor      # f32 [4B, 320]
     w2part: torch.Tensor      # f32 [G, 18496]
     correct: torch.Tensor     # i32 [B]
@@ -63,6 +64,8 @@ class StepBuffers:
             h_bf=torch.zeros(Bp, NH, **bf),
             dl_bf=torch.zeros(Bp, 16, **bf),
             dyc=torch.zeros(B, 144 * 192, dtype=torch.uint8, device=device),
+            fcpart=torch.zeros(max(1, (C.fc_bwd_splits(B) > 1) * C.fc_bwd_splits(B) * C.FCB_PART_STRIDE),
+                               dtype=torch.float32, device=device),
             c1part=torch.zeros(4 * B, 320, dtype=torch.float32, **z),
             w2part=torch.zeros(G, 18432 + 64, dtype=torch.float32, **z),
             correct=torch.zeros(B, dtype=torch.int32, **z),
@@ -103,7 +106,8 @@ def fc_bwd(ms, buf: StepBuffers, grad_scale: float = 1.0, loss_log: torch.Tensor
     p = native.ptr
     B = buf.B
     _C().fc_bwd(p(buf.dz1), p(buf.p), p(buf.pmask), p(ms.w1t), p(buf.h_bf), p(buf.dl_bf), p(buf.loss_rows),
-                p(ms.state), p(ms.grad), p(buf.dyc), p(loss_log), grad_scale, 1.0 / B, B, round_up(B, 32), _s())
+                p(ms.state), p(ms.grad), p(buf.dyc), p(loss_log), grad_scale, 1.0 / B, B, round_up(B, 32), _s(),
+                part=p(buf.fcpart))
 
 
 def conv_bwd(ms, data_u8: torch.Tensor, idx: torch.Tensor, buf: StepBuffers, grad_scale: float = 1.0,

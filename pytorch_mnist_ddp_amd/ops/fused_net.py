@@ -124,7 +124,7 @@ class FusedNetFunction(torch.autograd.Function):
                      0, 0, 0, p(state), 1.0 / B, p(buf.loss_rows), p(buf.dz1), p(buf.h_bf), p(buf.dl_bf),
                      B, round_up(B, 32), s, dlogp=p(dlogp))
         C.fc_bwd(p(buf.dz1), p(buf.p), p(buf.pmask), p(ms.w1t), p(buf.h_bf), p(buf.dl_bf), p(buf.loss_rows),
-                 p(state), p(grad), p(buf.dyc), 0, 1.0, 1.0 / B, B, round_up(B, 32), s)
+                 p(state), p(grad), p(buf.dyc), 0, 1.0, 1.0 / B, B, round_up(B, 32), s, part=p(buf.fcpart))
         C.conv_bwd(p(buf.dyc), p(buf.a1), p(ms.w2d), P + 4 * o["conv1.weight"], P + 4 * o["conv1.bias"],
                    0, 0, 0, p(state), p(buf.c1part), p(buf.w2part), p(grad), 1.0, B, s, xin=p(x))
         views = [grad[o[n]:o[n] + t.numel()].view(t.shape) for n, t in ms.module.named_parameters()]

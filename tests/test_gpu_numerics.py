@@ -45,7 +45,7 @@ def test_eval_forward_matches_fp32_reference(cuda_device, B):
     assert agree > 0.97
 
 
-@pytest.mark.parametrize("B", [64, 200])
+@pytest.mark.parametrize("B", [64, 200, 1500])
 def test_train_step_grads_match_fp32_reference_without_dropout(cuda_device, B):
     net, ref, ms, imgs, labels, u8, lab, idx, buf = _setup(B, cuda_device)
     ms.set_state(0, seed=123, rng_base=0, flags=FLAG_NO_DROPOUT)
@@ -131,7 +131,7 @@ def test_adadelta_matches_torch(cuda_device):
     assert torch.equal(ms.w2d.cpu().view(9, 32, 64), w2d)
 
 
-@pytest.mark.parametrize("B", [7, 200])
+@pytest.mark.parametrize("B", [7, 200, 1500])
 def test_backward_kernels_stagewise_exact(cuda_device, B):
     """Each backward kernel vs float64 math on the kernel's *own* bf16 inputs (no cascade)."""
     import torch.nn.functional as F

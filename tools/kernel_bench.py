@@ -48,7 +48,7 @@ def main():
     def fcb(role):
         return lambda: C.fc_bwd(p(buf.dz1), p(buf.p), p(buf.pmask), p(ms.w1t), p(buf.h_bf), p(buf.dl_bf),
                                 p(buf.loss_rows), p(ms.state), p(ms.grad), p(buf.dyc), 0, 1.0, 1.0 / B, B,
-                                round_up(B, 32), s, role=role)
+                                round_up(B, 32), s, role=role, part=p(buf.fcpart))
     rows = [("fc_bwd (all roles)", fcb(-1)), ("fc_bwd role C (dW2, loss)", fcb(0)),
             ("fc_bwd role A (dW1, 145 WGs)", fcb(1)), ("fc_bwd role B (dy)", fcb(2)),
             ("fc1_fwd", lambda: Fk.fc1_fwd(ms, buf)),
