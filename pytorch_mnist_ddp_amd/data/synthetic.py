@@ -105,6 +105,32 @@ def generate(n: int, seed: int, templates: torch.Tensor | None = None, chunk: in
     return images, labels
 
 
-def synthetic_mnist(train: bool, size: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+GENERATOR_VERSION = 2
+
+
+def synthetic_mnist(train: bool, size: int | None = None, cache_dir: str | None = None
+                    ) -> tuple[torch.Tensor, torch.Tensor]:
+    """The synthetic split; with ``cache_dir`` the generated tensors are kept on disk (like the
+    reference's downloaded ./data/MNIST) so later runs load them in milliseconds."""
+    import os
     n = size if size is not None else (TRAIN_SIZE if train else TEST_SIZE)
-    return generate(n, seed=(1 if train else 2) * 7919 + 17, label_noise=LABEL_NOISE if train else 0.0)
+    path = None
+    if cache_dir:
+        path = os.path.join(cache_dir, f"synthetic-v{GENERATOR_VERSION}-{'train' if train else 'test'}-{n}.pt")
+        if os.path.exists(path):
+            try:
+                d = torch.load(path, weights_only=True)
+                if d["images"].shape == (n, IMG, IMG) and d["labels"].shape == (n,):
+                    return d["images"], d["labels"]
+            except Exception:                              # torn / foreign file: regenerate
+                pass
+    images, labels = generate(n, seed=(1 if train else 2) * 7919 + 17, label_noise=LABEL_NOISE if train else 0.0)
+    if path:
+        try:
+            os.makedirs(cache_dir, exist_ok=True)
+            tmp = f"{path}.{os.getpid()}.tmp"
+            torch.save({"images": images, "labels": labels}, tmp)
+            os.replace(tmp, path)                          # atomic: concurrent ranks write identical bytes
+        except OSError:
+            pass
+    return images, labels
