@@ -140,6 +140,9 @@ void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 
 // misc
 void launch_set_step(StepState* st, int step, hipStream_t s);
+// device-counter stream hand-offs (engine DDP schedule 3)
+void launch_stream_signal(int* ctr, hipStream_t s);
+void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s);
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 

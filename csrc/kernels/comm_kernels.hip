@@ -32,3 +32,40 @@ void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStre
 }
 
 }  // namespace mnist
+
+namespace mnist {
+
+// ---- device-flag hand-offs between the compute stream and the DDP comm stream (schedule 3) ----
+// A captured cross-stream graph edge costs ~5 us of barrier-packet latency on the waiting queue;
+// these one-workgroup kernels replace the per-step edges with monotonic counters: signal = agent-
+// scope atomic add after the producing kernel's end-of-kernel release; wait = relaxed sc1 polling
+// with s_sleep until ctr_a >= ctr_b + delta.  A wait that exceeds ~60 s (far beyond any peer stall,
+// e.g. rank 0's test-set evaluation) sets err and returns (no GPU hang on a protocol bug); once err
+// is set every later wait returns immediately and Engine::synchronize() raises.
+__global__ void stream_signal_kernel(int* ctr) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* err) {
+  if (threadIdx.x != 0) return;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();               // 100 MHz
+  while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {      // ~60 s
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+void launch_stream_signal(int* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
+}
+void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s) {
+  hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(64), 0, s, a, b, delta, err);
+}
+
+}  // namespace mnist

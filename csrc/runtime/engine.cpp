@@ -60,6 +60,7 @@ void Engine::alloc_workspace() {
   const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
   const int S = fc_bwd_splits(max_batch_);
   const int64_t o_fp = carve(S > 1 ? (int64_t)S * FCB_PART_STRIDE * 4 : 256);   // large-batch fc partials
+  const int64_t o_sy = carve(256);                                                 // schedule-3 counters
   ws_bytes_ = off;
   HIP_OK(hipMalloc(&ws_, ws_bytes_));
   HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
@@ -76,6 +77,7 @@ void Engine::alloc_workspace() {
   c1part_ = reinterpret_cast<float*>(base + o_c1);
   w2part_ = reinterpret_cast<float*>(base + o_w2);
   fcpart_ = reinterpret_cast<float*>(base + o_fp);
+  sync_ = reinterpret_cast<int*>(base + o_sy);
 }
 
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
@@ -103,9 +105,16 @@ void Engine::enqueue_step(int batch, bool last) {
 
   TrunkFwdArgs tf{buf_.train_u8, buf_.train_idx, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
+  const bool sched3 = comm_ && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 3;
+  if (sched3 && !side_forked_) {       // once per chunk: order the comm stream after the chunk start
+    HIP_OK(hipEventRecord(ev_fc_, compute_));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    side_forked_ = true;
+  }
   launch_trunk_fwd(tf, B, true, compute_);
-  if (side_pending_) {                 // schedule 2: previous step's fc all-reduce + fc update
-    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+  if (side_pending_) {                 // schedule 2/3: previous step's fc all-reduce + fc update
+    if (sched3) launch_stream_wait(sync_ + 1, sync_ + 0, 0, sync_ + 2, compute_);
+    else HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
     side_pending_ = false;
   }
   launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
@@ -127,6 +136,26 @@ void Engine::enqueue_step(int batch, bool last) {
                  conv_wgrad_groups(B), nullptr};
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
+  if (sched3) {
+    launch_stream_signal(sync_ + 0, compute_);               // fc grads of this step are final
+    launch_conv_wgrad(cb, B, compute_);
+    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+    launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
+    side_pending_ = true;
+    launch_conv_dgrad(cb, B, compute_);
+    launch_conv_grad_reduce(cb, B, compute_);
+    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+    launch_adadelta(adc, ADA_CONV, compute_);
+    if (last) {                                              // chunk end: one real join edge
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      side_pending_ = false;
+      side_forked_ = false;
+    }
+    return;
+  }
   if (dist && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 2) {
     // Cross-step overlap: the fc bucket (fc1.w/b, fc2.w/b = 98.4 % of the bytes) is all-reduced on
     // its own communicator and updated on the comm stream while the compute stream runs the conv
@@ -223,6 +252,7 @@ int Engine::capture_train(int n, int batch, int stride) {
     for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
   } catch (...) {
     side_pending_ = false;
+    side_forked_ = false;
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
     throw;
@@ -292,6 +322,9 @@ void Engine::synchronize() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
   if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
+  int err = 0;
+  HIP_OK(hipMemcpy(&err, sync_ + 2, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) throw std::runtime_error("engine: a schedule-3 stream hand-off timed out (results invalid)");
 }
 
 }  // namespace mnist

@@ -66,7 +66,10 @@ class Engine {
   // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
   // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute;
   // 2 (needs attach_comm2) = as 1, but the fc branch is joined just before the next step's fc1,
-  //   so it overlaps the conv backward, the conv bucket, the conv update AND the next trunk_fwd
+  //   so it overlaps the conv backward, the conv bucket, the conv update AND the next trunk_fwd;
+  // 3 = as 2, but the per-step fork / join are device-counter hand-offs (one-WG signal / wait
+  //   kernels) instead of captured cross-queue edges; only each chunk's first fork and last join
+  //   are graph edges
   void set_dist_schedule(int s) { dist_sched_ = s; }
 
   // --- training
@@ -102,7 +105,9 @@ class Engine {
   bool concurrent_ = false;
   int dist_sched_ = 1;
   std::shared_ptr<RcclComm> comm_, comm2_;
-  bool side_pending_ = false;       // schedule 2: the previous step's fc branch is not joined yet
+  bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
+  bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
+  int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;
   hipStream_t wgrad_stream_ = nullptr;
   // workspace

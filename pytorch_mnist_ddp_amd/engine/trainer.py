@@ -85,9 +85,10 @@ class FusedTrainer:
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
-        # DDP schedule: 2 (fc bucket on its own communicator, overlapping across the step boundary)
-        # when a second communicator is given, else 1 (see csrc/runtime/engine.h)
-        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "2" if comm2 is not None else "1"))
+        # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
+        # device-counter stream hand-offs) when a second communicator is given, else 1
+        # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)
+        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "3" if comm2 is not None else "1"))
         self.engine.set_dist_schedule(sched)
         if comm is not None:
             self.engine.attach_comm(comm)
