@@ -20,6 +20,18 @@
 
 namespace mnist {
 
+// Phase timing (tools/phase_timing.hip compiles this file with MNIST_PHASE_TIMING): thread 0 of
+// every workgroup records s_memtime at each phase boundary.
+#ifdef MNIST_PHASE_TIMING
+constexpr int kPhaseMaxWG = 4096;
+__device__ uint64_t g_phase_times[kPhaseMaxWG * 8];
+#define PHASE_MARK(i)                                                                          \
+  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < kPhaseMaxWG)                   \
+    g_phase_times[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime();
+#else
+#define PHASE_MARK(i)
+#endif
+
 namespace {
 constexpr int STRIP = 8;                      // conv2 output rows per workgroup
 constexpr int A1_ROWS = STRIP + 2;            // 10 conv1 rows
@@ -60,6 +72,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
   const int strip = blockIdx.x;   // 0..2
   const int b = blockIdx.y;       // row in batch
   const int step = a.state ? a.state->step : 0;
+  PHASE_MARK(0);
 
   // ---- phase 0: issue every global load first (conv2 weights, conv1 weights, the gathered image
   // rows), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
@@ -118,6 +131,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     }
   }
   __syncthreads();
+  PHASE_MARK(1);
 
   // ---- phase 1: conv1 + bias + ReLU (fp32 VALU) -> a1 tile (bf16 NHWC, swizzled) [+ HBM copy]
   {
@@ -142,6 +156,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     }
   }
   __syncthreads();
+  PHASE_MARK(2);
 
   // ---- phase 1b: the last two conv2-weight chunks (swizzled) over the consumed input rows
   static_assert(W2_EARLY == 7, "phase 1b stores chunks 7 and 8");
@@ -153,6 +168,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = (i == 7) ? wv7 : wv8;
   }
   __syncthreads();
+  PHASE_MARK(3);
 
   // ---- phase 2: conv2 implicit GEMM on MFMA. wave w owns M-tiles 3w..3w+2 (16 pixels = 4 windows
   // each) x all 4 N-tiles (64 channels); K loop = 9 taps of 32 channels.
@@ -192,6 +208,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
   }
 
   __syncthreads();   // every wave is done with the conv2 weights: their region becomes the staging
+  PHASE_MARK(4);
   // ---- phase 3: bias + ReLU + 2x2 max-pool (in registers) -> LDS staging [channel][window]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -212,6 +229,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     }
   }
   __syncthreads();
+  PHASE_MARK(5);
 
   // ---- phase 4: dropout + coalesced stores.  One thread = 16 contiguous flat elements of one
   // channel = exactly one Philox block (48 = 3 x 16 per channel-strip), waves 0-2 only.
@@ -250,6 +268,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     dst[0] = s0;
     dst[1] = s1;
   }
+  PHASE_MARK(6);
 }
 
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s) {
