@@ -103,17 +103,19 @@ def main() -> int:
         parts.append(idx[: (idx.numel() // B) * B])
         ep += 1
     stream = torch.cat(parts)[: total * B]
-    tr.start_stream(stream)
+    tr.start_stream(stream, gather=False)
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
     if comm is not None:   # RCCL lazily sets up its channels on the first collective: do it untimed
         tr.synchronize()
+    tr.engine.gather_rows(0, args.warmup * B)
     tr.run_steps(args.warmup)
     tr.synchronize()
     if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    tr.engine.gather_rows(args.warmup * B, args.steps * B)   # the device DataLoader work is timed too
     tr.run_steps(args.steps)
     tr.synchronize()
     torch.cuda.synchronize()

@@ -45,6 +45,8 @@ EngineBuffers buffers_from_dict(const py::dict& d) {
   b.train_u8 = P<const uint8_t>(get("train_u8"));
   b.train_labels = P<const int32_t>(get("train_labels"));
   b.train_idx = P<const int32_t>(get("train_idx"));
+  b.epoch_u8 = P<uint8_t>(get("epoch_u8"));
+  b.epoch_labels = P<int32_t>(get("epoch_labels"));
   b.test_u8 = P<const uint8_t>(get("test_u8"));
   b.test_labels = P<const int32_t>(get("test_labels"));
   b.test_idx = P<const int32_t>(get("test_idx"));
@@ -217,6 +219,7 @@ PYBIND11_MODULE(_C, m) {
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)
+      .def("gather_rows", &Engine::gather_rows, py::arg("start"), py::arg("n"))
       .def("replay", &Engine::replay, py::call_guard<py::gil_scoped_release>())
       .def("eval", &Engine::eval)
       .def("capture_eval", &Engine::capture_eval)

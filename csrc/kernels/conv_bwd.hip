@@ -132,7 +132,8 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
         xs[e] = (row < IMG) ? srcf[r0 * IMG + e] : 0.0f;
       }
     } else {
-      const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
+      const int64_t row = (int64_t)step * a.idx_step_stride + b;   // idx == nullptr: pre-gathered epoch rows
+      const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
       const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG);
       for (int e = tid; e < DG_TROWS * IMG; e += 256) {
         const int row = r0 + e / IMG;

@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   const bool no_drop = (a.state->flags & STEP_FLAG_NO_DROPOUT) != 0;
   // the label is two dependent loads (index -> label): issue them before the row's 64 partial-sum
   // loads so their latency overlaps instead of trailing the softmax
-  const int y = a.dlogp ? 0 : a.labels[a.idx[(int64_t)step * a.idx_step_stride + b]];
+  const int64_t lrow = (int64_t)step * a.idx_step_stride + b;     // idx == nullptr: pre-gathered labels
+  const int y = a.dlogp ? 0 : a.labels[a.idx ? (int64_t)a.idx[lrow] : lrow];
   HeadRow r;
   head_forward_row(a, B, b, lane, true, no_drop, seed, off, r);
   float lp[NCLS];

@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
       if (tid < X_ROWS * IMG / 4)
         xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + strip * STRIP * IMG + tid * 4);
     } else {
-      const int img = a.idx[(int64_t)step * a.idx_step_stride + b];
+      const int64_t row = (int64_t)step * a.idx_step_stride + b;   // idx == nullptr: pre-gathered epoch rows
+      const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
       if (tid < XCH)
         xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
     }

@@ -103,7 +103,12 @@ void Engine::enqueue_step(int batch, bool last) {
   float* P = buf_.param;
   const float gscale = 1.0f / (float)world_;
 
-  TrunkFwdArgs tf{buf_.train_u8, buf_.train_idx, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
+  // pre-gathered epoch rows when available (one load level less on every step's critical path)
+  const bool pre = buf_.epoch_u8 != nullptr;
+  const uint8_t* data = pre ? buf_.epoch_u8 : buf_.train_u8;
+  const int32_t* idxp = pre ? nullptr : buf_.train_idx;
+  const int32_t* labels = pre ? buf_.epoch_labels : buf_.train_labels;
+  TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
   const bool sched3 = comm_ && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 3;
   if (sched3 && !side_forked_) {       // once per chunk: order the comm stream after the chunk start
@@ -120,7 +125,7 @@ void Engine::enqueue_step(int batch, bool last) {
   launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
-  ha.labels = buf_.train_labels; ha.idx = buf_.train_idx; ha.idx_step_stride = stride;
+  ha.labels = labels; ha.idx = idxp; ha.idx_step_stride = stride;
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
@@ -131,8 +136,8 @@ void Engine::enqueue_step(int batch, bool last) {
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
   const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
-  ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, buf_.train_u8,
-                 buf_.train_idx, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
+  ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
+                 idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
@@ -263,6 +268,13 @@ int Engine::capture_train(int n, int batch, int stride) {
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   return (int)graphs_.size() - 1;
+}
+
+void Engine::gather_rows(int64_t start, int64_t n) {
+  if (!buf_.epoch_u8 || !buf_.epoch_labels) throw std::runtime_error("gather_rows: no epoch buffers");
+  launch_gather_rows(buf_.train_u8, buf_.train_labels, buf_.train_idx, start, n, buf_.epoch_u8, buf_.epoch_labels,
+                     compute_);
+  HIP_OK(hipGetLastError());
 }
 
 void Engine::replay(int id) {

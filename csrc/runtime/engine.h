@@ -44,6 +44,8 @@ struct EngineBuffers {
   const uint8_t* train_u8 = nullptr;
   const int32_t* train_labels = nullptr;
   const int32_t* train_idx = nullptr;   // [steps * B] this rank's epoch order
+  uint8_t* epoch_u8 = nullptr;          // optional [steps * B][784] pre-gathered rows (gather_rows)
+  int32_t* epoch_labels = nullptr;      // optional [steps * B]
   const uint8_t* test_u8 = nullptr;
   const int32_t* test_labels = nullptr;
   const int32_t* test_idx = nullptr;    // [N_test]
@@ -78,6 +80,9 @@ class Engine {
   void train_steps(int n, int batch, int stride);
   int capture_train(int n, int batch, int stride);   // capture n steps into a graph, returns id
   void replay(int graph_id);
+  // device-side DataLoader: pre-gather epoch rows [start, start+n) (needs epoch_u8/epoch_labels);
+  // the step kernels then read the batch directly instead of through the index vector
+  void gather_rows(int64_t start, int64_t n);
   // --- eval (SequentialSampler over the test set, `n_batches` of `batch`, last may be short)
   void eval(int n_total, int batch);
   int capture_eval(int n_total, int batch);

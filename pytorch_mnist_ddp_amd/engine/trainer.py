@@ -62,6 +62,9 @@ class FusedTrainer:
         self.train_u8 = train.images.reshape(len(train), -1).contiguous().to(dev)
         self.train_labels = train.targets.to(torch.int32).to(dev)
         self.train_idx = torch.zeros(self.steps_per_epoch * self.B, dtype=torch.int32, device=dev)
+        # device-side DataLoader: each epoch's rows pre-gathered in sampler order (Engine::gather_rows)
+        self.epoch_u8 = torch.empty(self.steps_per_epoch * self.B, 784, dtype=torch.uint8, device=dev)
+        self.epoch_labels = torch.zeros(self.steps_per_epoch * self.B, dtype=torch.int32, device=dev)
         self.loss_log = torch.zeros(max(self.steps_per_epoch, 1), dtype=torch.float32, device=dev)
         self.n_test = len(test) if test is not None else 0
         if test is not None:
@@ -73,7 +76,7 @@ class FusedTrainer:
         bufs = mstate.buffers()
         p = native.ptr
         bufs.update(loss_log=p(self.loss_log), train_u8=p(self.train_u8), train_labels=p(self.train_labels),
-                    train_idx=p(self.train_idx))
+                    train_idx=p(self.train_idx), epoch_u8=p(self.epoch_u8), epoch_labels=p(self.epoch_labels))
         if test is not None:
             bufs.update(test_u8=p(self.test_u8), test_labels=p(self.test_labels), test_idx=p(self.test_idx),
                         test_loss_rows=p(self.test_loss_rows), test_correct=p(self.test_correct))
@@ -120,13 +123,16 @@ class FusedTrainer:
         else:
             self.engine.train_steps(n, batch, self.B)
 
-    def upload_indices(self, idx: torch.Tensor) -> None:
+    def upload_indices(self, idx: torch.Tensor, gather: bool = True) -> None:
+        """Upload this epoch's sampler order; ``gather`` also pre-gathers the rows on the device."""
         n = idx.numel()
         if n > self.train_idx.numel():
             raise ValueError("epoch index vector larger than the device buffer")
         host = idx.to(torch.int32).pin_memory() if torch.cuda.is_available() else idx.to(torch.int32)
         with torch.cuda.stream(self.compute):
             self.train_idx[:n].copy_(host, non_blocking=True)
+        if gather:
+            self.engine.gather_rows(0, n)
 
     # ------------------------------------------------------------------ training
     def train_epoch(self, epoch: int, idx: torch.Tensor, log_interval: int = 10, dry_run: bool = False,
@@ -176,9 +182,10 @@ class FusedTrainer:
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
 
     # ------------------------------------------------------------------ raw step stream (bench)
-    def start_stream(self, idx: torch.Tensor) -> None:
-        """Upload a flat index stream (steps * B rows) and reset the device step counter."""
-        self.upload_indices(idx)
+    def start_stream(self, idx: torch.Tensor, gather: bool = True) -> None:
+        """Upload a flat index stream (steps * B rows) and reset the device step counter.
+        With ``gather=False`` the caller pre-gathers row ranges itself (``engine.gather_rows``)."""
+        self.upload_indices(idx, gather=gather)
         self.engine.begin_epoch(self.seed, self.rng_base, 0, self.flags)
         self.rng_base += 2 * (idx.numel() // self.B)
 

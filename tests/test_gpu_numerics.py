@@ -131,7 +131,7 @@ def test_adadelta_matches_torch(cuda_device):
     assert torch.equal(ms.w2d.cpu().view(9, 32, 64), w2d)
 
 
-@pytest.mark.parametrize("B", [7, 200, 1500])
+@pytest.mark.parametrize("B", [7, 200, 1500, 2100])
 def test_backward_kernels_stagewise_exact(cuda_device, B):
     """Each backward kernel vs float64 math on the kernel's *own* bf16 inputs (no cascade)."""
     import torch.nn.functional as F
