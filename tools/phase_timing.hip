@@ -35,7 +35,8 @@ int main(int argc, char** argv) {
   uint16_t* a1 = dev_fill<uint16_t>((size_t)B * 26 * 26 * 32, 0);
   uint16_t* p = dev_fill<uint16_t>((size_t)B * 9216, 0);
   uint8_t* pm = dev_fill<uint8_t>((size_t)B * 9216, 0);
-  TrunkFwdArgs a{d_img, d_idx, 0, d_st, w1c, b1c, w2f, b2c, a1, p, pm, nullptr};
+  const bool pre = argc > 2 && atoi(argv[2]) == 1;   // 1: pre-gathered rows (no index load)
+  TrunkFwdArgs a{d_img, pre ? nullptr : d_idx, 0, d_st, w1c, b1c, w2f, b2c, a1, p, pm, nullptr};
   for (int it = 0; it < 5; ++it) launch_trunk_fwd(a, B, true, nullptr);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
