@@ -24,6 +24,8 @@ struct TrunkFwdArgs {
                               // when set, data_u8/idx are ignored
 };
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
+constexpr int TRUNK_IMG_MAX_B = 256;      // B <= this: one workgroup per image (every image has a CU)
+int trunk_strips_per_wg(int B);           // 3 (whole image per workgroup) or 1 (one strip)
 
 // fc1 split-K partial GEMM: z1part[s][b][o] = sum_{i in chunk s} p[b][i] * w1[o][i]
 constexpr int FC1_KSPLIT = 32;            // small batches: 16-row tiles, fragments straight from HBM/L2

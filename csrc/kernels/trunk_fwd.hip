@@ -4,10 +4,11 @@
 // Replaces reference mnist_ddp.py:49-56 (conv1, relu, conv2, relu, max_pool2d, dropout1, flatten)
 // plus the DataLoader's ToTensor/Normalize (mnist_ddp.py:153-156) and the H2D copy (:68).
 //
-// One workgroup (4 waves) = one image x one strip of 8 conv2-output rows (3 strips per image).
-//   * the 12x28 input rows are gathered from the HBM-resident uint8 dataset by index and normalised;
+// One workgroup = NS strips of 8 conv2-output rows of one image (3 strips per image; NS = 1 with
+// 4 waves, or NS = 3 = the whole image with 12 waves, chosen by batch size: trunk_strips_per_wg).
+//   * the input rows are gathered from the HBM-resident uint8 dataset by index and normalised;
 //   * conv1 (K=9, too small for MFMA) runs on the VALU in fp32 straight into an NHWC bf16 LDS tile;
-//   * conv2 is an implicit GEMM on v_mfma_f32_16x16x32_bf16: M = 192 pixels, N = 64 channels,
+//   * conv2 is an implicit GEMM on v_mfma_f32_16x16x32_bf16: M = 192 pixels per strip, N = 64,
 //     K = 9 taps x 32 channels; one 32-deep k-step is exactly one tap, so every A fragment is one
 //     16-byte LDS read of 8 contiguous channels at (pixel + tap offset);
 //   * the M index is ordered pool-window-major (m = 4*window + q), so each lane's 4 accumulator
@@ -33,59 +34,82 @@ __device__ uint64_t g_phase_times[kPhaseMaxWG * 8];
 #endif
 
 namespace {
-constexpr int STRIP = 8;                      // conv2 output rows per workgroup
-constexpr int A1_ROWS = STRIP + 2;            // 10 conv1 rows
-constexpr int X_ROWS = STRIP + 4;             // 12 input rows
+constexpr int STRIP = 8;                      // conv2 output rows per strip (3 strips per image)
 constexpr int WIN = (STRIP / 2) * HP;         // 48 pool windows per strip
 
-// LDS carve (bytes, all 16-aligned).  53,504 B so that three workgroups fit a CU (160 KiB): the
-// conv2-weight region is time-shared.  Weight chunks 0..6 of every thread (rows 0..447) are stored
-// in phase 0; the input rows live where chunks 7..8 go (rows 448..575) until conv1 has consumed
-// them, then those two chunks are stored from VGPRs (phase 1b).  After the MFMA loop the same
-// region holds the pool/flag staging (phases 3-4).
-constexpr int A1S_OFF = 0, A1S_BYTES = A1_ROWS * H1 * C1 * 2;                   // 16640
-constexpr int W2S_OFF = A1S_OFF + A1S_BYTES, W2S_BYTES = C2 * 9 * C1 * 2;       // 36864
-constexpr int W2_EARLY = 7;                                                     // chunks stored in phase 0
-constexpr int XS_OFF = W2S_OFF + W2_EARLY * 256 * 16, XS_BYTES = X_ROWS * IMG * 4;   // 1344 (alias)
-constexpr int POOL_OFF = W2S_OFF, POOL_BYTES = C2 * WIN * 4;                    // 12288 (alias)
-constexpr int FLAG_OFF = POOL_OFF + POOL_BYTES, FLAG_BYTES = C2 * WIN;          // 3072 (alias)
-constexpr int LDS_TOTAL = W2S_OFF + W2S_BYTES;
-static_assert(FLAG_OFF + FLAG_BYTES <= LDS_TOTAL && XS_OFF + XS_BYTES <= LDS_TOTAL, "LDS aliasing");
-static_assert(3 * LDS_TOTAL <= 160 * 1024, "three workgroups per CU");
+// One workgroup = NS strips of one image (NS = 1: 4 waves, grid 3 x B; NS = 3: 12 waves, grid B).
+// NS = 3 stages the conv2 weights (36.9 KB) once per image instead of once per strip and computes
+// the 26 a1 rows once (strips recompute 2 halo rows); it is the faster form while every image
+// gets a CU of its own (B <= 256), NS = 1 (three workgroups per CU) beyond.
+//
+// LDS carve (bytes, 16-aligned), time-shared so NS = 1 fits three workgroups per CU (160 KiB):
+//   [0, A1S)           a1 tile (bf16 NHWC, swizzled)          -> after the MFMA loop: pool staging
+//   [W2S_OFF, +36864)  conv2 weights: the EARLY chunks of every thread are stored in phase 0, the
+//                      input rows live where the parked chunks go until conv1 has consumed them,
+//                      then the parked chunks are stored from VGPRs (phase 1b) -> later: flags
+template <int NS>
+struct TrunkCfg {
+  static constexpr int THREADS = 256 * NS;
+  static constexpr int ROWS2 = STRIP * NS;                    // conv2 output rows
+  static constexpr int A1_ROWS = ROWS2 + 2, X_ROWS = ROWS2 + 4;
+  static constexpr int A1S_BYTES = A1_ROWS * H1 * C1 * 2;     // 16640 | 43264
+  static constexpr int W2S_OFF = A1S_BYTES, W2S_BYTES = C2 * 9 * C1 * 2;
+  static constexpr int CHUNKS = W2S_BYTES / 16 / THREADS;     // 16-B weight chunks per thread: 9 | 3
+  static constexpr int EARLY = NS == 1 ? 7 : 2;               // stored in phase 0, rest parked
+  static constexpr int XS_OFF = W2S_OFF + EARLY * THREADS * 16, XS_BYTES = X_ROWS * IMG * 4;
+  static constexpr int WIN_LD = WIN * NS + 4;                 // [channel][window] row: 52 | 148 =
+                                                              // 20 mod 32 words -> conflict-free rows
+  static constexpr int POOL_OFF = 0, POOL_BYTES = C2 * WIN_LD * 4;
+  static constexpr int FLAG_OFF = W2S_OFF, FLAG_BYTES = C2 * WIN_LD;
+  static constexpr int LDS = W2S_OFF + W2S_BYTES;             // 53504 | 80128
+  static constexpr int C1_PIX = THREADS / 4;                  // conv1 pixels per pass (4 chunks each)
+  static constexpr int C1_ITERS = (A1_ROWS * H1 + C1_PIX - 1) / C1_PIX;   // 5 | 4
+  static_assert(CHUNKS * THREADS * 16 == W2S_BYTES, "weight chunking");
+  static_assert(XS_OFF + XS_BYTES <= LDS, "input rows alias the parked weight chunks");
+  static_assert(POOL_BYTES <= A1S_BYTES && FLAG_OFF + FLAG_BYTES <= LDS, "epilogue staging aliasing");
+  static_assert(NS != 1 || 3 * LDS <= 160 * 1024, "three strip workgroups per CU");
+};
 
 // 16-byte-chunk XOR swizzles (4 chunks of 8 channels per 64-byte row) against ds_read_b128 bank
-// conflicts: a1 rows are indexed by pixel, w2 rows by (channel, tap).
-__device__ __forceinline__ int swz_a1(int pix) { return 0 * pix; }   // model: no XOR beats (p>>2)&3
+// conflicts.  a1: keyed by the pixel's column, which makes the conv2 A-fragment reads (2 rows x 8
+// columns of pixels per 16-lane group) conflict-free (tools/lds_banks.py: 4 LDS cycles per
+// wave-instruction vs 8 unswizzled) while each conv1 store stays 64 contiguous bytes per pixel.
+// w2: rows indexed by (channel, tap).
+__device__ __forceinline__ int swz_a1(int col) { return col & 3; }
 __device__ __forceinline__ int swz_w2(int n) { return (4 - ((n >> 2) & 3)) & 3; }
 }  // namespace
 
-template <bool TRAIN>
-__global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_TOTAL];
-  float* xs = reinterpret_cast<float*>(smem + XS_OFF);
-  uint16_t* a1s = reinterpret_cast<uint16_t*>(smem + A1S_OFF);
-  uint16_t* w2s = reinterpret_cast<uint16_t*>(smem + W2S_OFF);
-  float* pool_s = reinterpret_cast<float*>(smem + POOL_OFF);
-  uint8_t* flag_s = smem + FLAG_OFF;
+template <bool TRAIN, int NS>
+__global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(TrunkFwdArgs a) {
+  using K = TrunkCfg<NS>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[K::LDS];
+  float* xs = reinterpret_cast<float*>(smem + K::XS_OFF);
+  uint16_t* a1s = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* w2s = reinterpret_cast<uint16_t*>(smem + K::W2S_OFF);
+  float* pool_s = reinterpret_cast<float*>(smem + K::POOL_OFF);
+  uint8_t* flag_s = smem + K::FLAG_OFF;
 
   const int tid = threadIdx.x;
-  const int strip = blockIdx.x;   // 0..2
-  const int b = blockIdx.y;       // row in batch
+  const int strip0 = blockIdx.x * NS;   // first strip of this workgroup
+  const int b = blockIdx.y;             // row in batch
   const int step = a.state ? a.state->step : 0;
   PHASE_MARK(0);
 
-  // ---- phase 0: issue every global load first (conv2 weights, conv1 weights, the gathered image
-  // rows), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
+  // ---- phase 0: issue every global load first (input rows, conv2 weights, conv1 weights, conv2
+  // bias), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
   const int c = tid & 3;                         // conv1: fixed 8-channel chunk per thread
-  float w[8][9], bias[8];
-  uint4 wv7, wv8;                                // last two conv2-weight chunks, parked until phase 1b
+  float w[8][9], bias[8], bias2[4];
+  constexpr int PARKED = K::CHUNKS - K::EARLY;
+  static_assert(PARKED == 1 || PARKED == 2, "parked chunk count");
+  uint4 wp0, wp1 = {0u, 0u, 0u, 0u};            // conv2-weight chunks held in VGPRs until phase 1b
+                                                 // (named scalars: an array here lands in scratch)
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.w2f);
-    uint4 wv[W2_EARLY];
+    uint4 wv[K::EARLY];
 #pragma unroll
-    for (int i = 0; i < W2_EARLY; ++i) wv[i] = src[tid + 256 * i];
-    wv7 = src[tid + 256 * 7];
-    wv8 = src[tid + 256 * 8];
+    for (int i = 0; i < K::EARLY; ++i) wv[i] = src[tid + K::THREADS * i];
+    wp0 = src[tid + K::THREADS * K::EARLY];
+    if constexpr (PARKED == 2) wp1 = src[tid + K::THREADS * (K::EARLY + 1)];
     const float4* w1v = reinterpret_cast<const float4*>(a.w1c + c * 72);
 #pragma unroll
     for (int k = 0; k < 18; ++k) {
@@ -98,26 +122,28 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
     const float4 b0 = b1v[0], b1 = b1v[1];
     bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
     bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
-    uint4 xv = {0u, 0u, 0u, 0u};
-    float4 xf = {0.f, 0.f, 0.f, 0.f};
-    constexpr int XCH = X_ROWS * IMG / 16;       // 21 16-byte chunks (image rows are 16-B aligned)
 #pragma unroll
-    for (int i = 0; i < W2_EARLY; ++i) {          // swizzle only permutes chunks inside a 64-B row
-      const int ch = tid + 256 * i;
-      const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
+    for (int nt = 0; nt < 4; ++nt) bias2[nt] = a.b2c[nt * 16 + (tid & 15)];
+#pragma unroll
+    for (int i = 0; i < K::EARLY; ++i) {         // swizzle only permutes chunks inside a 64-B row
+      const int ch = tid + K::THREADS * i;
+      const int row = ch >> 2, kc = ch & 3;      // row = n*9 + tap
       *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(row / 9)) * 8)) = wv[i];
     }
-    if (a.xin) {                                  // module API: fp32 input rows (84 float4)
-      if (tid < X_ROWS * IMG / 4)
-        xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + strip * STRIP * IMG + tid * 4);
+    uint4 xv = {0u, 0u, 0u, 0u};
+    float4 xf = {0.f, 0.f, 0.f, 0.f};
+    constexpr int XCH = K::X_ROWS * IMG / 16;    // 16-byte chunks of the input rows (rows are 16-B aligned)
+    const int64_t xoff = (int64_t)strip0 * STRIP * IMG;
+    if (a.xin) {                                 // module API: fp32 input rows
+      if (tid < K::X_ROWS * IMG / 4)
+        xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + xoff + tid * 4);
     } else {
       const int64_t row = (int64_t)step * a.idx_step_stride + b;   // idx == nullptr: pre-gathered epoch rows
       const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
-      if (tid < XCH)
-        xv = *reinterpret_cast<const uint4*>(a.data_u8 + (int64_t)img * (IMG * IMG) + strip * STRIP * IMG + tid * 16);
+      if (tid < XCH) xv = *reinterpret_cast<const uint4*>(a.data_u8 + img * (IMG * IMG) + xoff + tid * 16);
     }
     if (a.xin) {
-      if (tid < X_ROWS * IMG / 4) *reinterpret_cast<float4*>(xs + tid * 4) = xf;
+      if (tid < K::X_ROWS * IMG / 4) *reinterpret_cast<float4*>(xs + tid * 4) = xf;
     } else if (tid < XCH) {
       const uint32_t words[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
@@ -135,52 +161,51 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
   PHASE_MARK(1);
 
   // ---- phase 1: conv1 + bias + ReLU (fp32 VALU) -> a1 tile (bf16 NHWC, swizzled) [+ HBM copy]
-  {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const int pidx = (tid >> 2) + 64 * i;
-      if (pidx < A1_ROWS * H1) {
-        const int r = pidx / H1, col = pidx - r * H1;
-        const float* xp = xs + r * IMG + col;
-        float o[8];
+  for (int i = 0; i < K::C1_ITERS; ++i) {
+    const int pidx = (tid >> 2) + K::C1_PIX * i;
+    if (pidx < K::A1_ROWS * H1) {
+      const int r = pidx / H1, col = pidx - r * H1;
+      const float* xp = xs + r * IMG + col;
+      float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaxf(conv1_preact(xp, IMG, w[j], bias[j]), 0.0f);
-        uint4 v;
-        v.x = pack2bf(o[0], o[1]); v.y = pack2bf(o[2], o[3]);
-        v.z = pack2bf(o[4], o[5]); v.w = pack2bf(o[6], o[7]);
-        *reinterpret_cast<uint4*>(a1s + pidx * 32 + ((c ^ swz_a1(pidx)) * 8)) = v;
-        if (TRAIN && (r < STRIP || strip == 2)) {
-          const int grow = strip * STRIP + r;
-          *reinterpret_cast<uint4*>(a.a1_out + (((int64_t)b * H1 + grow) * H1 + col) * C1 + c * 8) = v;
-        }
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(conv1_preact(xp, IMG, w[j], bias[j]), 0.0f);
+      uint4 v;
+      v.x = pack2bf(o[0], o[1]); v.y = pack2bf(o[2], o[3]);
+      v.z = pack2bf(o[4], o[5]); v.w = pack2bf(o[6], o[7]);
+      *reinterpret_cast<uint4*>(a1s + pidx * 32 + ((c ^ swz_a1(col)) * 8)) = v;
+      if (TRAIN && (r < K::ROWS2 || strip0 + NS == 3)) {   // halo rows are written by their owner strip
+        const int grow = strip0 * STRIP + r;
+        *reinterpret_cast<uint4*>(a.a1_out + (((int64_t)b * H1 + grow) * H1 + col) * C1 + c * 8) = v;
       }
     }
   }
   __syncthreads();
   PHASE_MARK(2);
 
-  // ---- phase 1b: the last two conv2-weight chunks (swizzled) over the consumed input rows
-  static_assert(W2_EARLY == 7, "phase 1b stores chunks 7 and 8");
+  // ---- phase 1b: the parked conv2-weight chunks (swizzled) over the consumed input rows
 #pragma unroll
-  for (int i = W2_EARLY; i < 9; ++i) {
-    const int ch = tid + 256 * i;                // 2304 chunks of 16 B
-    const int row = ch >> 2, kc = ch & 3;        // row = n*9 + tap
-    const int n = row / 9;
-    *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(n)) * 8)) = (i == 7) ? wv7 : wv8;
+  for (int i = 0; i < PARKED; ++i) {
+    const int ch = tid + K::THREADS * (K::EARLY + i);
+    const int row = ch >> 2, kc = ch & 3;
+    *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(row / 9)) * 8)) = i ? wp1 : wp0;
   }
   __syncthreads();
   PHASE_MARK(3);
 
-  // ---- phase 2: conv2 implicit GEMM on MFMA. wave w owns M-tiles 3w..3w+2 (16 pixels = 4 windows
-  // each) x all 4 N-tiles (64 channels); K loop = 9 taps of 32 channels.
+  // ---- phase 2: conv2 implicit GEMM on MFMA.  Wave w works on strip w/4 of the workgroup and owns
+  // its M-tiles 3(w%4)..+2 (16 pixels = 4 pool windows each) x all 4 N-tiles (64 channels);
+  // K loop = 9 taps of 32 channels.
   const int wave = tid >> 6, lane = tid & 63;
+  const int sl = NS == 1 ? 0 : wave >> 2, wl = wave & 3;   // strip within the workgroup, wave in strip
   const int m = lane & 15, kg = lane >> 4;
-  int pix_base[3];
+  int pix_base[3], col_base[3];
 #pragma unroll
   for (int mt = 0; mt < 3; ++mt) {
-    const int win = 4 * (3 * wave + mt) + (m >> 2), q = m & 3;
-    const int pr = win / HP, pc = win - pr * HP;
-    pix_base[mt] = (2 * pr + (q >> 1)) * H1 + 2 * pc + (q & 1);
+    const int win = 4 * (3 * wl + mt) + (m >> 2), q = m & 3;
+    const int pr = win / HP + (STRIP / 2) * sl, pc = win % HP;
+    col_base[mt] = 2 * pc + (q & 1);
+    pix_base[mt] = (2 * pr + (q >> 1)) * H1 + col_base[mt];
   }
   floatx4 acc[3][4];
 #pragma unroll
@@ -195,7 +220,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 3; ++mt) {
       const int pix = pix_base[mt] + toff;
-      A[mt] = ld16(a1s + pix * 32 + ((kg ^ swz_a1(pix)) * 8));
+      A[mt] = ld16(a1s + pix * 32 + ((kg ^ swz_a1(col_base[mt] + t % 3)) * 8));
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -208,39 +233,38 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
       for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(A[mt], Bf[nt], acc[mt][nt]);
   }
 
-  __syncthreads();   // every wave is done with the conv2 weights: their region becomes the staging
+  __syncthreads();   // a1 tile and conv2 weights are consumed: their regions become the staging
   PHASE_MARK(4);
   // ---- phase 3: bias + ReLU + 2x2 max-pool (in registers) -> LDS staging [channel][window]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int n = nt * 16 + m;
-    const float bias = a.b2c[n];
 #pragma unroll
     for (int mt = 0; mt < 3; ++mt) {
-      const int win = 4 * (3 * wave + mt) + kg;
-      float best = fmaxf(acc[mt][nt][0] + bias, 0.0f);
+      const int win = WIN * sl + 4 * (3 * wl + mt) + kg;
+      float best = fmaxf(acc[mt][nt][0] + bias2[nt], 0.0f);
       int arg = 0;
 #pragma unroll
       for (int r = 1; r < 4; ++r) {
-        const float v = fmaxf(acc[mt][nt][r] + bias, 0.0f);
+        const float v = fmaxf(acc[mt][nt][r] + bias2[nt], 0.0f);
         if (v > best) { best = v; arg = r; }   // first max wins, as torch max_pool2d
       }
-      pool_s[n * WIN + win] = best;
-      flag_s[n * WIN + win] = (uint8_t)(arg | ((best > 0.0f) ? 8 : 0));
+      pool_s[n * K::WIN_LD + win] = best;
+      flag_s[n * K::WIN_LD + win] = (uint8_t)(arg | ((best > 0.0f) ? 8 : 0));
     }
   }
   __syncthreads();
   PHASE_MARK(5);
 
   // ---- phase 4: dropout + coalesced stores.  One thread = 16 contiguous flat elements of one
-  // channel = exactly one Philox block (48 = 3 x 16 per channel-strip), waves 0-2 only.
+  // channel = exactly one Philox block (3 per channel-strip).
   const uint64_t seed = a.state ? a.state->seed : 0;
   const uint64_t off = a.state ? a.state->rng_base + 2ull * (uint64_t)step : 0;
   const bool drop = TRAIN && !(a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT));
-  if (tid < C2 * 3) {
-    const int n = tid / 3, j16 = (tid - n * 3) * 16;
-    const int flat = n * NPOOL + strip * WIN + j16;
-    const float* ps = pool_s + n * WIN + j16;
+  if (tid < C2 * 3 * NS) {
+    const int n = tid / (3 * NS), j16 = (tid - n * 3 * NS) * 16;
+    const int flat = n * NPOOL + strip0 * WIN + j16;
+    const float* ps = pool_s + n * K::WIN_LD + j16;
     float o[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -248,7 +272,7 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
       o[4 * q] = pv.x; o[4 * q + 1] = pv.y; o[4 * q + 2] = pv.z; o[4 * q + 3] = pv.w;
     }
     if (TRAIN) {
-      const uint4 fl = *reinterpret_cast<const uint4*>(flag_s + n * WIN + j16);
+      const uint4 fl = *reinterpret_cast<const uint4*>(flag_s + n * K::WIN_LD + j16);
       u32x4 rw = {0u, 0u, 0u, 0u};
       if (drop) rw = dropout_block(seed, off, ((uint64_t)b * NFLAT + flat) >> 4);
       uint32_t mk[4] = {fl.x, fl.y, fl.z, fl.w};
@@ -272,12 +296,20 @@ __global__ __launch_bounds__(256, 3) void trunk_fwd_kernel(TrunkFwdArgs a) {
   PHASE_MARK(6);
 }
 
+int trunk_strips_per_wg(int B) { return B <= TRUNK_IMG_MAX_B ? 3 : 1; }
+
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s) {
-  dim3 grid(3, B), block(256);
-  if (train)
-    hipLaunchKernelGGL(trunk_fwd_kernel<true>, grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL(trunk_fwd_kernel<false>, grid, block, 0, s, a);
+  if (trunk_strips_per_wg(B) == 3) {
+    if (train)
+      hipLaunchKernelGGL((trunk_fwd_kernel<true, 3>), dim3(1, B), dim3(768), 0, s, a);
+    else
+      hipLaunchKernelGGL((trunk_fwd_kernel<false, 3>), dim3(1, B), dim3(768), 0, s, a);
+  } else {
+    if (train)
+      hipLaunchKernelGGL((trunk_fwd_kernel<true, 1>), dim3(3, B), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((trunk_fwd_kernel<false, 1>), dim3(3, B), dim3(256), 0, s, a);
+  }
 }
 
 }  // namespace mnist

@@ -142,3 +142,31 @@ def test_mnist_scripts_single_process_cpu(tmp_path):
     assert r.stdout.count("Train Epoch:") == 1 and "Total cost time" not in r.stdout
     sd = torch.load(os.path.join(tmp_path, "mnist_cnn.pt"), weights_only=True)
     assert not any(k.startswith("module.") for k in sd)
+
+
+@pytest.mark.slow
+def test_mnist_ddp_slurm_rank_discovery_gloo(tmp_path):
+    """SLURM path (mnist_ddp.py:20-22): rank from SLURM_PROCID, world size from --world-size."""
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+        env.update(SLURM_PROCID=str(rank), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+        cmd = [sys.executable, os.path.join(ROOT, "mnist_ddp.py"), "--no-cuda", "--world-size", "2",
+               "--epochs", "1", "--batch-size", "64", "--synthetic", "--synthetic-train-size", "256",
+               "--synthetic-test-size", "100", "--dry-run"]
+        procs.append(subprocess.Popen(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=600)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, outs[-1]
+    assert "| distributed init (rank 0): env://, local rank:0, world size:2" in outs[0]
+    assert "| distributed init (rank 1): env://, local rank:0, world size:2" in outs[1]
+    assert outs[0].count("Test set: Average loss:") == 1 and "Test set" not in outs[1]

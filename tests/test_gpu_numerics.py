@@ -28,7 +28,7 @@ def _setup(B, dev, seed=1, data_seed=5):
     return net, ref, ms, imgs, labels, u8, lab, idx, buf
 
 
-@pytest.mark.parametrize("B", [1, 7, 100, 200, 1000])
+@pytest.mark.parametrize("B", [1, 7, 100, 200, 1000, 8192])
 def test_eval_forward_matches_fp32_reference(cuda_device, B):
     net, ref, ms, imgs, labels, u8, lab, idx, buf = _setup(B, cuda_device)
     Fk.eval_forward(ms, u8, lab, idx, buf)
@@ -45,7 +45,7 @@ def test_eval_forward_matches_fp32_reference(cuda_device, B):
     assert agree > 0.97
 
 
-@pytest.mark.parametrize("B", [64, 200, 1500])
+@pytest.mark.parametrize("B", [64, 200, 1500, 8192])
 def test_train_step_grads_match_fp32_reference_without_dropout(cuda_device, B):
     net, ref, ms, imgs, labels, u8, lab, idx, buf = _setup(B, cuda_device)
     ms.set_state(0, seed=123, rng_base=0, flags=FLAG_NO_DROPOUT)

@@ -1,8 +1,12 @@
 // Per-phase timing of trunk_fwd: compiles the kernel with MNIST_PHASE_TIMING (thread 0 of every
 // workgroup stamps s_memtime at each phase boundary) and prints per-phase medians over workgroups.
-// build: hipcc -x hip --offload-arch=gfx950 -O3 -fno-slp-vectorize -Icsrc tools/phase_timing.hip -o /tmp/phase_timing
+// build: hipcc -x hip --offload-arch=gfx950 -O3 -fno-slp-vectorize -Icsrc/kernels tools/phase_timing.hip -o /tmp/phase_timing
+// (-DTRUNK_SRC='"path"' times another revision of the kernel, e.g. a `git show` copy; see trunk_ab.sh)
 #define MNIST_PHASE_TIMING 1
-#include "../csrc/kernels/trunk_fwd.hip"
+#ifndef TRUNK_SRC
+#define TRUNK_SRC "../csrc/kernels/trunk_fwd.hip"
+#endif
+#include TRUNK_SRC
 
 #include <algorithm>
 #include <cstdio>
@@ -20,7 +24,7 @@ int main(int argc, char** argv) {
   using namespace mnist;
   const int B = argc > 1 ? atoi(argv[1]) : 200;
   if (3 * B > mnist::kPhaseMaxWG) { printf("B too large for the timing buffer (max %d)\n", mnist::kPhaseMaxWG / 3); return 1; }
-  const int N = 1024;
+  const int N = std::max(1024, B);
   std::vector<uint8_t> img((size_t)N * 784);
   for (auto& x : img) x = (uint8_t)(rand() & 0xFF);
   uint8_t* d_img; CK(hipMalloc(&d_img, img.size())); CK(hipMemcpy(d_img, img.data(), img.size(), hipMemcpyHostToDevice));
@@ -40,21 +44,36 @@ int main(int argc, char** argv) {
   for (int it = 0; it < 5; ++it) launch_trunk_fwd(a, B, true, nullptr);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  constexpr int kReps = 50;
   CK(hipEventRecord(e0, nullptr));
-  launch_trunk_fwd(a, B, true, nullptr);
+  for (int it = 0; it < kReps; ++it) launch_trunk_fwd(a, B, true, nullptr);
   CK(hipEventRecord(e1, nullptr));
   CK(hipDeviceSynchronize());
   float ms = 0; CK(hipEventElapsedTime(&ms, e0, e1));
-  const int nwg = 3 * B;
+  ms /= kReps;
+  const int nwg = 3 * B / trunk_strips_per_wg(B);
   std::vector<uint64_t> t((size_t)nwg * 8);
   CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_phase_times), t.size() * 8));
   const char* names[6] = {"0 loads+W2/x staging", "1 conv1 (VALU)", "1b W2 tail", "2 conv2 MFMA",
                           "3 pool epilogue", "4 dropout+stores"};
-  printf("B=%d  kernel %.2f us (events), %d WGs; s_memtime ticks are per-XCD shader clocks\n", B, ms * 1000, nwg);
+  printf("B=%d  kernel %.2f us (events, mean of 50 back-to-back), %d WGs; s_memtime ticks are per-XCD shader clocks\n", B, ms * 1000, nwg);
   std::vector<double> tot;
   for (int w = 0; w < nwg; ++w) tot.push_back((double)(t[w * 8 + 6] - t[w * 8]));
   std::sort(tot.begin(), tot.end());
   printf("  WG lifetime ticks: median %.0f  p10 %.0f  p90 %.0f\n", tot[nwg / 2], tot[nwg / 10], tot[nwg * 9 / 10]);
+  {  // per-XCD (WG id % 8 shares a clock) dispatch spread and span
+    std::vector<double> st, sp;
+    for (int x = 0; x < 8; ++x) {
+      uint64_t lo = ~0ull, hi = 0, last_start = 0;
+      for (int w = x; w < nwg; w += 8) {
+        lo = std::min(lo, t[w * 8]); hi = std::max(hi, t[w * 8 + 6]); last_start = std::max(last_start, t[w * 8]);
+      }
+      st.push_back((double)(last_start - lo)); sp.push_back((double)(hi - lo));
+    }
+    std::sort(st.begin(), st.end()); std::sort(sp.begin(), sp.end());
+    printf("  per-XCD: last WG start after first %.0f..%.0f ticks, first start -> last end %.0f..%.0f ticks\n",
+           st[0], st[7], sp[0], sp[7]);
+  }
   for (int ph = 0; ph < 6; ++ph) {
     std::vector<double> d;
     for (int w = 0; w < nwg; ++w) d.push_back((double)(t[w * 8 + ph + 1] - t[w * 8 + ph]));
