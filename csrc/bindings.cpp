@@ -216,6 +216,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_concurrent", &Engine::set_concurrent)
       .def("set_dist_schedule", &Engine::set_dist_schedule)
+      .def("set_fuse_fc_update", &Engine::set_fuse_fc_update)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

@@ -102,4 +102,24 @@ struct NormLut {
 __constant__ constexpr NormLut kNormLut{};
 __device__ __forceinline__ float normalize_u8(uint8_t v) { return kNormLut.v[v]; }
 
+// One Adadelta element update (torch/optim/adadelta.py, foreach order: mul_, addcmul_, add+sqrt,
+// add+sqrt, div_, mul_, mul_, addcmul_, add_), every operation individually rounded (FMA
+// contraction off), so the result is a pure function of the inputs - bitwise identical in every
+// kernel that applies it (the optimizer kernels and the fused fc-backward epilogue).
+struct Ada {
+  float rho, eps, wd, lr;
+  __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {
+#pragma clang fp contract(off)
+    if (wd != 0.0f) g = g + wd * p;
+    const float c = 1.0f - rho;
+    sq = sq * rho + (c * g) * g;
+    const float sd = sqrtf(sq + eps);
+    float d = sqrtf(acc + eps);
+    d = (d / sd) * g;
+    acc = acc * rho + (c * d) * d;
+    p = p + (-lr) * d;
+    return p;
+  }
+};
+
 }  // namespace mnist

@@ -67,11 +67,27 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
 constexpr int DYC_REC = 192, DYC_ROUTE = 128;
 constexpr int64_t DYC_BYTES_PER_IMAGE = (int64_t)NPOOL * DYC_REC;   // 27648
 
+// Single-GPU fused fc update: with param != nullptr (and an unsplit batch, B <= FC_BWD_SPLIT_ROWS)
+// the role A / C epilogues apply the Adadelta step to fc1 / fc2 the moment each gradient is final
+// (same Ada math as the optimizer kernels -> bitwise equal), so the memory-bound fc update
+// (98.4 % of the parameters) runs under role B instead of in the step tail.  w1 is rewritten in
+// place (only the next step's fc1_fwd reads it); the transposed shadow goes to w1t_out, which
+// must not be the w1t buffer role B of the same launch is reading.
+struct FcUpdate {
+  float* param;
+  float* square_avg;
+  float* acc_delta;
+  const float* lr;
+  float rho, eps, weight_decay;
+  uint16_t* w1;               // bf16 [128][9216]
+  uint16_t* w1t_out;          // bf16 [9216][128]
+};
+
 struct FcBwdArgs {
   const uint16_t* dz1;        // bf16 [Bp][128]
   const uint16_t* p;          // bf16 [Bp][9216] (rows >= B are masked)
   const uint8_t* pmask;       // [B][9216]
-  const uint16_t* w1t;        // bf16 [9216][128]
+  const uint16_t* w1t;        // bf16 [9216][128] (read by role B)
   const uint16_t* h_bf;       // bf16 [Bp][128]
   const uint16_t* dl_bf;      // bf16 [Bp][16]
   const float* loss_rows;     // [B]
@@ -82,6 +98,7 @@ struct FcBwdArgs {
   float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
   float inv_batch;
   float* part;                // B > FC_BWD_SPLIT_ROWS: [fc_bwd_splits(B)][FCB_PART_STRIDE] partial fc grads
+  FcUpdate upd;               // optional fused fc Adadelta (zero-initialised = off)
 };
 // Large batches split the batch (= K of the fc weight gradients) over fc_bwd_splits(B) groups of
 // workgroups writing fp32 partials that fc_grad_reduce sums in fixed order; B <= 1024 writes the
@@ -135,8 +152,9 @@ struct AdadeltaArgs {
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
 void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
-// conv gradient slab reduce + the whole Adadelta update in one launch (single-GPU step tail)
-void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
+// conv gradient slab reduce + the whole Adadelta update in one launch (single-GPU step tail);
+// conv_only when fc_bwd already applied the fc update (FcBwdArgs::upd)
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s);
 // Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
 void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 

@@ -24,25 +24,7 @@ constexpr int64_t FC_TAIL_N = OFF_CONV1_W - OFF_FC1_B;            // 1472 (fc1.b
 constexpr int64_t CONV_N = PARAM_TOTAL - OFF_CONV1_W;             // 18880
 constexpr int CONV_WGS = (int)((CONV_N / 4 + 255) / 256);         // 19
 
-// Every operation individually rounded (FMA contraction off), in torch's order
-// (optim/adadelta.py: mul_, addcmul_, add+sqrt, add+sqrt, div_, mul_, mul_, addcmul_, add_), so
-// the result is a pure function of the inputs - identical in every kernel / inlining context
-// (with contraction on, the same source fused differently in the fused reduce+update launch).
-struct Ada {
-  float rho, eps, wd, lr;
-  __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {
-#pragma clang fp contract(off)
-    if (wd != 0.0f) g = g + wd * p;
-    const float c = 1.0f - rho;
-    sq = sq * rho + (c * g) * g;
-    const float sd = sqrtf(sq + eps);
-    float d = sqrtf(acc + eps);
-    d = (d / sd) * g;
-    acc = acc * rho + (c * d) * d;
-    p = p + (-lr) * d;
-    return p;
-  }
-};
+// Per-element math: Ada (device_utils.h), contraction off so every launch path is bitwise equal.
 
 __device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, float v) {
   const int rel = (int)(e - OFF_CONV2_W);
@@ -143,16 +125,19 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
 // conv-gradient slab reduction, whose workgroups apply the update to each conv parameter as soon as
 // its gradient is final (no grad round trip, no extra kernel boundary; both halves are memory-
 // bound and overlap).  Same per-element math as the two-kernel path, so results are bitwise equal.
-__global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B) {
+// conv_only: the fc parameters were already updated by fc_bwd's fused epilogue (FcBwdArgs::upd).
+__global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int conv_only) {
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   __shared__ float4 red[256];
   const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
-  if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }
-  bid -= FC1_TILES;
-  if (bid == 0) { elementwise<true>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
-  bid -= 1;
+  if (!conv_only) {
+    if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }
+    bid -= FC1_TILES;
+    if (bid == 0) { elementwise<true>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
+    bid -= 1;
+  }
   float* gbuf = c.grad;
   reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
     gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
@@ -165,8 +150,9 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
   });
 }
 
-void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
-  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(FC1_TILES + 1 + RED_WGS), dim3(256), 0, s, a, c, B);
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s) {
+  const int grid = (conv_only ? 0 : FC1_TILES + 1) + RED_WGS;
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(grid), dim3(256), 0, s, a, c, B, conv_only ? 1 : 0);
 }
 
 static int adadelta_grid(int region) {

@@ -367,6 +367,96 @@ __device__ __forceinline__ int swz_row128(int row, int col) {   // 64 bf16 per r
 }
 constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
 
+// Fused fc1 Adadelta (FcUpdate, single GPU, unsplit batch): the tile's final gradients are still in
+// the MFMA accumulators (lane: o = 32 wave + 16 mt + 4 g + r, i = i0 + 16 nt + (lane & 15)), so
+// the update reads p / sq / acc once, writes them back with the gradient, and the bf16 shadows
+// leave through two LDS transposes as whole 128-B (w1 rows) / 256-B (w1t rows) runs.
+__device__ __forceinline__ void fc_bwd_role_a_update(const FcBwdArgs& a, const floatx4 (&acc)[2][4], bool ones,
+                                                     int i0, unsigned char* smem) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
+  const FcUpdate& u = a.upd;
+  const Ada ad{u.rho, u.eps, u.weight_decay, *u.lr};
+  const float sc = a.grad_scale;
+  if (ones) {                                           // fc1.bias: column 0 of the ones-GEMM
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t e = OFF_FC1_B + 32 * wave + 16 * mt + 4 * g + r;
+          const float gv = acc[mt][0][r] * sc;
+          float p = u.param[e], sq = u.square_avg[e], ac = u.acc_delta[e];
+          ad.step(p, gv, sq, ac);
+          a.grad[e] = gv;
+          u.param[e] = p;
+          u.square_avg[e] = sq;
+          u.acc_delta[e] = ac;
+        }
+    }
+    return;
+  }
+  // The gradient tile goes through LDS once so that the update runs on whole 256-B row runs: thread
+  // (row group, c4) owns float4 column c4 of rows o = (tid >> 4) + 16 k (k = 0..7) - coalesced 16-B
+  // loads / stores of p, sq, acc, grad and 8-B bf16 w1 stores, instead of 4-B scattered accesses.
+  constexpr int GT_LD = 68, WTS_LD = 136;               // padded fp32 / bf16 rows (16-B aligned)
+  float* gt = reinterpret_cast<float*>(smem);                             // [128 o][64 i] fp32
+  uint16_t* wts = reinterpret_cast<uint16_t*>(smem);                      // [64 i][128 o] (after gt)
+  __syncthreads();                                      // the k-loop's LDS tiles are dead
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)                       // banks: 16 g + (lane & 15), conflict-free
+        gt[(32 * wave + 16 * mt + 4 * g + r) * GT_LD + 16 * nt + (lane & 15)] = acc[mt][nt][r] * sc;
+  __syncthreads();
+  const int c4 = tid & 15, orow = tid >> 4;
+  float4 pv[8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {                         // 2 rounds of 12 x 16-B loads in flight
+    float4 sv[4], av[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = OFF_FC1_W + (int64_t)(orow + 16 * (4 * h + k)) * NFLAT + i0 + 4 * c4;
+      pv[4 * h + k] = *reinterpret_cast<const float4*>(u.param + e);
+      sv[k] = *reinterpret_cast<const float4*>(u.square_avg + e);
+      av[k] = *reinterpret_cast<const float4*>(u.acc_delta + e);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = orow + 16 * (4 * h + k);
+      const int64_t e = OFF_FC1_W + (int64_t)o * NFLAT + i0 + 4 * c4;
+      const float4 gv = *reinterpret_cast<const float4*>(gt + o * GT_LD + 4 * c4);
+      float4& p = pv[4 * h + k];
+      ad.step(p.x, gv.x, sv[k].x, av[k].x);
+      ad.step(p.y, gv.y, sv[k].y, av[k].y);
+      ad.step(p.z, gv.z, sv[k].z, av[k].z);
+      ad.step(p.w, gv.w, sv[k].w, av[k].w);
+      *reinterpret_cast<float4*>(a.grad + e) = gv;
+      *reinterpret_cast<float4*>(u.param + e) = p;
+      *reinterpret_cast<float4*>(u.square_avg + e) = sv[k];
+      *reinterpret_cast<float4*>(u.acc_delta + e) = av[k];
+      *reinterpret_cast<uint2*>(u.w1 + (int64_t)o * NFLAT + i0 + 4 * c4) = uint2{pack2bf(p.x, p.y), pack2bf(p.z, p.w)};
+    }
+  }
+  __syncthreads();                                      // gt is dead: the w1t transpose reuses it
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int o = orow + 16 * k;
+    wts[(4 * c4 + 0) * WTS_LD + o] = f2bf(pv[k].x);
+    wts[(4 * c4 + 1) * WTS_LD + o] = f2bf(pv[k].y);
+    wts[(4 * c4 + 2) * WTS_LD + o] = f2bf(pv[k].z);
+    wts[(4 * c4 + 3) * WTS_LD + o] = f2bf(pv[k].w);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {                         // w1t: 64 rows x 256 B (one 16 KB run)
+    const int c = tid + 256 * k, row = c >> 4, c16 = c & 15;
+    *reinterpret_cast<uint4*>(u.w1t_out + (int64_t)(i0 + row) * NH + c16 * 8) =
+        *reinterpret_cast<const uint4*>(wts + row * WTS_LD + c16 * 8);
+  }
+}
+
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
 // loaded into VGPRs while the current one (double-buffered LDS) feeds the MFMAs; one barrier per slab.
 __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, int sp, int S,
@@ -427,6 +517,10 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
         }
       }
     }
+  }
+  if (S == 1 && a.upd.param) {
+    fc_bwd_role_a_update(a, acc, ones, i0, smem);
+    return;
   }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -585,9 +679,19 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
     const int col = ln & 15;
     float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
     const float sc = (S == 1) ? a.grad_scale : 1.0f;
-    if (c < NCLS) {
-      if (nt < 8) dst[OFF_FC2_W + c * NH + 16 * nt + col] = s * sc;
-      else if (col == 0) dst[OFF_FC2_B + c] = s * sc;
+    const int64_t k = (c >= NCLS) ? -1 : (nt < 8) ? OFF_FC2_W + c * NH + 16 * nt + col : (col == 0) ? OFF_FC2_B + c : -1;
+    if (k >= 0) {
+      const float gv = s * sc;
+      dst[k] = gv;
+      if (S == 1 && a.upd.param) {                     // fused fc2 Adadelta (FcUpdate)
+        const FcUpdate& u = a.upd;
+        const Ada ad{u.rho, u.eps, u.weight_decay, *u.lr};
+        float p = u.param[k], sq = u.square_avg[k], ac = u.acc_delta[k];
+        ad.step(p, gv, sq, ac);
+        u.param[k] = p;
+        u.square_avg[k] = sq;
+        u.acc_delta[k] = ac;
+      }
     }
   }
   if (wave == 0) {
@@ -607,7 +711,7 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
 }  // namespace
 
 template <bool BIG>
-__global__ __launch_bounds__(256) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
+__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   const int bid = blockIdx.x + bid0;
   const int S = fc_bwd_splits(B);

@@ -61,6 +61,7 @@ void Engine::alloc_workspace() {
   const int S = fc_bwd_splits(max_batch_);
   const int64_t o_fp = carve(S > 1 ? (int64_t)S * FCB_PART_STRIDE * 4 : 256);   // large-batch fc partials
   const int64_t o_sy = carve(256);                                                 // schedule-3 counters
+  const int64_t o_wt = carve((int64_t)NFLAT * NH * 2);                             // alternate w1t
   ws_bytes_ = off;
   HIP_OK(hipMalloc(&ws_, ws_bytes_));
   HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
@@ -78,6 +79,7 @@ void Engine::alloc_workspace() {
   w2part_ = reinterpret_cast<float*>(base + o_w2);
   fcpart_ = reinterpret_cast<float*>(base + o_fp);
   sync_ = reinterpret_cast<int*>(base + o_sy);
+  w1t_alt_ = reinterpret_cast<uint16_t*>(base + o_wt);
 }
 
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
@@ -129,13 +131,23 @@ void Engine::enqueue_step(int batch, bool last) {
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
-  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state, buf_.grad, dyc_,
-               buf_.loss_log, gscale, 1.0f / (float)B, fcpart_};
+  const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
+  // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t
+  // the step started with while role A writes the updated one, so the transposed shadow alternates
+  // between buf_.w1t and w1t_alt_ (host-tracked, static within a captured chunk); a chunk that
+  // ends on the alternate copy copies it back, so buf_.w1t is current at every chunk boundary.
+  const bool fuse_fc = fuse_fc_update_ && !dist && !concurrent_ && fc_bwd_splits(B) == 1;
+  FcBwdArgs fb{dz1_, p_, pmask_, w1t_in_alt_ ? w1t_alt_ : buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state,
+               buf_.grad, dyc_, buf_.loss_log, gscale, 1.0f / (float)B, fcpart_};
+  if (fuse_fc) {
+    fb.upd = FcUpdate{P, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_, buf_.w1,
+                      w1t_in_alt_ ? buf_.w1t : w1t_alt_};
+    w1t_in_alt_ = !w1t_in_alt_;
+  }
   launch_fc_bwd(fb, B, Bp, compute_);
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
-  const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
@@ -221,8 +233,13 @@ void Engine::enqueue_step(int batch, bool last) {
   if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
   launch_conv_dgrad(cb, B, compute_);
   if (ws != compute_) HIP_OK(hipStreamWaitEvent(compute_, ev_w_, 0));
-  if (one_update) {                     // single GPU: slab reduce + full Adadelta in one launch
-    launch_adadelta_reduce(adc, cb, B, compute_);
+  if (one_update) {                     // single GPU: slab reduce + (conv or full) Adadelta in one launch
+    launch_adadelta_reduce(adc, cb, B, fuse_fc, compute_);
+    if (last && w1t_in_alt_) {
+      HIP_OK(hipMemcpyAsync(buf_.w1t, w1t_alt_, (size_t)NFLAT * NH * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                            compute_));
+      w1t_in_alt_ = false;
+    }
     return;
   }
   launch_conv_grad_reduce(cb, B, compute_);
@@ -258,6 +275,7 @@ int Engine::capture_train(int n, int batch, int stride) {
   } catch (...) {
     side_pending_ = false;
     side_forked_ = false;
+    w1t_in_alt_ = false;
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
     throw;

@@ -43,7 +43,8 @@ class FusedTrainer:
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
-                 two_buckets: bool = True, concurrent: bool | None = None, comm2=None):
+                 two_buckets: bool = True, concurrent: bool | None = None, comm2=None,
+                 fuse_fc_update: bool | None = None):
         C = native.load()
         self.C, self.ms = C, mstate
         dev = mstate.device
@@ -88,6 +89,12 @@ class FusedTrainer:
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
+        # single GPU, opt-in (MNIST_AMD_FUSE_FC=1): fc_bwd applies the fc Adadelta step in its
+        # epilogue, bitwise equal to the step-tail update but ~1 us/step slower (the update is
+        # HBM-bound either way and loses its overlap with the conv slab reduce; docs/PERF_NOTES.md)
+        if fuse_fc_update is None:
+            fuse_fc_update = os.environ.get("MNIST_AMD_FUSE_FC", "0") == "1"
+        self.engine.set_fuse_fc_update(bool(fuse_fc_update))
         # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
         # device-counter stream hand-offs) when a second communicator is given, else 1
         # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)

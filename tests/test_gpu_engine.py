@@ -13,13 +13,13 @@ from pytorch_mnist_ddp_amd.models.net import Net
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(dev, graph_steps, n_train=2000, n_test=1000, B=200, seed=1):
+def _trainer(dev, graph_steps, n_train=2000, n_test=1000, B=200, seed=1, **kw):
     torch.manual_seed(seed)
     net = Net()
     tr = load_mnist(synthetic_data=True, train=True, synthetic_size=n_train, verbose=False)
     te = load_mnist(synthetic_data=True, train=False, synthetic_size=n_test, verbose=False)
     ms = ModelState(net, dev, lr=1.0)
-    t = FusedTrainer(ms, tr, te, B, 1000, num_samples=n_train, seed=seed, graph_steps=graph_steps)
+    t = FusedTrainer(ms, tr, te, B, 1000, num_samples=n_train, seed=seed, graph_steps=graph_steps, **kw)
     return net, ms, t
 
 
@@ -58,3 +58,24 @@ def test_partial_last_batch_and_dry_run(cuda_device):
     st = t.train_epoch(2, idx, dry_run=True, log_fn=lambda b, n, l: logs.append((b, n, l)))
     assert st.steps == 1
     assert torch.isfinite(ms.param).all()
+
+
+@pytest.mark.parametrize("graph_steps", [0, 3, 4])
+def test_fused_fc_update_bitwise_equals_step_tail_update(cuda_device, graph_steps):
+    """fc_bwd's fused fc Adadelta epilogue (w1t ping-pong, odd and even chunk lengths, eager) ==
+    the separate step-tail update, bit for bit, including every bf16 shadow."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(5))
+    _, ms_f, tf = _trainer(cuda_device, graph_steps=graph_steps, fuse_fc_update=True)
+    _, ms_u, tu = _trainer(cuda_device, graph_steps=graph_steps, fuse_fc_update=False)
+    for ep in (1, 2):
+        tf.train_epoch(ep, idx)
+        tu.train_epoch(ep, idx)
+    torch.cuda.synchronize()
+    for name in ("param", "grad", "square_avg", "acc_delta", "w1", "w1t", "w2f", "w2d"):
+        assert torch.equal(getattr(ms_f, name), getattr(ms_u, name)), name
+    assert torch.equal(tf.loss_log, tu.loss_log)
+    w1 = ms_f.views(ms_f.param)["fc1.weight"]
+    assert torch.equal(ms_f.w1t.view(9216, 128), w1.t().contiguous().to(torch.bfloat16))
+    lf, cf, _ = tf.evaluate()
+    lu, cu, _ = tu.evaluate()
+    assert lf == lu and cf == cu
