@@ -61,6 +61,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--force-comm", action="store_true",
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
+    ap.add_argument("--allreduce", choices=["rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "rccl"),
+                    help="DDP gradient all-reduce: RCCL, or the direct xGMI reduce-scatter/all-gather kernel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +93,7 @@ def main() -> int:
     comm, comm2 = create_rccl_comms(world, rank, local) if use_pg else (None, None)
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                      two_buckets=not args.single_bucket, comm2=comm2)
+                      two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
     if comm is not None:
         tr.engine.broadcast_params(0)     # DDP construction semantics: rank-0 weights everywhere
 
@@ -139,7 +141,7 @@ def main() -> int:
         ms2 = ModelState(net2, dev, lr=1.0)
         tr2 = FusedTrainer(ms2, train, test, B, 1000, num_samples=len(sampler), world_size=world, rank=rank,
                            comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                           two_buckets=not args.single_bucket, comm2=comm2)
+                           two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
         if comm is not None:
             tr2.engine.broadcast_params(0)
         if use_pg:
@@ -182,7 +184,8 @@ def main() -> int:
             "config": {"model": "mnist_cnn (reference Net: conv32-conv64-maxpool-fc128-fc10, 1.2M params)",
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
-                       "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2},
+                       "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
+                       "allreduce": tr.allreduce if world > 1 or comm is not None else None},
             "wallclock_20ep_s": round(wall, 3) if wall is not None else None,
             "baseline_wallclock_20ep_s": base,
             "vs_baseline_wallclock": round(base / wall, 1) if (wall and base) else None,

@@ -186,6 +186,33 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world_size", &RcclComm::world_size)
       .def_property_readonly("rank", &RcclComm::rank);
 
+  py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
+      .def(py::init([](int world, int rank, int device, uintptr_t in, uintptr_t out, int64_t numel, int channels) {
+             return std::make_shared<XgmiComm>(world, rank, device, P<float>(in), P<float>(out), numel, channels);
+           }),
+           py::arg("world_size"), py::arg("rank"), py::arg("device"), py::arg("in_ptr"), py::arg("out_ptr"),
+           py::arg("numel"), py::arg("channels") = 2)
+      .def("record", [](const XgmiComm& c) {
+        auto v = c.record();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("connect", [](XgmiComm& c, std::vector<py::bytes> recs) {
+        std::vector<std::vector<uint8_t>> v;
+        for (auto& r : recs) {
+          std::string s = r;
+          v.emplace_back(s.begin(), s.end());
+        }
+        c.connect(v);
+      })
+      .def("allreduce", [](XgmiComm& c, int channel, int64_t offset, int64_t count, uintptr_t stream) {
+        c.allreduce(channel, offset, count, S(stream));
+      }, py::arg("channel"), py::arg("offset"), py::arg("count"), py::arg("stream"))
+      .def("error", &XgmiComm::error)
+      .def("set_timeout_seconds", &XgmiComm::set_timeout_seconds)
+      .def_property_readonly("connected", &XgmiComm::connected)
+      .def_property_readonly("world_size", &XgmiComm::world_size)
+      .def_property_readonly("rank", &XgmiComm::rank);
+
   // ---------------- DDP gradient reducer (module-level path) ----------------
   py::class_<BucketReducer>(m, "BucketReducer")
       .def(py::init([](std::vector<std::vector<int64_t>> numels, int world, std::shared_ptr<RcclComm> comm) {
@@ -213,6 +240,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
       .def("attach_comm", &Engine::attach_comm)
       .def("attach_comm2", &Engine::attach_comm2)
+      .def("attach_xgmi", &Engine::attach_xgmi)
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_concurrent", &Engine::set_concurrent)
       .def("set_dist_schedule", &Engine::set_dist_schedule)

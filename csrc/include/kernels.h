@@ -169,4 +169,21 @@ void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStre
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 
+// direct xGMI all-reduce (reduce-scatter + all-gather over IPC-mapped peer buckets; xgmi_allreduce.hip)
+constexpr int XGMI_MAX_RANKS = 8;          // one node
+constexpr int XGMI_MAX_WG = 256;           // flag slots per (stage, rank)
+constexpr int XGMI_FLAG_INTS = 2 * XGMI_MAX_RANKS * XGMI_MAX_WG;   // [stage][src rank][wg]
+struct XgmiArgs {
+  const float* in[XGMI_MAX_RANKS];   // every rank's input bucket (peer mappings; own = local)
+  float* out[XGMI_MAX_RANKS];        // every rank's output bucket
+  int* flags[XGMI_MAX_RANKS];        // every rank's flag block of this channel
+  int* ctr;                          // local per-WG call counters [XGMI_MAX_WG]
+  int* err;                          // local error flag (timeout)
+  int world, rank;
+  int64_t nvec;                      // bucket length in float4s
+  uint64_t timeout_ticks;            // s_memrealtime ticks (100 MHz)
+};
+int xgmi_workgroups(int64_t nvec, int world);
+void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
+
 }  // namespace mnist

@@ -1,0 +1,155 @@
+// Direct xGMI all-reduce for the DDP gradient buckets (runtime/xgmi_comm.cpp).
+//
+// MI355X GPUs in a node are fully connected by point-to-point xGMI links (7 per GPU), so a ring
+// (what RCCL picks for a 4.7 MB bucket) drives only 2 of them per GPU and pays 2(W-1) latency-bound
+// hops.  Here every rank maps every peer's bucket (IPC) and the sum is two direct phases:
+//   phase 1 (reduce-scatter): rank r reads shard r of all W input buckets over the W-1 links at
+//            once, sums them in rank order 0..W-1 (same bits on every rank, run to run) and writes
+//            shard r of its OUTPUT bucket;
+//   phase 2 (all-gather):     rank r reads shard p of rank p's output bucket for every p != r.
+// Inputs and outputs are separate buffers, so the only hand-offs are "every rank's inputs are
+// final" (stage 0) and "every rank's shard is reduced" (stage 1): a rank's next-step producer
+// kernels overwrite only its input bucket, which peers read before stage 1 completes, and its
+// next call writes its output shard only after stage 0 of that call (= after every peer left
+// phase 2 of this one).
+//
+// Hand-offs are per workgroup: WG b of every rank covers the same index set in both phases, so WG b
+// waits only for WG b of the peers (no grid-wide barrier, no co-residency requirement).  Payload
+// loads/stores are buffer ops with sc0 sc1 (system-coherent: bypass this GPU's caches and write
+// through), drained with s_waitcnt vmcnt(0) before the workgroup barrier that precedes the flag
+// stores; flags are system-scope atomics carrying a per-WG call counter (monotonic, no reset, so
+// graph replays need no host work).  A wait that exceeds the timeout sets *err and returns; every
+// later call then returns at once and the host raises (XgmiComm::check).
+#include "../include/kernels.h"
+
+namespace mnist {
+
+namespace {
+typedef __attribute__((ext_vector_type(4))) float f4;
+constexpr int SYS = 17;   // cache policy bits: sc0 | sc1 (system scope)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 ld_sys(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, SYS));
+}
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, int64_t i, f4 v) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u4;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)(i * 16), 0, SYS);
+}
+
+// Stage hand-off of workgroup b: lane p (< world) publishes this WG's call counter into rank p's
+// flag slot [stage][my rank][b], then polls its own slot [stage][p][b].  Returns false (and sets
+// *err) on timeout.
+__device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
+  __syncthreads();
+  bool ok = true;
+  const int p = threadIdx.x;
+  if (p < a.world) {
+    __hip_atomic_store(a.flags[p] + (stage * XGMI_MAX_RANKS + a.rank) * XGMI_MAX_WG + b, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    const int* slot = a.flags[a.rank] + (stage * XGMI_MAX_RANKS + p) * XGMI_MAX_WG + b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();            // 100 MHz
+    while (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+    }
+  }
+  return __syncthreads_and(ok);
+}
+}  // namespace
+
+// W is a template parameter so the per-peer loads unroll into one straight batch (a runtime
+// `p < world` guard makes hipcc wait vmcnt(0) after every load).  Buffer ops are bounds-checked by
+// the descriptor: loads past the bucket return 0 and stores past it are dropped, so the shard
+// edges need no guards, and a zero-length descriptor turns a load into a no-op.
+template <int W>
+__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
+  __shared__ int s_epoch, s_err;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    const int e = a.ctr[b] + 1;          // only this lane of this WG touches ctr[b]; calls are stream ordered
+    a.ctr[b] = e;
+    s_epoch = e;
+    s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_err) return;
+  const int e = s_epoch;
+  const int r = a.rank;
+  const int64_t S4 = (a.nvec + W - 1) / W;                 // float4s per shard
+  const int64_t step = (int64_t)gridDim.x * 256;
+  const int64_t bytes = a.nvec * 16;
+  const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
+
+  if (!xgmi_stage(a, 0, b, e)) return;
+  // ---- phase 1: shard r of the sum -> my output
+  {
+    __amdgpu_buffer_rsrc_t in[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) in[p] = rsrc(a.in[p], bytes);
+    const int64_t hi = (r + 1) * S4;
+    for (int64_t i = r * S4 + (int64_t)b * 256 + tid; i < hi; i += 2 * step) {
+      const int64_t i2 = i + step;
+      f4 v[W], w[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        v[p] = ld_sys(in[p], i);
+        w[p] = ld_sys(in[p], i2);
+      }
+      f4 s = v[0], t = w[0];
+#pragma unroll
+      for (int p = 1; p < W; ++p) {
+        s += v[p];
+        t += w[p];
+      }
+      st_sys(out, i, s);
+      if (i2 < hi) st_sys(out, i2, t);
+    }
+  }
+  if (!xgmi_stage(a, 1, b, e)) return;
+  // ---- phase 2: every other rank's reduced shard -> my output (the same index set per WG)
+  {
+    __amdgpu_buffer_rsrc_t src[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) src[p] = rsrc(a.out[p], p == r ? 0 : bytes);   // own shard: no-op load
+    for (int64_t k = (int64_t)b * 256 + tid; k < S4; k += step) {
+      f4 v[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) v[p] = ld_sys(src[p], p * S4 + k);
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (p != r) st_sys(out, p * S4 + k, v[p]);
+    }
+  }
+}
+
+int xgmi_workgroups(int64_t nvec, int world) {
+  const int64_t s4 = (nvec + world - 1) / world;
+  int64_t g = (s4 + 511) / 512;                      // >= 2 float4 per lane per phase-1 pass
+  if (g < 1) g = 1;
+  if (g > XGMI_MAX_WG) g = XGMI_MAX_WG;
+  return (int)g;
+}
+
+void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
+  const dim3 g(xgmi_workgroups(a.nvec, a.world)), blk(256);
+  switch (a.world) {
+    case 2: hipLaunchKernelGGL(xgmi_allreduce_kernel<2>, g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(xgmi_allreduce_kernel<3>, g, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL(xgmi_allreduce_kernel<4>, g, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(xgmi_allreduce_kernel<5>, g, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL(xgmi_allreduce_kernel<6>, g, blk, 0, s, a); break;
+    case 7: hipLaunchKernelGGL(xgmi_allreduce_kernel<7>, g, blk, 0, s, a); break;
+    case 8: hipLaunchKernelGGL(xgmi_allreduce_kernel<8>, g, blk, 0, s, a); break;
+    default: break;   // world 1: nothing to reduce (the host rejects > XGMI_MAX_RANKS)
+  }
+}
+
+}  // namespace mnist

@@ -92,6 +92,12 @@ void Engine::attach_comm2(std::shared_ptr<RcclComm> comm) {
   comm2_ = std::move(comm);
 }
 
+void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
+  if (x && x->world_size() != world_) throw std::runtime_error("xgmi world size mismatch");
+  if (x && x->world_size() > 1 && !x->connected()) throw std::runtime_error("xgmi communicator not connected");
+  xgmi_ = std::move(x);
+}
+
 void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags) {
   StepState host{step0, flags, seed, rng_base};
   // tiny H2D of 24 bytes, ordered on the compute stream (never inside a captured graph)
@@ -112,7 +118,9 @@ void Engine::enqueue_step(int batch, bool last) {
   const int32_t* labels = pre ? buf_.epoch_labels : buf_.train_labels;
   TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
-  const bool sched3 = comm_ && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 3;
+  // the direct xGMI all-reduce runs in schedule 3 (its two channels = the two RCCL communicators)
+  const bool sched3 = (comm_ && comm2_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3;
+  if (xgmi_ && !sched3 && !comm_) throw std::runtime_error("xgmi all-reduce needs DDP schedule 3 (or an RCCL comm)");
   if (sched3 && !side_forked_) {       // once per chunk: order the comm stream after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
@@ -131,7 +139,7 @@ void Engine::enqueue_step(int batch, bool last) {
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
-  const bool dist = comm_ != nullptr;   // world_size 1 + comm exercises the DDP schedule (tests)
+  const bool dist = comm_ != nullptr || xgmi_ != nullptr;   // world_size 1 + comm: DDP schedule (tests)
   // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t
   // the step started with while role A writes the updated one, so the transposed shadow alternates
   // between buf_.w1t and w1t_alt_ (host-tracked, static within a captured chunk); a chunk that
@@ -154,16 +162,20 @@ void Engine::enqueue_step(int batch, bool last) {
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
   if (sched3) {
+    // xGMI: the reduced gradients land in the communicator's output buffer, the update reads there
+    if (xgmi_) ad.grad = adc.grad = xgmi_->out();
     launch_stream_signal(sync_ + 0, compute_);               // fc grads of this step are final
     launch_conv_wgrad(cb, B, compute_);
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
+    else comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
     launch_adadelta(ad, ADA_FC, comm_stream_);
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
     side_pending_ = true;
     launch_conv_dgrad(cb, B, compute_);
     launch_conv_grad_reduce(cb, B, compute_);
-    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+    if (xgmi_) xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);
+    else comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
     launch_adadelta(adc, ADA_CONV, compute_);
     if (last) {                                              // chunk end: one real join edge
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
@@ -355,6 +367,7 @@ void Engine::synchronize() {
   int err = 0;
   HIP_OK(hipMemcpy(&err, sync_ + 2, sizeof(int), hipMemcpyDeviceToHost));
   if (err) throw std::runtime_error("engine: a schedule-3 stream hand-off timed out (results invalid)");
+  if (xgmi_ && xgmi_->error()) throw std::runtime_error("engine: an xGMI all-reduce stage timed out (results invalid)");
 }
 
 }  // namespace mnist

@@ -24,6 +24,7 @@
 
 #include "../include/kernels.h"
 #include "rccl_comm.h"
+#include "xgmi_comm.h"
 
 namespace mnist {
 
@@ -63,6 +64,10 @@ class Engine {
   // second communicator for the fc bucket: lets it stay in flight across the step boundary
   // (joined only before the next step's fc1) while the conv bucket reduces on the first
   void attach_comm2(std::shared_ptr<RcclComm> comm);
+  // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC over buf.grad -> x->out()) in place
+  // of the RCCL all-reduces of schedule 3; RCCL stays attached for the parameter broadcast
+  void attach_xgmi(std::shared_ptr<XgmiComm> x);
+  static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1;
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
   void set_concurrent(bool on) { concurrent_ = on; }
   // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
@@ -113,6 +118,7 @@ class Engine {
   bool concurrent_ = false;
   int dist_sched_ = 1;
   std::shared_ptr<RcclComm> comm_, comm2_;
+  std::shared_ptr<XgmiComm> xgmi_;
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error

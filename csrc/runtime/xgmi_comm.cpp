@@ -1,0 +1,150 @@
+#include "xgmi_comm.h"
+
+#include <string.h>
+#include <unistd.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "../include/kernels.h"
+
+namespace mnist {
+
+namespace {
+void ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("xgmi: ") + what + ": " + hipGetErrorString(e));
+}
+
+// export record of one rank: where its input / output buckets and flag blocks live
+struct Record {
+  hipIpcMemHandle_t in_h, out_h, flags_h;
+  int64_t in_off, out_off;
+  int64_t numel;
+  int32_t world, rank, channels, pid;
+};
+
+void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  ok(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)), "hipMemGetAddressRange");
+  ok(hipIpcGetMemHandle(h, base), "hipIpcGetMemHandle");
+  *off = (int64_t)((const char*)p - (const char*)base);
+}
+}  // namespace
+
+XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels)
+    : world_(world), rank_(rank), device_(device), channels_(channels), in_(in), out_(out), numel_(numel) {
+  if (world < 1 || world > XGMI_MAX_RANKS) throw std::runtime_error("xgmi: world size must be 1..8");
+  if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
+  if (channels < 1) throw std::runtime_error("xgmi: need at least one channel");
+  if (((uintptr_t)in | (uintptr_t)out) & 15) throw std::runtime_error("xgmi: buffers must be 16-byte aligned");
+  ok(hipSetDevice(device), "hipSetDevice");
+  ok(hipMalloc(&flags_, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMalloc(flags)");
+  ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
+  ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
+  ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
+  ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
+  ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
+  ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  set_timeout_seconds(60.0);
+}
+
+XgmiComm::~XgmiComm() {
+  hipSetDevice(device_);
+  hipDeviceSynchronize();
+  for (void* p : opened_) hipIpcCloseMemHandle(p);
+  if (flags_) hipFree(flags_);
+  if (ctr_) hipFree(ctr_);
+  if (err_) hipFree(err_);
+}
+
+void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
+
+std::vector<uint8_t> XgmiComm::record() const {
+  Record r;
+  memset(&r, 0, sizeof(r));
+  export_ptr(in_, &r.in_h, &r.in_off);
+  export_ptr(out_, &r.out_h, &r.out_off);
+  int64_t foff = 0;
+  export_ptr(flags_, &r.flags_h, &foff);
+  if (foff != 0) throw std::runtime_error("xgmi: flag block is not an allocation base");
+  r.numel = numel_;
+  r.world = world_;
+  r.rank = rank_;
+  r.channels = channels_;
+  r.pid = (int32_t)getpid();
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(&r);
+  return std::vector<uint8_t>(b, b + sizeof(r));
+}
+
+void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
+  if ((int)records.size() != world_) throw std::runtime_error("xgmi: need one record per rank");
+  ok(hipSetDevice(device_), "hipSetDevice");
+  peer_in_.assign(world_, nullptr);
+  peer_out_.assign(world_, nullptr);
+  peer_flags_.assign(world_, nullptr);
+  // one mapping per distinct handle (the input and output buckets may share a caching-allocator segment)
+  std::vector<std::pair<hipIpcMemHandle_t, void*>> maps;
+  auto open = [&](const hipIpcMemHandle_t& h) -> char* {
+    for (auto& m : maps)
+      if (memcmp(&m.first, &h, sizeof(h)) == 0) return (char*)m.second;
+    void* p = nullptr;
+    ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    opened_.push_back(p);
+    maps.emplace_back(h, p);
+    return (char*)p;
+  };
+  for (int q = 0; q < world_; ++q) {
+    if (records[q].size() != sizeof(Record)) throw std::runtime_error("xgmi: bad record size");
+    Record r;
+    memcpy(&r, records[q].data(), sizeof(r));
+    if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_)
+      throw std::runtime_error("xgmi: peer record does not match this communicator");
+    if (q == rank_) {
+      peer_in_[q] = in_;
+      peer_out_[q] = out_;
+      peer_flags_[q] = flags_;
+      continue;
+    }
+    peer_in_[q] = reinterpret_cast<const float*>(open(r.in_h) + r.in_off);
+    peer_out_[q] = reinterpret_cast<float*>(open(r.out_h) + r.out_off);
+    peer_flags_[q] = reinterpret_cast<int*>(open(r.flags_h));
+  }
+  connected_ = true;
+}
+
+void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream) {
+  if (channel < 0 || channel >= channels_) throw std::runtime_error("xgmi: bad channel");
+  if (offset < 0 || count < 0 || offset + count > numel_ || (offset & 3) || (count & 3))
+    throw std::runtime_error("xgmi: range must lie in the buffer, offset and count multiples of 4");
+  if (count == 0) return;
+  if (world_ == 1) {
+    if (out_ != in_)
+      ok(hipMemcpyAsync(out_ + offset, in_ + offset, count * sizeof(float), hipMemcpyDeviceToDevice, stream),
+         "hipMemcpyAsync");
+    return;
+  }
+  if (!connected_) throw std::runtime_error("xgmi: connect() first");
+  XgmiArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int q = 0; q < world_; ++q) {
+    a.in[q] = peer_in_[q] + offset;
+    a.out[q] = peer_out_[q] + offset;
+    a.flags[q] = peer_flags_[q] + (int64_t)channel * XGMI_FLAG_INTS;
+  }
+  a.ctr = ctr_ + (int64_t)channel * XGMI_MAX_WG;
+  a.err = err_;
+  a.world = world_;
+  a.rank = rank_;
+  a.nvec = count / 4;
+  a.timeout_ticks = timeout_ticks_;
+  launch_xgmi_allreduce(a, stream);
+}
+
+int XgmiComm::error() const {
+  int v = 0;
+  ok(hipMemcpy(&v, err_, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy(err)");
+  return v;
+}
+
+}  // namespace mnist

@@ -1,0 +1,58 @@
+// Direct xGMI gradient all-reduce between the GPUs of one node (kernels/xgmi_allreduce.hip).
+//
+// The reference averages DDP gradients with ProcessGroupNCCL's ring all-reduce (mnist_ddp.py:173,
+// reducer at :72).  On MI355X every GPU pair has its own xGMI link, so this communicator maps every
+// peer's gradient buckets into its address space once (hipIpc handles exchanged through the c10d
+// store) and reduces with one kernel per bucket: a reduce-scatter that pulls shard r of all peers
+// over all links at once, then an all-gather of the reduced shards - two direct hops instead of the
+// ring's 2(W-1).  Input (the producers' gradient buffer) and output (what the optimizer reads) are
+// separate buffers, which removes the end-of-call barrier an in-place version needs.
+//
+// Channels: independent flag / counter sets, one per bucket that may be in flight concurrently with
+// another (the engine's fc bucket on the comm stream, conv bucket on the compute stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+
+namespace mnist {
+
+class XgmiComm {
+ public:
+  // in / out: this rank's flat input and output buffers of `numel` floats (device allocations that
+  // support IPC export: hipMalloc or blocks of torch's caching allocator)
+  XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels);
+  ~XgmiComm();
+  XgmiComm(const XgmiComm&) = delete;
+  XgmiComm& operator=(const XgmiComm&) = delete;
+
+  std::vector<uint8_t> record() const;                               // this rank's export record
+  void connect(const std::vector<std::vector<uint8_t>>& records);   // every rank's, in rank order
+  bool connected() const { return connected_; }
+
+  // out[offset, offset+count) = sum over ranks of in[offset, offset+count); offset and count in
+  // floats, multiples of 4.  Graph-capturable (no host work beyond the launch).
+  void allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream);
+  // device error flag (a stage wait timed out on this rank); synchronous read
+  int error() const;
+  void set_timeout_seconds(double s);
+  int world_size() const { return world_; }
+  int rank() const { return rank_; }
+  float* out() const { return out_; }
+
+ private:
+  int world_, rank_, device_, channels_;
+  float *in_, *out_;
+  int64_t numel_;
+  int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
+  int* ctr_ = nullptr;       // [channels][XGMI_MAX_WG], local
+  int* err_ = nullptr;
+  uint64_t timeout_ticks_;
+  bool connected_ = false;
+  std::vector<const float*> peer_in_;
+  std::vector<float*> peer_out_;
+  std::vector<int*> peer_flags_;
+  std::vector<void*> opened_;   // IPC mappings to close
+};
+
+}  // namespace mnist

@@ -44,7 +44,7 @@ class FusedTrainer:
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
                  two_buckets: bool = True, concurrent: bool | None = None, comm2=None,
-                 fuse_fc_update: bool | None = None):
+                 fuse_fc_update: bool | None = None, allreduce: str | None = None):
         C = native.load()
         self.C, self.ms = C, mstate
         dev = mstate.device
@@ -105,6 +105,23 @@ class FusedTrainer:
         if comm2 is not None:
             self.engine.attach_comm2(comm2)
         self.comm, self.comm2 = comm, comm2
+        # gradient all-reduce: "rccl" (ncclAllReduce per bucket) or "xgmi" (direct reduce-scatter +
+        # all-gather over IPC-mapped peer buckets, csrc/runtime/xgmi_comm.h; self-tested at startup,
+        # falls back to RCCL on every rank if any rank fails).  Used on the DDP path (world > 1 or an
+        # attached RCCL comm); RCCL stays attached for the parameter broadcast.
+        if allreduce is None:
+            allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "rccl")
+        if allreduce not in ("rccl", "xgmi"):
+            raise ValueError(f"allreduce must be 'rccl' or 'xgmi', got {allreduce!r}")
+        self.xgmi, self.grad_out = None, None
+        if allreduce == "xgmi" and (comm is not None or world_size > 1):
+            from ..parallel.distributed import create_xgmi_comm
+            self.grad_out = torch.zeros_like(mstate.grad)
+            self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad, self.grad_out)
+            if self.xgmi is not None:
+                self.engine.set_dist_schedule(3)
+                self.engine.attach_xgmi(self.xgmi)
+        self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None
         self.use_graphs = self.graph_steps > 0

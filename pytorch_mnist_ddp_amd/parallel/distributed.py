@@ -93,3 +93,95 @@ def create_rccl_comms(world_size: int, rank: int, device: int, n: int = 2):
     conv bucket on the first and the fc bucket on the second, concurrently)."""
     return [create_rccl_comm(world_size, rank, device, tag=str(i)) for i in range(n)]
 
+
+
+_XGMI_KEY = "pytorch_mnist_ddp_amd/xgmi_record"
+_xgmi_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
+
+
+def _all_ok(flag: bool, device) -> bool:
+    """Every rank's verdict (MIN over the default process group)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return flag
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device if on_gpu else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, grad_out: torch.Tensor,
+                     tag: str | None = None, channels: int = 2, verify: bool = True):
+    """Direct xGMI all-reduce communicator over ``grad_in`` -> ``grad_out`` (csrc/runtime/xgmi_comm.h).
+
+    Every rank exports IPC handles of its two buffers and its flag blocks through the c10d store and
+    maps every peer's.  With ``verify`` each channel is then exercised on a rank-dependent pattern
+    whose sum is exact in fp32 (5 s stage timeout), and the ranks agree on the outcome.  Returns the
+    communicator, or ``None`` on every rank when any rank failed to map its peers or to verify
+    (callers then keep the RCCL all-reduce)."""
+    from ..ops import native
+    global _xgmi_seq
+    C = native.load()
+    if tag is None:
+        tag = str(_xgmi_seq)
+    _xgmi_seq += 1
+    dev = torch.device(device)
+    numel = grad_in.numel()
+    x = None
+    try:
+        x = C.XgmiComm(world_size, rank, dev.index or 0, native.ptr(grad_in), native.ptr(grad_out), numel, channels)
+        if world_size > 1:
+            store = dist.distributed_c10d._get_default_store()
+            store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
+            keys = [f"{_XGMI_KEY}/{tag}/{q}" for q in range(world_size)]
+            store.wait(keys, timedelta(minutes=5))
+            x.connect([store.get(k) for k in keys])
+        ok = True
+    except RuntimeError as e:
+        print(f"[xgmi] rank {rank}: setup failed ({e})", flush=True)
+        ok = False
+    if not _all_ok(ok, dev):
+        return None
+    if verify:
+        ok = _verify_xgmi(x, world_size, rank, grad_in, grad_out, channels)
+        if not _all_ok(ok, dev):
+            if rank == 0:
+                print("[xgmi] self-test failed: keeping the RCCL all-reduce", flush=True)
+            return None
+    return x
+
+
+def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torch.Tensor, channels: int) -> bool:
+    n = grad_in.numel()
+    cut = (n // 2) & ~3                                  # channel c covers its own quarter-aligned range
+    ranges = [(0, cut), (cut, n - cut)] if channels >= 2 else [(0, n)]
+    i = torch.arange(n, device=grad_in.device, dtype=torch.float32)
+    base = torch.remainder(i, 97.0) * 0.25 - 3.0         # multiples of 1/4 in [-3, 21]: sums are exact
+    s_main = torch.cuda.current_stream(grad_in.device)
+    side = torch.cuda.Stream(device=grad_in.device)
+    x.set_timeout_seconds(5.0)
+    ok = True
+    try:
+        for it in range(3):                              # repeated calls exercise the per-WG counters
+            scale = float(it + 1)
+            with torch.no_grad():
+                grad_in.copy_(base * (scale * (rank + 1)))
+                grad_out.fill_(float("nan"))
+            torch.cuda.synchronize(grad_in.device)
+            streams = [s_main, side]
+            for c, (off, cnt) in enumerate(ranges):       # both channels in flight concurrently
+                x.allreduce(c, off, cnt, streams[c % 2].cuda_stream)
+            torch.cuda.synchronize(grad_in.device)
+            expect = base * (scale * world * (world + 1) / 2)
+            if x.error() or not torch.equal(grad_out, expect):
+                ok = False
+                break
+    except RuntimeError as e:
+        print(f"[xgmi] rank {rank}: self-test error ({e})", flush=True)
+        ok = False
+    finally:
+        x.set_timeout_seconds(60.0)
+        with torch.no_grad():
+            grad_in.zero_()
+            grad_out.zero_()
+        torch.cuda.synchronize(grad_in.device)
+    return ok

@@ -141,12 +141,17 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         tr = load_mnist(synthetic_data=True, train=True, synthetic_size=1024, verbose=False)
         idx = torch.randperm(1024, generator=torch.Generator().manual_seed(0))
         res = []
-        # schedule 1 (one comm), schedule 2 (cross-step fc branch, two comms), eager schedule 2, no comm
-        for c, c2, gs, sched in ((comm, None, 4, 1), (comm, comm2, 4, 2), (comm, comm2, 0, 2),
-                                 (comm, comm2, 4, 3), (comm, comm2, 0, 3), (None, None, 4, 1)):
+        # schedule 1 (one comm), schedule 2 (cross-step fc branch, two comms), eager schedule 2,
+        # schedule 3 with RCCL and with the xGMI all-reduce (world 1: its output buffer path), no comm
+        for c, c2, gs, sched, ar in ((comm, None, 4, 1, "rccl"), (comm, comm2, 4, 2, "rccl"),
+                                     (comm, comm2, 0, 2, "rccl"), (comm, comm2, 4, 3, "rccl"),
+                                     (comm, comm2, 0, 3, "rccl"), (comm, comm2, 4, 3, "xgmi"),
+                                     (comm, comm2, 0, 3, "xgmi"), (None, None, 4, 1, "rccl")):
             torch.manual_seed(5)
             ms = ModelState(Net(), cuda_device)
-            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=gs, comm2=c2)
+            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=gs, comm2=c2,
+                             allreduce=ar)
+            assert t.allreduce == ar
             t.engine.set_dist_schedule(sched)
             t.train_epoch(1, idx)
             t.synchronize()
