@@ -61,8 +61,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--force-comm", action="store_true",
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
-    ap.add_argument("--allreduce", choices=["rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "rccl"),
-                    help="DDP gradient all-reduce: RCCL, or the direct xGMI reduce-scatter/all-gather kernel")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
+                    help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernel, or "
+                         "auto (time both at startup, keep the faster)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,7 +186,8 @@ def main() -> int:
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
                        "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
-                       "allreduce": tr.allreduce if world > 1 or comm is not None else None},
+                       "allreduce": tr.allreduce if world > 1 or comm is not None else None,
+                       "allreduce_probe_us": tr.allreduce_timings or None},
             "wallclock_20ep_s": round(wall, 3) if wall is not None else None,
             "baseline_wallclock_20ep_s": base,
             "vs_baseline_wallclock": round(base / wall, 1) if (wall and base) else None,

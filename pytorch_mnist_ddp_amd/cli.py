@@ -70,6 +70,9 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='DDP gradient bucket cap in MiB (default 25, as torch DDP)')
     g.add_argument('--first-bucket-mb', type=float, default=1.0,
                    help='DDP first-bucket cap in MiB (default 1, as torch DDP)')
+    g.add_argument('--allreduce', choices=['auto', 'rccl', 'xgmi'], default=None,
+                   help='DDP gradient all-reduce of the fused engine: RCCL, the direct xGMI kernel, or auto '
+                        '(default; times both at startup and keeps the faster)')
     g.add_argument('--profile', action='store_true', default=False,
                    help='emit roctx ranges and per-epoch device timings')
     g.add_argument('--json-log', default=None, help='append per-epoch JSON metrics to this file')

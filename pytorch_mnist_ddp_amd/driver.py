@@ -177,7 +177,9 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
-                           comm2=comm2)
+                           comm2=comm2, allreduce=getattr(args, 'allreduce', None))
+    if distributed and rank == 0 and trainer.allreduce_timings:
+        print(f"| gradient all-reduce: {trainer.allreduce} (probe us/step: {trainer.allreduce_timings})", flush=True)
     trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper
     n_train = len(train_data)
     n_batches = num_batches(len(train_stream), args.batch_size)

@@ -105,19 +105,30 @@ class FusedTrainer:
         if comm2 is not None:
             self.engine.attach_comm2(comm2)
         self.comm, self.comm2 = comm, comm2
-        # gradient all-reduce: "rccl" (ncclAllReduce per bucket) or "xgmi" (direct reduce-scatter +
+        # gradient all-reduce: "rccl" (ncclAllReduce per bucket), "xgmi" (direct reduce-scatter +
         # all-gather over IPC-mapped peer buckets, csrc/runtime/xgmi_comm.h; self-tested at startup,
-        # falls back to RCCL on every rank if any rank fails).  Used on the DDP path (world > 1 or an
-        # attached RCCL comm); RCCL stays attached for the parameter broadcast.
+        # falls back to RCCL on every rank if any rank fails) or "auto" (default: with world > 1 and
+        # RCCL comms attached, time both on this node's links and keep the faster).  Used on the DDP
+        # path; RCCL stays attached for the parameter broadcast.
         if allreduce is None:
-            allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "rccl")
-        if allreduce not in ("rccl", "xgmi"):
-            raise ValueError(f"allreduce must be 'rccl' or 'xgmi', got {allreduce!r}")
-        self.xgmi, self.grad_out = None, None
-        if allreduce == "xgmi" and (comm is not None or world_size > 1):
-            from ..parallel.distributed import create_xgmi_comm
+            allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
+        if allreduce not in ("rccl", "xgmi", "auto"):
+            raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
+        self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
+        want = allreduce == "xgmi" and (comm is not None or world_size > 1)
+        want = want or (allreduce == "auto" and comm is not None and world_size > 1)
+        if want:
+            from ..parallel.distributed import choose_allreduce, create_xgmi_comm
             self.grad_out = torch.zeros_like(mstate.grad)
             self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad, self.grad_out)
+            if self.xgmi is not None and allreduce == "auto":
+                split = mstate.bucket_split
+                with torch.cuda.stream(self.compute):
+                    pick, self.allreduce_timings = choose_allreduce(
+                        comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad, self.grad_out,
+                        (0, split), (split, mstate.grad.numel() - split), dev)
+                if pick != "xgmi":
+                    self.xgmi = None
             if self.xgmi is not None:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)

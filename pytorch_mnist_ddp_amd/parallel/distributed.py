@@ -185,3 +185,56 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
             grad_out.zero_()
         torch.cuda.synchronize(grad_in.device)
     return ok
+
+
+def _max_over_ranks(v: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return v
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([v], dtype=torch.float64, device=device if on_gpu else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def time_bucket_allreduce(calls, device, iters: int = 20, warmup: int = 3) -> float:
+    """Microseconds per invocation of ``calls`` (a list of zero-argument launchers enqueued on the
+    current stream), max over ranks; all ranks must call this collectively."""
+    for _ in range(warmup):
+        for c in calls:
+            c()
+    torch.cuda.synchronize(device)
+    barrier()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(iters):
+        for c in calls:
+            c()
+    t1.record()
+    t1.synchronize()
+    return _max_over_ranks(t0.elapsed_time(t1) * 1000.0 / iters, device)
+
+
+def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad_in: torch.Tensor, grad_out: torch.Tensor,
+                     fc_range: tuple[int, int], conv_range: tuple[int, int], device) -> tuple[str, dict]:
+    """Measure one step's two bucket all-reduces with RCCL and with the direct xGMI kernel on this
+    node and return the faster (``"rccl"`` / ``"xgmi"``) plus the timings - the same decision on
+    every rank (timings are maxima over ranks).  Buffers are zeroed afterwards."""
+    from ..ops import native
+    s = torch.cuda.current_stream(device).cuda_stream
+    gp = native.ptr(grad_in)
+    with torch.no_grad():
+        grad_in.zero_()
+    rc = [lambda: rccl_fc.allreduce_sum(gp + 4 * fc_range[0], fc_range[1], 0, s),
+          lambda: rccl_conv.allreduce_sum(gp + 4 * conv_range[0], conv_range[1], 0, s)]
+    xc = [lambda: xgmi.allreduce(1, fc_range[0], fc_range[1], s),
+          lambda: xgmi.allreduce(0, conv_range[0], conv_range[1], s)]
+    t_r = time_bucket_allreduce(rc, device)
+    t_x = time_bucket_allreduce(xc, device)
+    err = _max_over_ranks(float(xgmi.error()), device)
+    with torch.no_grad():
+        grad_in.zero_()
+        grad_out.zero_()
+    torch.cuda.synchronize(device)
+    pick = "xgmi" if (err == 0 and t_x < t_r) else "rccl"
+    return pick, {"rccl_us": round(t_r, 1), "xgmi_us": round(t_x, 1)}

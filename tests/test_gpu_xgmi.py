@@ -18,3 +18,31 @@ def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=dict(os.environ, PYTHONPATH=ROOT))
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+
+
+def test_allreduce_auto_choice_plumbing_world1(cuda_device):
+    """choose_allreduce at world 1 (RCCL comms + the xGMI communicator's copy path): both launch
+    sequences run, the timings come back and the buffers are left zeroed."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from pytorch_mnist_ddp_amd.parallel.distributed import choose_allreduce, create_rccl_comms, create_xgmi_comm
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=cuda_device)
+    try:
+        c0, c1 = create_rccl_comms(1, 0, 0)
+        n, split = 1200000, 1181120
+        gin = torch.randn(n, device=cuda_device)
+        gout = torch.randn(n, device=cuda_device)
+        x = create_xgmi_comm(1, 0, cuda_device, gin, gout)
+        assert x is not None
+        pick, t = choose_allreduce(c1, c0, x, gin, gout, (0, split), (split, n - split), cuda_device)
+        assert pick in ("rccl", "xgmi") and t["rccl_us"] > 0 and t["xgmi_us"] > 0
+        assert int(gin.abs().sum().item()) == 0 and int(gout.abs().sum().item()) == 0
+    finally:
+        dist.destroy_process_group()
