@@ -175,5 +175,10 @@ __global__ void set_step_kernel(StepState* st, int step) { st->step = step; }
 void launch_set_step(StepState* st, int step, hipStream_t s) {
   hipLaunchKernelGGL(set_step_kernel, dim3(1), dim3(1), 0, s, st, step);
 }
+// the whole StepState from kernel arguments: stream ordered, no host buffer to keep alive, no sync
+__global__ void set_state_kernel(StepState* st, StepState v) { *st = v; }
+void launch_set_state(StepState* st, const StepState& v, hipStream_t s) {
+  hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(1), 0, s, st, v);
+}
 
 }  // namespace mnist

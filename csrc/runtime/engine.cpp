@@ -42,15 +42,18 @@ Engine::~Engine() {
 }
 
 void Engine::alloc_workspace() {
-  const int M = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
-  const int Mp = round_up(M, 64);
+  // forward activations (p, fc1 partials) serve the training batch and the eval batch (which may
+  // be the whole test split in one launch); the backward-only buffers only the training batch
+  const int Ma = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
+  const int M = max_batch_;
+  const int Mp = round_up(M, 64), Map = round_up(Ma, 64);
   const int G = conv_wgrad_groups(max_batch_);   // monotonic in B
   int64_t off = 0;
   auto carve = [&](int64_t bytes) { int64_t o = off; off += align256(bytes); return o; };
   const int64_t o_a1 = carve((int64_t)M * H1 * H1 * C1 * 2);
-  const int64_t o_p = carve((int64_t)Mp * NFLAT * 2);
+  const int64_t o_p = carve((int64_t)Map * NFLAT * 2);
   const int64_t o_pm = carve((int64_t)M * NFLAT);
-  const int64_t o_z1 = carve((int64_t)FC1_KSPLIT * M * NH * 4);
+  const int64_t o_z1 = carve((int64_t)FC1_KSPLIT * Ma * NH * 4);
   const int64_t o_lr = carve((int64_t)M * 4);
   const int64_t o_dz = carve((int64_t)Mp * NH * 2);
   const int64_t o_h = carve((int64_t)Mp * NH * 2);
@@ -99,10 +102,9 @@ void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
 }
 
 void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags) {
-  StepState host{step0, flags, seed, rng_base};
-  // tiny H2D of 24 bytes, ordered on the compute stream (never inside a captured graph)
-  HIP_OK(hipMemcpyAsync(buf_.state, &host, sizeof(StepState), hipMemcpyHostToDevice, compute_));
-  HIP_OK(hipStreamSynchronize(compute_));   // `host` lives on this stack frame
+  // 24 bytes as kernel arguments, ordered on the compute stream (never inside a captured graph):
+  // no host sync, so the next epoch is enqueued while the previous one still runs
+  launch_set_state(buf_.state, StepState{step0, flags, seed, rng_base}, compute_);
 }
 
 void Engine::enqueue_step(int batch, bool last) {

@@ -82,7 +82,11 @@ class FusedTrainer:
             bufs.update(test_u8=p(self.test_u8), test_labels=p(self.test_labels), test_idx=p(self.test_idx),
                         test_loss_rows=p(self.test_loss_rows), test_correct=p(self.test_correct))
         torch.cuda.synchronize(dev)
-        self.engine = C.Engine(bufs, self.B, max(self.TB, 1) if test is not None else 1,
+        # evaluation runs the whole test split as ONE batch (per-row results are bitwise the same as
+        # with --test-batch-size chunks: every eval kernel computes rows independently and the
+        # losses / hits are summed once on the host): 3 launches instead of 3 per 1000 images
+        self.eval_batch = self.n_test if 0 < self.n_test <= 16384 else max(self.TB, 1)
+        self.engine = C.Engine(bufs, self.B, max(self.eval_batch, self.TB, 1) if test is not None else 1,
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay)
         self.engine.set_bucket_split(two_buckets)
@@ -171,11 +175,13 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------ training
     def train_epoch(self, epoch: int, idx: torch.Tensor, log_interval: int = 10, dry_run: bool = False,
-                    log_fn=None) -> EpochStats:
+                    log_fn=None, sync: bool = True) -> EpochStats:
         """Run one epoch over this rank's index vector ``idx``.
 
         ``log_fn(batch_idx, batch_len, loss)`` is called (in order) for every batch with
         ``batch_idx % log_interval == 0``; pass None to skip the per-chunk syncs entirely.
+        ``sync=False`` returns as soon as the epoch is enqueued (``train_seconds`` is then the enqueue
+        time): the caller overlaps host work - the next epoch's sampler order - with the GPU.
         """
         n = idx.numel()
         full, last = divmod(n, self.B)
@@ -213,7 +219,8 @@ class FusedTrainer:
                 loss = float(self.loss_log[full].item())
                 logged[full] = loss
                 log_fn(full, last, loss)
-        self.compute.synchronize()
+        if sync:
+            self.compute.synchronize()
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
 
     # ------------------------------------------------------------------ raw step stream (bench)
@@ -247,12 +254,13 @@ class FusedTrainer:
         """Return (sum of per-sample NLL, correct, N) over the whole test split."""
         if self.n_test == 0:
             return 0.0, 0, 0
-        if self.use_graphs:
+        # one batch = 3 launches: eager (a captured graph only pays when there are many batches)
+        if self.use_graphs and self.n_test > self.eval_batch:
             if self._eval_graph is None:
-                self._eval_graph = self.engine.capture_eval(self.n_test, self.TB)
+                self._eval_graph = self.engine.capture_eval(self.n_test, self.eval_batch)
             self.engine.replay(self._eval_graph)
         else:
-            self.engine.eval(self.n_test, self.TB)
+            self.engine.eval(self.n_test, self.eval_batch)
         self.compute.synchronize()
         loss_sum = float(self.test_loss_rows.double().sum().item())
         correct = int(self.test_correct.sum().item())

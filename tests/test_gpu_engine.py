@@ -79,3 +79,20 @@ def test_fused_fc_update_bitwise_equals_step_tail_update(cuda_device, graph_step
     lf, cf, _ = tf.evaluate()
     lu, cu, _ = tu.evaluate()
     assert lf == lu and cf == cu
+
+
+def test_whole_split_eval_bitwise_equals_test_batch_chunks(cuda_device):
+    """evaluate() runs the test split as one batch; per-row losses / hits must be bitwise the
+    chunked (--test-batch-size 1000) ones."""
+    _, ms, t = _trainer(cuda_device, graph_steps=4, n_train=2000, n_test=4000)
+    assert t.eval_batch == 4000
+    t.train_epoch(1, torch.randperm(2000, generator=torch.Generator().manual_seed(1)))
+    rows = []
+    for batch in (1000, 4000, 1000):
+        t.engine.eval(4000, batch)
+        torch.cuda.synchronize()
+        rows.append((t.test_loss_rows.clone(), t.test_correct.clone()))
+    for l_, c_ in rows[1:]:
+        assert torch.equal(l_, rows[0][0]) and torch.equal(c_, rows[0][1])
+    loss, correct, n = t.evaluate()
+    assert n == 4000 and correct == int(rows[0][1].sum())
