@@ -183,8 +183,14 @@ struct XgmiArgs {
   int world, rank;
   int64_t nvec;                      // bucket length in float4s
   uint64_t timeout_ticks;            // s_memrealtime ticks (100 MHz)
+  // optional fused Adadelta (conv bucket): with fuse_ada, phase 2 applies the update to every element
+  // it gathers (flat index ada_base + bucket index; grad = the reduced values), refreshes the conv2
+  // bf16 shadows and advances ada.state_inc->step - the bucket's separate update launch disappears
+  int fuse_ada;
+  int64_t ada_base;
+  AdadeltaArgs ada;
 };
-int xgmi_workgroups(int64_t nvec, int world);
+int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada);
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
 
 }  // namespace mnist

@@ -20,6 +20,7 @@
 // stores; flags are system-scope atomics carrying a per-WG call counter (monotonic, no reset, so
 // graph replays need no host work).  A wait that exceeds the timeout sets *err and returns; every
 // later call then returns at once and the host raises (XgmiComm::check).
+#include "../include/device_utils.h"
 #include "../include/kernels.h"
 
 namespace mnist {
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
   }
   if (!xgmi_stage(a, 1, b, e)) return;
   // ---- phase 2: every other rank's reduced shard -> my output (the same index set per WG)
-  {
+  if (!a.fuse_ada) {
     __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) src[p] = rsrc(a.out[p], p == r ? 0 : bytes);   // own shard: no-op load
@@ -127,20 +128,62 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
       for (int p = 0; p < W; ++p)
         if (p != r) st_sys(out, p * S4 + k, v[p]);
     }
+    return;
+  }
+  // fused Adadelta: the gathered sums (own shard re-read from the local output) are the gradients
+  if (b == 0 && tid == 0 && a.ada.state_inc) a.ada.state_inc->step += 1;   // end-of-step marker
+  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
+  __amdgpu_buffer_rsrc_t src[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) src[p] = rsrc(a.out[p], bytes);
+  for (int64_t k = (int64_t)b * 256 + tid; k < S4; k += step) {
+    f4 v[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) v[p] = ld_sys(src[p], p * S4 + k);
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const int64_t j = p * S4 + k;
+      if (j >= a.nvec) continue;
+      if (p != r) st_sys(out, j, v[p]);
+      const int64_t e = a.ada_base + 4 * j;
+      float4 pr = *reinterpret_cast<float4*>(a.ada.param + e);
+      float4 sq = *reinterpret_cast<float4*>(a.ada.square_avg + e);
+      float4 ac = *reinterpret_cast<float4*>(a.ada.acc_delta + e);
+      ad.step(pr.x, v[p].x, sq.x, ac.x);
+      ad.step(pr.y, v[p].y, sq.y, ac.y);
+      ad.step(pr.z, v[p].z, sq.z, ac.z);
+      ad.step(pr.w, v[p].w, sq.w, ac.w);
+      *reinterpret_cast<float4*>(a.ada.param + e) = pr;
+      *reinterpret_cast<float4*>(a.ada.square_avg + e) = sq;
+      *reinterpret_cast<float4*>(a.ada.acc_delta + e) = ac;
+      const float pv[4] = {pr.x, pr.y, pr.z, pr.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {             // conv2.weight -> w2f [64][9][32], w2d [9][32][64]
+        const int rel = (int)(e + q - OFF_CONV2_W);
+        if (rel < 0 || rel >= C2 * C1 * 9) continue;
+        const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
+        const uint16_t h = f2bf(pv[q]);
+        a.ada.w2f[(co * 9 + t) * C1 + ci] = h;
+        a.ada.w2d[(t * C1 + ci) * C2 + co] = h;
+      }
+    }
   }
 }
 
-int xgmi_workgroups(int64_t nvec, int world) {
+int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada) {
   const int64_t s4 = (nvec + world - 1) / world;
-  int64_t g = (s4 + 511) / 512;                      // >= 2 float4 per lane per phase-1 pass
+  // >= 2 float4 per lane per phase-1 pass; with the fused update (W elementwise Adadelta steps per
+  // index) spread wider so its dependent load -> update -> store chains run on more CUs
+  int64_t g = fuse_ada ? (s4 + 127) / 128 : (s4 + 511) / 512;
   if (g < 1) g = 1;
   if (g > XGMI_MAX_WG) g = XGMI_MAX_WG;
   return (int)g;
 }
 
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
-  const dim3 g(xgmi_workgroups(a.nvec, a.world)), blk(256);
+  const dim3 g(xgmi_workgroups(a.nvec, a.world, a.fuse_ada != 0)), blk(256);
   switch (a.world) {
+    case 1: hipLaunchKernelGGL(xgmi_allreduce_kernel<1>, g, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(xgmi_allreduce_kernel<2>, g, blk, 0, s, a); break;
     case 3: hipLaunchKernelGGL(xgmi_allreduce_kernel<3>, g, blk, 0, s, a); break;
     case 4: hipLaunchKernelGGL(xgmi_allreduce_kernel<4>, g, blk, 0, s, a); break;
@@ -148,7 +191,7 @@ void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
     case 6: hipLaunchKernelGGL(xgmi_allreduce_kernel<6>, g, blk, 0, s, a); break;
     case 7: hipLaunchKernelGGL(xgmi_allreduce_kernel<7>, g, blk, 0, s, a); break;
     case 8: hipLaunchKernelGGL(xgmi_allreduce_kernel<8>, g, blk, 0, s, a); break;
-    default: break;   // world 1: nothing to reduce (the host rejects > XGMI_MAX_RANKS)
+    default: break;   // the host rejects world sizes outside 1..XGMI_MAX_RANKS
   }
 }
 

@@ -176,9 +176,12 @@ void Engine::enqueue_step(int batch, bool last) {
     side_pending_ = true;
     launch_conv_dgrad(cb, B, compute_);
     launch_conv_grad_reduce(cb, B, compute_);
-    if (xgmi_) xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);
-    else comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
-    launch_adadelta(adc, ADA_CONV, compute_);
+    if (xgmi_) {   // conv bucket all-reduce with the conv Adadelta step fused into its gather phase
+      xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_, &adc);
+    } else {
+      comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+      launch_adadelta(adc, ADA_CONV, compute_);
+    }
     if (last) {                                              // chunk end: one real join edge
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));

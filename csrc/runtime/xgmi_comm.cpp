@@ -47,6 +47,12 @@ XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
   ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   set_timeout_seconds(60.0);
+  if (world == 1) {                       // nothing to map: the kernel runs against itself
+    peer_in_.assign(1, in_);
+    peer_out_.assign(1, out_);
+    peer_flags_.assign(1, flags_);
+    connected_ = true;
+  }
 }
 
 XgmiComm::~XgmiComm() {
@@ -113,17 +119,11 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
   connected_ = true;
 }
 
-void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream) {
+void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream, const AdadeltaArgs* ada) {
   if (channel < 0 || channel >= channels_) throw std::runtime_error("xgmi: bad channel");
   if (offset < 0 || count < 0 || offset + count > numel_ || (offset & 3) || (count & 3))
     throw std::runtime_error("xgmi: range must lie in the buffer, offset and count multiples of 4");
   if (count == 0) return;
-  if (world_ == 1) {
-    if (out_ != in_)
-      ok(hipMemcpyAsync(out_ + offset, in_ + offset, count * sizeof(float), hipMemcpyDeviceToDevice, stream),
-         "hipMemcpyAsync");
-    return;
-  }
   if (!connected_) throw std::runtime_error("xgmi: connect() first");
   XgmiArgs a;
   memset(&a, 0, sizeof(a));
@@ -138,6 +138,11 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
   a.rank = rank_;
   a.nvec = count / 4;
   a.timeout_ticks = timeout_ticks_;
+  if (ada) {
+    a.fuse_ada = 1;
+    a.ada_base = offset;
+    a.ada = *ada;
+  }
   launch_xgmi_allreduce(a, stream);
 }
 

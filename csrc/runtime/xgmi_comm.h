@@ -15,6 +15,8 @@
 #include <stdint.h>
 #include <vector>
 
+#include "../include/kernels.h"
+
 namespace mnist {
 
 class XgmiComm {
@@ -32,7 +34,10 @@ class XgmiComm {
 
   // out[offset, offset+count) = sum over ranks of in[offset, offset+count); offset and count in
   // floats, multiples of 4.  Graph-capturable (no host work beyond the launch).
-  void allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream);
+  // With `ada` (conv bucket of the engine): the kernel also applies the Adadelta step to the reduced
+  // elements (flat parameter index = offset + bucket index) - see XgmiArgs::fuse_ada.
+  void allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream,
+                 const AdadeltaArgs* ada = nullptr);
   // device error flag (a stage wait timed out on this rank); synchronous read
   int error() const;
   void set_timeout_seconds(double s);
