@@ -129,6 +129,7 @@ struct ConvBwdArgs {
   float grad_scale;
   int wgrad_groups;           // G
   const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
+  int* signal_ctr;            // optional: conv2_wgrad adds 1 at kernel start (schedule-3 hand-off)
 };
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad

@@ -322,6 +322,11 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
   const int mt0 = 2 * (wave & 1), ng = wave >> 1;
   const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
   const int G = gridDim.x, g = blockIdx.x;
+  // DDP schedule 3: announce "this step's fc gradients are final" to the comm stream.  fc_bwd, the
+  // previous kernel on this stream, has completed and released its writes, so one lane's add at
+  // kernel start is the signal - no separate signal launch on the critical path.
+  if (a.signal_ctr && g == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const int rows = H2 * B;
   const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
   const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;

@@ -166,8 +166,9 @@ void Engine::enqueue_step(int batch, bool last) {
   if (sched3) {
     // xGMI: the reduced gradients land in the communicator's output buffer, the update reads there
     if (xgmi_) ad.grad = adc.grad = xgmi_->out();
-    launch_stream_signal(sync_ + 0, compute_);               // fc grads of this step are final
-    launch_conv_wgrad(cb, B, compute_);
+    ConvBwdArgs cbs = cb;
+    cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
+    launch_conv_wgrad(cbs, B, compute_);
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
     if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
     else comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
