@@ -106,6 +106,20 @@ __device__ __forceinline__ float normalize_u8(uint8_t v) { return kNormLut.v[v];
 // add+sqrt, div_, mul_, mul_, addcmul_, add_), every operation individually rounded (FMA
 // contraction off), so the result is a pure function of the inputs - bitwise identical in every
 // kernel that applies it (the optimizer kernels and the fused fc-backward epilogue).
+// Spin (one lane) until *a >= target: relaxed agent-scope polls with s_sleep; after ~60 s sets *err
+// and gives up (a protocol bug must not hang the GPU).  Used by the schedule-3 stream hand-offs.
+__device__ __forceinline__ void spin_until_geq(const int* a, int target, int* err) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();               // 100 MHz
+  while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
 struct Ada {
   float rho, eps, wd, lr;
   __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {

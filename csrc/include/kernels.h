@@ -22,6 +22,9 @@ struct TrunkFwdArgs {
   uint8_t* pmask_out;         // u8   [B][9216]        (train only)
   const float* xin;           // optional fp32 [B][784] already-normalised input (module API);
                               // when set, data_u8/idx are ignored
+  const int* wait_a;          // optional (schedule 3): completion held until *wait_a >= *wait_b
+  const int* wait_b;
+  int* wait_err;
 };
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s);
 constexpr int TRUNK_IMG_MAX_B = 256;      // B <= this: one workgroup per image (every image has a CU)

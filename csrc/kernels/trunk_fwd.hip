@@ -294,6 +294,12 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
     dst[1] = s1;
   }
   PHASE_MARK(6);
+  // DDP schedule 3: the kernel completes only once the comm stream's fc update of the previous step
+  // is done (*wait_a >= *wait_b), so fc1_fwd - which reads the updated fc weights - can follow with
+  // no separate wait launch; one lane of the last workgroup spins while the others drain.
+  if (a.wait_a && blockIdx.x == gridDim.x - 1 && b == (int)gridDim.y - 1 && tid == 0)
+    spin_until_geq(a.wait_a, __hip_atomic_load(a.wait_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                   a.wait_err);
 }
 
 int trunk_strips_per_wg(int B) { return B <= TRUNK_IMG_MAX_B ? 3 : 1; }

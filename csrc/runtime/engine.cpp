@@ -128,10 +128,17 @@ void Engine::enqueue_step(int batch, bool last) {
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
     side_forked_ = true;
   }
+  // schedule 2/3: the previous step's fc all-reduce + fc update must be done before fc1_fwd; in
+  // schedule 3 trunk_fwd itself holds its completion for it (device counters, no extra launch)
+  const bool hold = side_pending_ && sched3;
+  if (hold) {
+    tf.wait_a = sync_ + 1;
+    tf.wait_b = sync_ + 0;
+    tf.wait_err = sync_ + 2;
+  }
   launch_trunk_fwd(tf, B, true, compute_);
-  if (side_pending_) {                 // schedule 2/3: previous step's fc all-reduce + fc update
-    if (sched3) launch_stream_wait(sync_ + 1, sync_ + 0, 0, sync_ + 2, compute_);
-    else HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+  if (side_pending_) {
+    if (!hold) HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
     side_pending_ = false;
   }
   launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
