@@ -187,11 +187,13 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &RcclComm::rank);
 
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
-      .def(py::init([](int world, int rank, int device, uintptr_t in, uintptr_t out, int64_t numel, int channels) {
-             return std::make_shared<XgmiComm>(world, rank, device, P<float>(in), P<float>(out), numel, channels);
+      .def(py::init([](int world, int rank, int device, uintptr_t in, uintptr_t out, int64_t numel, int channels,
+                       int64_t oneshot_max) {
+             return std::make_shared<XgmiComm>(world, rank, device, P<float>(in), P<float>(out), numel, channels,
+                                               oneshot_max);
            }),
            py::arg("world_size"), py::arg("rank"), py::arg("device"), py::arg("in_ptr"), py::arg("out_ptr"),
-           py::arg("numel"), py::arg("channels") = 2)
+           py::arg("numel"), py::arg("channels") = 2, py::arg("oneshot_max") = 32768)
       .def("record", [](const XgmiComm& c) {
         auto v = c.record();
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());

@@ -182,6 +182,8 @@ struct XgmiArgs {
   const float* in[XGMI_MAX_RANKS];   // every rank's input bucket (peer mappings; own = local)
   float* out[XGMI_MAX_RANKS];        // every rank's output bucket
   int* flags[XGMI_MAX_RANKS];        // every rank's flag block of this channel
+  float* stage[XGMI_MAX_RANKS];      // one-shot: every rank's staging block of this channel (2 slots)
+  int64_t slot_floats;               // one-shot: floats per staging slot
   int* ctr;                          // local per-WG call counters [XGMI_MAX_WG]
   int* err;                          // local error flag (timeout)
   int world, rank;
@@ -196,5 +198,8 @@ struct XgmiArgs {
 };
 int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada);
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
+// small buckets: one-shot variant - copy-in to a staging slot (alternating by call parity), ONE
+// stage hand-off, every rank sums all ranks' slots itself (same rank order -> same bits as above)
+void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s);
 
 }  // namespace mnist

@@ -66,6 +66,30 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e) {
 }
 }  // namespace
 
+// Fused Adadelta on one float4 of reduced gradients at flat parameter index e (+ conv2 bf16 shadows)
+__device__ __forceinline__ void ada_update4(const XgmiArgs& a, const Ada& ad, int64_t e, f4 g) {
+  float4 pr = *reinterpret_cast<float4*>(a.ada.param + e);
+  float4 sq = *reinterpret_cast<float4*>(a.ada.square_avg + e);
+  float4 ac = *reinterpret_cast<float4*>(a.ada.acc_delta + e);
+  ad.step(pr.x, g.x, sq.x, ac.x);
+  ad.step(pr.y, g.y, sq.y, ac.y);
+  ad.step(pr.z, g.z, sq.z, ac.z);
+  ad.step(pr.w, g.w, sq.w, ac.w);
+  *reinterpret_cast<float4*>(a.ada.param + e) = pr;
+  *reinterpret_cast<float4*>(a.ada.square_avg + e) = sq;
+  *reinterpret_cast<float4*>(a.ada.acc_delta + e) = ac;
+  const float pv[4] = {pr.x, pr.y, pr.z, pr.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {             // conv2.weight -> w2f [64][9][32], w2d [9][32][64]
+    const int rel = (int)(e + q - OFF_CONV2_W);
+    if (rel < 0 || rel >= C2 * C1 * 9) continue;
+    const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
+    const uint16_t h = f2bf(pv[q]);
+    a.ada.w2f[(co * 9 + t) * C1 + ci] = h;
+    a.ada.w2d[(t * C1 + ci) * C2 + co] = h;
+  }
+}
+
 // W is a template parameter so the per-peer loads unroll into one straight batch (a runtime
 // `p < world` guard makes hipcc wait vmcnt(0) after every load).  Buffer ops are bounds-checked by
 // the descriptor: loads past the bucket return 0 and stores past it are dropped, so the shard
@@ -145,28 +169,76 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
       const int64_t j = p * S4 + k;
       if (j >= a.nvec) continue;
       if (p != r) st_sys(out, j, v[p]);
-      const int64_t e = a.ada_base + 4 * j;
-      float4 pr = *reinterpret_cast<float4*>(a.ada.param + e);
-      float4 sq = *reinterpret_cast<float4*>(a.ada.square_avg + e);
-      float4 ac = *reinterpret_cast<float4*>(a.ada.acc_delta + e);
-      ad.step(pr.x, v[p].x, sq.x, ac.x);
-      ad.step(pr.y, v[p].y, sq.y, ac.y);
-      ad.step(pr.z, v[p].z, sq.z, ac.z);
-      ad.step(pr.w, v[p].w, sq.w, ac.w);
-      *reinterpret_cast<float4*>(a.ada.param + e) = pr;
-      *reinterpret_cast<float4*>(a.ada.square_avg + e) = sq;
-      *reinterpret_cast<float4*>(a.ada.acc_delta + e) = ac;
-      const float pv[4] = {pr.x, pr.y, pr.z, pr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {             // conv2.weight -> w2f [64][9][32], w2d [9][32][64]
-        const int rel = (int)(e + q - OFF_CONV2_W);
-        if (rel < 0 || rel >= C2 * C1 * 9) continue;
-        const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
-        const uint16_t h = f2bf(pv[q]);
-        a.ada.w2f[(co * 9 + t) * C1 + ci] = h;
-        a.ada.w2d[(t * C1 + ci) * C2 + co] = h;
-      }
+      ada_update4(a, ad, a.ada_base + 4 * j, v[p]);
     }
+  }
+}
+
+// One-shot: WG b owns the float4 index set {b*256 + tid + m*grid*256}.  It copies its part of this
+// rank's input into staging slot (call parity) with write-through stores, publishes stage 0, then
+// reads that part of every rank's slot and sums in rank order.  A slot is rewritten two calls later,
+// after stage 0 of the call in between, i.e. after every peer's WG b finished reading it - so one
+// hand-off per call suffices (the two-shot kernel needs two).
+template <int W>
+__global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
+  __shared__ int s_epoch, s_err;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    const int e = a.ctr[b] + 1;
+    a.ctr[b] = e;
+    s_epoch = e;
+    s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_err) return;
+  const int e = s_epoch, r = a.rank;
+  const int64_t step = (int64_t)gridDim.x * 256, bytes = a.nvec * 16;
+  const int64_t slot = (e & 1) * a.slot_floats;
+  const int64_t k0 = (int64_t)b * 256 + tid;
+  constexpr int KMAX = 4;                      // float4s per lane kept in registers (host-checked)
+  f4 mine[KMAX];
+#pragma unroll
+  for (int m = 0; m < KMAX; ++m) {
+    const int64_t k = k0 + m * step;
+    if (k < a.nvec) {
+      mine[m] = *reinterpret_cast<const f4*>(a.in[r] + 4 * k);
+      st_sys(rsrc(a.stage[r] + slot, bytes), k, mine[m]);
+    }
+  }
+  if (!xgmi_stage(a, 0, b, e)) return;
+  __amdgpu_buffer_rsrc_t src[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) src[p] = rsrc(a.stage[p] + slot, p == r ? 0 : bytes);   // own: registers
+  if (a.fuse_ada && b == 0 && tid == 0 && a.ada.state_inc) a.ada.state_inc->step += 1;
+  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, a.fuse_ada ? *a.ada.lr : 0.0f};
+  const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
+#pragma unroll
+  for (int m = 0; m < KMAX; ++m) {
+    const int64_t k = k0 + m * step;
+    if (k >= a.nvec) break;
+    f4 v[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) v[p] = ld_sys(src[p], k);
+    f4 s = (r == 0) ? mine[m] : v[0];
+#pragma unroll
+    for (int p = 1; p < W; ++p) s += (p == r) ? mine[m] : v[p];
+    if (a.fuse_ada) ada_update4(a, ad, a.ada_base + 4 * k, s);
+    else st_sys(out, k, s);
+  }
+}
+
+void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
+  const dim3 g((unsigned)((a.nvec + 255) / 256 < XGMI_MAX_WG ? (a.nvec + 255) / 256 : XGMI_MAX_WG)), blk(256);
+  switch (a.world) {
+    case 1: hipLaunchKernelGGL(xgmi_oneshot_kernel<1>, g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(xgmi_oneshot_kernel<2>, g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(xgmi_oneshot_kernel<3>, g, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL(xgmi_oneshot_kernel<4>, g, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(xgmi_oneshot_kernel<5>, g, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL(xgmi_oneshot_kernel<6>, g, blk, 0, s, a); break;
+    case 7: hipLaunchKernelGGL(xgmi_oneshot_kernel<7>, g, blk, 0, s, a); break;
+    case 8: hipLaunchKernelGGL(xgmi_oneshot_kernel<8>, g, blk, 0, s, a); break;
+    default: break;
   }
 }
 

@@ -17,9 +17,9 @@ void ok(hipError_t e, const char* what) {
 
 // export record of one rank: where its input / output buckets and flag blocks live
 struct Record {
-  hipIpcMemHandle_t in_h, out_h, flags_h;
+  hipIpcMemHandle_t in_h, out_h, flags_h, stage_h;
   int64_t in_off, out_off;
-  int64_t numel;
+  int64_t numel, oneshot_max;
   int32_t world, rank, channels, pid;
 };
 
@@ -32,8 +32,13 @@ void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
 }
 }  // namespace
 
-XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels)
-    : world_(world), rank_(rank), device_(device), channels_(channels), in_(in), out_(out), numel_(numel) {
+XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
+                   int64_t oneshot_max)
+    : world_(world), rank_(rank), device_(device), channels_(channels), in_(in), out_(out), numel_(numel),
+      oneshot_max_(oneshot_max) {
+  // the one-shot kernel keeps <= 4 float4 per lane of <= XGMI_MAX_WG workgroups
+  if (oneshot_max < 0 || oneshot_max > 4LL * 4 * 256 * XGMI_MAX_WG || (oneshot_max & 3))
+    throw std::runtime_error("xgmi: bad one-shot size");
   if (world < 1 || world > XGMI_MAX_RANKS) throw std::runtime_error("xgmi: world size must be 1..8");
   if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
   if (channels < 1) throw std::runtime_error("xgmi: need at least one channel");
@@ -45,12 +50,14 @@ XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64
   ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
   ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
+  ok(hipMalloc(&stage_, sizeof(float) * (2 * oneshot_max + 4) * channels), "hipMalloc(stage)");
   ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   set_timeout_seconds(60.0);
   if (world == 1) {                       // nothing to map: the kernel runs against itself
     peer_in_.assign(1, in_);
     peer_out_.assign(1, out_);
     peer_flags_.assign(1, flags_);
+    peer_stage_.assign(1, stage_);
     connected_ = true;
   }
 }
@@ -62,6 +69,7 @@ XgmiComm::~XgmiComm() {
   if (flags_) hipFree(flags_);
   if (ctr_) hipFree(ctr_);
   if (err_) hipFree(err_);
+  if (stage_) hipFree(stage_);
 }
 
 void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
@@ -74,7 +82,10 @@ std::vector<uint8_t> XgmiComm::record() const {
   int64_t foff = 0;
   export_ptr(flags_, &r.flags_h, &foff);
   if (foff != 0) throw std::runtime_error("xgmi: flag block is not an allocation base");
+  export_ptr(stage_, &r.stage_h, &foff);
+  if (foff != 0) throw std::runtime_error("xgmi: staging block is not an allocation base");
   r.numel = numel_;
+  r.oneshot_max = oneshot_max_;
   r.world = world_;
   r.rank = rank_;
   r.channels = channels_;
@@ -89,6 +100,7 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
   peer_in_.assign(world_, nullptr);
   peer_out_.assign(world_, nullptr);
   peer_flags_.assign(world_, nullptr);
+  peer_stage_.assign(world_, nullptr);
   // one mapping per distinct handle (the input and output buckets may share a caching-allocator segment)
   std::vector<std::pair<hipIpcMemHandle_t, void*>> maps;
   auto open = [&](const hipIpcMemHandle_t& h) -> char* {
@@ -104,17 +116,20 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
     if (records[q].size() != sizeof(Record)) throw std::runtime_error("xgmi: bad record size");
     Record r;
     memcpy(&r, records[q].data(), sizeof(r));
-    if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_)
+    if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_ ||
+        r.oneshot_max != oneshot_max_)
       throw std::runtime_error("xgmi: peer record does not match this communicator");
     if (q == rank_) {
       peer_in_[q] = in_;
       peer_out_[q] = out_;
       peer_flags_[q] = flags_;
+      peer_stage_[q] = stage_;
       continue;
     }
     peer_in_[q] = reinterpret_cast<const float*>(open(r.in_h) + r.in_off);
     peer_out_[q] = reinterpret_cast<float*>(open(r.out_h) + r.out_off);
     peer_flags_[q] = reinterpret_cast<int*>(open(r.flags_h));
+    peer_stage_[q] = reinterpret_cast<float*>(open(r.stage_h));
   }
   connected_ = true;
 }
@@ -131,7 +146,9 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
     a.in[q] = peer_in_[q] + offset;
     a.out[q] = peer_out_[q] + offset;
     a.flags[q] = peer_flags_[q] + (int64_t)channel * XGMI_FLAG_INTS;
+    a.stage[q] = peer_stage_[q] + (int64_t)channel * 2 * oneshot_max_;
   }
+  a.slot_floats = oneshot_max_;
   a.ctr = ctr_ + (int64_t)channel * XGMI_MAX_WG;
   a.err = err_;
   a.world = world_;
@@ -143,7 +160,8 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
     a.ada_base = offset;
     a.ada = *ada;
   }
-  launch_xgmi_allreduce(a, stream);
+  if (count <= oneshot_max_) launch_xgmi_allreduce_oneshot(a, stream);
+  else launch_xgmi_allreduce(a, stream);
 }
 
 int XgmiComm::error() const {

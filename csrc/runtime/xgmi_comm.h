@@ -23,7 +23,10 @@ class XgmiComm {
  public:
   // in / out: this rank's flat input and output buffers of `numel` floats (device allocations that
   // support IPC export: hipMalloc or blocks of torch's caching allocator)
-  XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels);
+  // Buckets of at most `oneshot_max` floats use the one-shot kernel (one hand-off per call; staging
+  // slots allocated here, 2 per channel); larger ones the two-shot reduce-scatter + all-gather.
+  XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
+           int64_t oneshot_max = 32768);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -50,6 +53,8 @@ class XgmiComm {
   float *in_, *out_;
   int64_t numel_;
   int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
+  float* stage_ = nullptr;   // [channels][2][oneshot_max_], IPC exported
+  int64_t oneshot_max_;
   int* ctr_ = nullptr;       // [channels][XGMI_MAX_WG], local
   int* err_ = nullptr;
   uint64_t timeout_ticks_;
@@ -57,6 +62,7 @@ class XgmiComm {
   std::vector<const float*> peer_in_;
   std::vector<float*> peer_out_;
   std::vector<int*> peer_flags_;
+  std::vector<float*> peer_stage_;
   std::vector<void*> opened_;   // IPC mappings to close
 };
 

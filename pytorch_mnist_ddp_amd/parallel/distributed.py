@@ -110,7 +110,7 @@ def _all_ok(flag: bool, device) -> bool:
 
 
 def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, grad_out: torch.Tensor,
-                     tag: str | None = None, channels: int = 2, verify: bool = True):
+                     tag: str | None = None, channels: int = 2, verify: bool = True, oneshot_max: int = 32768):
     """Direct xGMI all-reduce communicator over ``grad_in`` -> ``grad_out`` (csrc/runtime/xgmi_comm.h).
 
     Every rank exports IPC handles of its two buffers and its flag blocks through the c10d store and
@@ -128,7 +128,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
     numel = grad_in.numel()
     x = None
     try:
-        x = C.XgmiComm(world_size, rank, dev.index or 0, native.ptr(grad_in), native.ptr(grad_out), numel, channels)
+        x = C.XgmiComm(world_size, rank, dev.index or 0, native.ptr(grad_in), native.ptr(grad_out), numel, channels,
+                       oneshot_max)
         if world_size > 1:
             store = dist.distributed_c10d._get_default_store()
             store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
@@ -152,7 +153,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
 
 def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torch.Tensor, channels: int) -> bool:
     n = grad_in.numel()
-    cut = (n // 2) & ~3                                  # channel c covers its own quarter-aligned range
+    # channel 0: a small range (one-shot kernel), channel 1: the rest (two-shot when large)
+    cut = min((n // 2) & ~3, 16384)
     ranges = [(0, cut), (cut, n - cut)] if channels >= 2 else [(0, n)]
     i = torch.arange(n, device=grad_in.device, dtype=torch.float32)
     base = torch.remainder(i, 97.0) * 0.25 - 3.0         # multiples of 1/4 in [-3, 21]: sums are exact
