@@ -20,7 +20,8 @@ struct Record {
   hipIpcMemHandle_t in_h, out_h, flags_h, stage_h;
   int64_t in_off, out_off;
   int64_t numel, oneshot_max;
-  int32_t world, rank, channels, pid;
+  int32_t world, rank, channels, pid, device;
+  char host[64];                 // IPC mappings only exist between the GPUs of one node
 };
 
 void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
@@ -90,6 +91,8 @@ std::vector<uint8_t> XgmiComm::record() const {
   r.rank = rank_;
   r.channels = channels_;
   r.pid = (int32_t)getpid();
+  r.device = device_;
+  gethostname(r.host, sizeof(r.host) - 1);
   const uint8_t* b = reinterpret_cast<const uint8_t*>(&r);
   return std::vector<uint8_t>(b, b + sizeof(r));
 }
@@ -119,6 +122,15 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
     if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_ ||
         r.oneshot_max != oneshot_max_)
       throw std::runtime_error("xgmi: peer record does not match this communicator");
+    char host[64] = {0};
+    gethostname(host, sizeof(host) - 1);
+    if (strncmp(host, r.host, sizeof(host)) != 0)
+      throw std::runtime_error("xgmi: ranks span more than one node (peer on " + std::string(r.host) + ")");
+    if (q != rank_ && r.device != device_) {
+      int can = 0;
+      ok(hipDeviceCanAccessPeer(&can, device_, r.device), "hipDeviceCanAccessPeer");
+      if (!can) throw std::runtime_error("xgmi: no peer access to device " + std::to_string(r.device));
+    }
     if (q == rank_) {
       peer_in_[q] = in_;
       peer_out_[q] = out_;
