@@ -24,8 +24,16 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
   constexpr int KS = KC / 32;              // 9
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int m = lane & 15, kg = lane >> 4;
-  const int chunk = blockIdx.y;
-  const int row = blockIdx.x * 16 + m;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (linear id mod 8), so
+  // give every XCD 4 whole K-chunks (all row tiles of each): a chunk's 74 KB w1 slice is then
+  // fetched into ONE XCD's L2 instead of all eight (grid = R x 32, R*32 divisible by 8)
+  static_assert(FC1_KSPLIT == 32, "4 K-chunks per XCD");
+  const int R = gridDim.x;
+  const int lin = blockIdx.x + R * blockIdx.y;
+  const int xcd = lin & 7, j = lin >> 3;
+  const int chunk = 4 * xcd + j / R;
+  const int tile = j - (j / R) * R;
+  const int row = tile * 16 + m;
   const bool valid = row < B;
   const uint16_t* pa = p + (int64_t)(valid ? row : 0) * NFLAT + chunk * KC + 8 * kg;
   const uint16_t* pb = w1 + (int64_t)(32 * wave + m) * NFLAT + chunk * KC + 8 * kg;
@@ -45,7 +53,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int b = blockIdx.x * 16 + 4 * kg + r;
+    const int b = tile * 16 + 4 * kg + r;
     if (b < B) {
       float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
       dst[0] = acc0[r];
