@@ -11,10 +11,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,engine_steps", [(2, 30), (4, 0)])
-def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps):
+@pytest.mark.parametrize("world,engine_steps,fault", [(2, 30, False), (4, 0, True)])
+def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps, fault):
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "xgmi_check.py"), "--world", str(world),
            "--same-device", "--iters", "20", "--engine-steps", str(engine_steps), "--timeout", "100"]
+    if fault:
+        cmd.append("--fault-test")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=dict(os.environ, PYTHONPATH=ROOT))
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])

@@ -9,7 +9,9 @@ not xGMI).  Checks, on every rank:
   1. the startup self-test of ``create_xgmi_comm`` passes;
   2. random fp32 buckets: every rank's output equals the rank-ordered fp32 sum, bitwise;
   3. the same through a captured hipGraph replayed with fresh inputs;
-  4. (``--engine-steps``) the fused trainer with the xGMI all-reduce at this world size, dropout
+  4. (``--fault-test``) a rank that never arrives is detected by the others' stage timeouts
+     (error flag set, no hang);
+  5. (``--engine-steps``) the fused trainer with the xGMI all-reduce at this world size, dropout
      off: parameters stay bitwise identical across ranks and the loss decreases;
 then prints per-call latency for the model's two bucket sizes.  Exit code 0 = all ranks passed.
 """
@@ -100,6 +102,8 @@ def worker(rank: int, world: int, port: int, args, q) -> None:
             us = (time.perf_counter() - t0) / args.iters * 1e6
             msgs.append(f"{name}: {us:.1f} us/call")
         assert x.error() == 0
+        if args.fault_test:
+            msgs.append(_fault_check(torch, dist, world, rank, dev, x, s))
         if args.engine_steps:
             msgs.append(_engine_check(torch, dist, world, rank, dev, args.engine_steps))
         q.put((rank, True, "; ".join(msgs)))
@@ -107,6 +111,28 @@ def worker(rank: int, world: int, port: int, args, q) -> None:
         q.put((rank, False, "; ".join(msgs + [f"{type(e).__name__}: {e}"])))
     finally:
         dist.destroy_process_group()
+
+
+def _fault_check(torch, dist, world, rank, dev, x, s) -> str:
+    """A peer that never arrives (rank world-1 skips one call): the others' stage waits must time
+    out, set the error flag and return - no hang - and the flag must stay set (later calls return
+    at once), which Engine::synchronize turns into an exception."""
+    x.set_timeout_seconds(0.5)
+    dist.barrier()
+    t0 = time.perf_counter()
+    if rank != world - 1:
+        x.allreduce(0, FC_N, CONV_N, s.cuda_stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert x.error() == 1, "missing peer was not detected"
+        assert dt < 10.0, f"timeout took {dt:.1f} s"
+        x.allreduce(0, FC_N, CONV_N, s.cuda_stream)      # poisoned: returns immediately
+        torch.cuda.synchronize()
+        res = f"fault detected in {dt:.2f} s"
+    else:
+        res = "skipped the call (the missing peer)"
+    dist.barrier()
+    return res
 
 
 def _engine_check(torch, dist, world, rank, dev, steps) -> str:
@@ -147,6 +173,8 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--engine-steps", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--fault-test", action="store_true",
+                    help="last rank skips one call: the others must time out cleanly (run last; poisons the comm)")
     args = ap.parse_args()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import torch.multiprocessing as mp
