@@ -170,3 +170,27 @@ def test_mnist_ddp_slurm_rank_discovery_gloo(tmp_path):
     assert "| distributed init (rank 0): env://, local rank:0, world size:2" in outs[0]
     assert "| distributed init (rank 1): env://, local rank:0, world size:2" in outs[1]
     assert outs[0].count("Test set: Average loss:") == 1 and "Test set" not in outs[1]
+
+
+def _agree_worker(rank, world, port, q):
+    from pytorch_mnist_ddp_amd.parallel.distributed import _all_ok, _max_over_ranks
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", world_size=world, rank=rank)
+    try:
+        # the all-reduce choice and its fallback are collective decisions: one failing rank makes
+        # every rank fall back, and probe timings are maxima over ranks
+        q.put((rank, _all_ok(True, "cpu"), _all_ok(rank != 1, "cpu"), _max_over_ranks(1.5 * (rank + 1), "cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_choice_is_collective_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert [r[1:] for r in res] == [(True, False, 3.0), (True, False, 3.0)]
