@@ -96,3 +96,17 @@ def test_whole_split_eval_bitwise_equals_test_batch_chunks(cuda_device):
         assert torch.equal(l_, rows[0][0]) and torch.equal(c_, rows[0][1])
     loss, correct, n = t.evaluate()
     assert n == 4000 and correct == int(rows[0][1].sum())
+
+
+def test_torch_profiler_sees_native_kernels(cuda_device):
+    """the hand-written kernels launched by the C++ engine on torch streams show up
+    in torch.profiler (kineto/roctracer) traces by name."""
+    from torch.profiler import ProfilerActivity, profile
+    _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=400, n_test=100)
+    t.train_epoch(1, torch.randperm(400, generator=torch.Generator().manual_seed(2)))   # warm
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        t.train_epoch(2, torch.randperm(400, generator=torch.Generator().manual_seed(3)))
+        torch.cuda.synchronize()
+    names = " ".join({e.name for e in prof.events()})
+    for k in ("trunk_fwd", "fc1_fwd", "head_train", "fc_bwd", "conv2_wgrad", "conv2_dgrad", "adadelta"):
+        assert k in names, k
