@@ -66,11 +66,11 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e) {
 }
 }  // namespace
 
-// Fused Adadelta on one float4 of reduced gradients at flat parameter index e (+ conv2 bf16 shadows)
-__device__ __forceinline__ void ada_update4(const XgmiArgs& a, const Ada& ad, int64_t e, f4 g) {
-  float4 pr = *reinterpret_cast<float4*>(a.ada.param + e);
-  float4 sq = *reinterpret_cast<float4*>(a.ada.square_avg + e);
-  float4 ac = *reinterpret_cast<float4*>(a.ada.acc_delta + e);
+// Fused Adadelta on one float4 of reduced gradients at flat parameter index e (+ conv2 bf16 shadows);
+// pr / sq / ac are the element's current param / square_avg / acc_delta (loaded by the caller, so the
+// one-shot kernel can issue those local loads before it waits for its peers)
+__device__ __forceinline__ void ada_update4(const XgmiArgs& a, const Ada& ad, int64_t e, f4 g, float4 pr,
+                                            float4 sq, float4 ac) {
   ad.step(pr.x, g.x, sq.x, ac.x);
   ad.step(pr.y, g.y, sq.y, ac.y);
   ad.step(pr.z, g.z, sq.z, ac.z);
@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
       const int64_t j = p * S4 + k;
       if (j >= a.nvec) continue;
       if (p != r) st_sys(out, j, v[p]);
-      ada_update4(a, ad, a.ada_base + 4 * j, v[p]);
+      const int64_t e = a.ada_base + 4 * j;
+      ada_update4(a, ad, e, v[p], *reinterpret_cast<float4*>(a.ada.param + e),
+                  *reinterpret_cast<float4*>(a.ada.square_avg + e), *reinterpret_cast<float4*>(a.ada.acc_delta + e));
     }
   }
 }
@@ -197,12 +199,19 @@ __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
   const int64_t k0 = (int64_t)b * 256 + tid;
   constexpr int KMAX = 4;                      // float4s per lane kept in registers (host-checked)
   f4 mine[KMAX];
+  float4 pr[KMAX], sq[KMAX], ac[KMAX];           // fused update: local state loaded before the wait
 #pragma unroll
   for (int m = 0; m < KMAX; ++m) {
     const int64_t k = k0 + m * step;
     if (k < a.nvec) {
       mine[m] = *reinterpret_cast<const f4*>(a.in[r] + 4 * k);
       st_sys(rsrc(a.stage[r] + slot, bytes), k, mine[m]);
+      if (a.fuse_ada) {
+        const int64_t el = a.ada_base + 4 * k;
+        pr[m] = *reinterpret_cast<const float4*>(a.ada.param + el);
+        sq[m] = *reinterpret_cast<const float4*>(a.ada.square_avg + el);
+        ac[m] = *reinterpret_cast<const float4*>(a.ada.acc_delta + el);
+      }
     }
   }
   if (!xgmi_stage(a, 0, b, e)) return;
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
     f4 s = (r == 0) ? mine[m] : v[0];
 #pragma unroll
     for (int p = 1; p < W; ++p) s += (p == r) ? mine[m] : v[p];
-    if (a.fuse_ada) ada_update4(a, ad, a.ada_base + 4 * k, s);
+    if (a.fuse_ada) ada_update4(a, ad, a.ada_base + 4 * k, s, pr[m], sq[m], ac[m]);
     else st_sys(out, k, s);
   }
 }
