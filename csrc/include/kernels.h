@@ -201,5 +201,9 @@ void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
 // small buckets: one-shot variant - copy-in to a staging slot (alternating by call parity), ONE
 // stage hand-off, every rank sums all ranks' slots itself (same rank order -> same bits as above)
 void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s);
+// the engine's fc bucket [0, OFF_CONV1_W) with the fc Adadelta step + w1/w1t shadows fused (two-shot,
+// 64x32 fc1.weight tiles as the unit of work; needs a.ada and a.nvec == OFF_CONV1_W / 4)
+int xgmi_fc_fused_workgroups(int world);
+void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s);
 
 }  // namespace mnist

@@ -251,6 +251,173 @@ void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fc bucket with the fc Adadelta step fused (two-shot).  The unit of work is a 64(o) x 32(i) tile
+// of fc1.weight (576 tiles) plus one pseudo-tile for the tail (fc1.b, fc2.w, fc2.b; 368 float4):
+// shard p = units [p*577/W, (p+1)*577/W).  Phase 1: WG b reduces units b, b+G, .. of shard r (rank
+// order) into its output bucket; stage 1; phase 2: WG b gathers units b, b+G, .. of EVERY shard
+// (all loads in flight at once), applies Ada::step with the gathered sums as gradients and writes
+// param / square_avg / acc_delta plus the bf16 shadows w1 [128][9216] and w1t [9216][128] (tile
+// transposed through LDS) - exactly the adadelta kernel's fc1 tile math, so bitwise equal to the
+// all-reduce + separate update it replaces.  The fc branch of the DDP step loses a launch and a
+// 4.7 MB gradient re-read.
+namespace {
+constexpr int FCU_TILES = 2 * (NFLAT / 32);                      // 576
+constexpr int FCU_UNITS = FCU_TILES + 1;                         // + tail
+constexpr int FCU_TAIL_F4 = (int)((OFF_CONV1_W - OFF_FC1_B) / 4);  // 368
+constexpr int FCU_TS = 72;                                       // padded LDS row (bf16) of a tile
+
+__device__ __forceinline__ int fcu_lo(int p, int W) { return p * FCU_UNITS / W; }
+// float4 index (in the bucket) of this thread's h-th float4 of unit u (h = 0, 1)
+__device__ __forceinline__ int fcu_f4(int u, int h, int tid) {
+  if (u < FCU_TILES) {
+    const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+    const int o = 64 * ot + (tid >> 2), i = 32 * it + (tid & 3) * 8;
+    return (o * NFLAT + i) / 4 + h;
+  }
+  const int q = tid + 256 * h;                                   // tail: 368 float4
+  return q < FCU_TAIL_F4 ? (int)(OFF_FC1_B / 4) + q : -1;
+}
+}  // namespace
+
+template <int W>
+__global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
+  constexpr int UMAX = W == 1 ? 3 : W == 2 ? 2 : 1;              // units per shard per WG (host grid)
+  __shared__ int s_epoch, s_err;
+  __shared__ __attribute__((aligned(16))) uint16_t ts[W * UMAX][32 * FCU_TS];
+  const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
+  if (tid == 0) {
+    const int e = a.ctr[b] + 1;
+    a.ctr[b] = e;
+    s_epoch = e;
+    s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_err) return;
+  const int e = s_epoch, r = a.rank;
+  const int64_t bytes = a.nvec * 16;
+  const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
+  if (!xgmi_stage(a, 0, b, e)) return;
+  // ---- phase 1: my shard's units, rank-order sums -> my output
+  {
+    __amdgpu_buffer_rsrc_t in[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) in[p] = rsrc(a.in[p], bytes);
+    const int lo = fcu_lo(r, W), hi = fcu_lo(r + 1, W);
+#pragma unroll
+    for (int m = 0; m < UMAX; ++m) {
+      const int u = lo + b + m * G;
+      if (u >= hi) break;
+      f4 v[2][W];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+#pragma unroll
+        for (int p = 0; p < W; ++p) v[h][p] = ld_sys(in[p], q < 0 ? a.nvec : q);   // q < 0: past the end -> 0
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+        f4 t = v[h][0];
+#pragma unroll
+        for (int p = 1; p < W; ++p) t += v[h][p];
+        if (q >= 0) st_sys(out, q, t);
+      }
+    }
+  }
+  if (!xgmi_stage(a, 1, b, e)) return;
+  // ---- phase 2: every shard's units of this WG: gathered sums + local optimizer state, all in flight
+  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
+  f4 g[W][UMAX][2];
+  float4 pr[W][UMAX][2], sq[W][UMAX][2], ac[W][UMAX][2];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
+#pragma unroll
+    for (int m = 0; m < UMAX; ++m) {
+      const int u = fcu_lo(p, W) + b + m * G;
+      if (u >= fcu_lo(p + 1, W)) continue;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+        if (q < 0) continue;
+        g[p][m][h] = ld_sys(src, q);
+        pr[p][m][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
+        sq[p][m][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
+        ac[p][m][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+#pragma unroll
+    for (int m = 0; m < UMAX; ++m) {
+      const int u = fcu_lo(p, W) + b + m * G;
+      if (u >= fcu_lo(p + 1, W)) continue;
+      float v8[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+        if (q < 0) continue;
+        float4 P = pr[p][m][h], S = sq[p][m][h], A = ac[p][m][h];
+        const f4 G4 = g[p][m][h];
+        ad.step(P.x, G4.x, S.x, A.x);
+        ad.step(P.y, G4.y, S.y, A.y);
+        ad.step(P.z, G4.z, S.z, A.z);
+        ad.step(P.w, G4.w, S.w, A.w);
+        reinterpret_cast<float4*>(a.ada.param)[q] = P;
+        reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
+        reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
+        v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
+      }
+      if (u < FCU_TILES) {                                          // bf16 shadows of the fc1 tile
+        const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+        const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
+        uint4 lo4;
+        lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
+        lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
+        *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
+        uint16_t* t = ts[p * UMAX + m];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[(ic + j) * FCU_TS + ol] = f2bf(v8[j]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+#pragma unroll
+    for (int m = 0; m < UMAX; ++m) {
+      const int u = fcu_lo(p, W) + b + m * G;
+      if (u >= fcu_lo(p + 1, W) || u >= FCU_TILES) continue;
+      const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+      const int il = tid >> 3, oc = (tid & 7) * 8;
+      *reinterpret_cast<uint4*>(a.ada.w1t + (int64_t)(32 * it + il) * NH + 64 * ot + oc) =
+          *reinterpret_cast<const uint4*>(ts[p * UMAX + m] + il * FCU_TS + oc);
+    }
+  }
+}
+
+int xgmi_fc_fused_workgroups(int world) {
+  const int per = (FCU_UNITS + world - 1) / world;
+  return per < XGMI_MAX_WG ? per : XGMI_MAX_WG;
+}
+
+void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s) {
+  const dim3 g(xgmi_fc_fused_workgroups(a.world)), blk(256);
+  switch (a.world) {
+    case 1: hipLaunchKernelGGL(xgmi_fc_fused_kernel<1>, g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(xgmi_fc_fused_kernel<2>, g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(xgmi_fc_fused_kernel<3>, g, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL(xgmi_fc_fused_kernel<4>, g, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(xgmi_fc_fused_kernel<5>, g, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL(xgmi_fc_fused_kernel<6>, g, blk, 0, s, a); break;
+    case 7: hipLaunchKernelGGL(xgmi_fc_fused_kernel<7>, g, blk, 0, s, a); break;
+    case 8: hipLaunchKernelGGL(xgmi_fc_fused_kernel<8>, g, blk, 0, s, a); break;
+    default: break;
+  }
+}
+
 int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada) {
   const int64_t s4 = (nvec + world - 1) / world;
   // >= 2 float4 per lane per phase-1 pass; with the fused update (W elementwise Adadelta steps per

@@ -177,9 +177,13 @@ void Engine::enqueue_step(int batch, bool last) {
     cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
     launch_conv_wgrad(cbs, B, compute_);
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
-    else comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
+    if (xgmi_ && xgmi_fuse_fc_) {   // fc bucket all-reduce with the fc Adadelta step fused
+      xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
+    } else {
+      if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
+      else comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+      launch_adadelta(ad, ADA_FC, comm_stream_);
+    }
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
     side_pending_ = true;
     launch_conv_dgrad(cb, B, compute_);

@@ -146,11 +146,10 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
   connected_ = true;
 }
 
-void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream, const AdadeltaArgs* ada) {
+XgmiArgs XgmiComm::args(int channel, int64_t offset, int64_t count) const {
   if (channel < 0 || channel >= channels_) throw std::runtime_error("xgmi: bad channel");
   if (offset < 0 || count < 0 || offset + count > numel_ || (offset & 3) || (count & 3))
     throw std::runtime_error("xgmi: range must lie in the buffer, offset and count multiples of 4");
-  if (count == 0) return;
   if (!connected_) throw std::runtime_error("xgmi: connect() first");
   XgmiArgs a;
   memset(&a, 0, sizeof(a));
@@ -167,6 +166,20 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
   a.rank = rank_;
   a.nvec = count / 4;
   a.timeout_ticks = timeout_ticks_;
+  return a;
+}
+
+void XgmiComm::allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada) {
+  XgmiArgs a = args(channel, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W);
+  a.fuse_ada = 1;
+  a.ada_base = OFF_FC1_W;
+  a.ada = ada;
+  launch_xgmi_fc_fused(a, stream);
+}
+
+void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream, const AdadeltaArgs* ada) {
+  XgmiArgs a = args(channel, offset, count);
+  if (count == 0) return;
   if (ada) {
     a.fuse_ada = 1;
     a.ada_base = offset;

@@ -41,6 +41,9 @@ class XgmiComm {
   // elements (flat parameter index = offset + bucket index) - see XgmiArgs::fuse_ada.
   void allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream,
                  const AdadeltaArgs* ada = nullptr);
+  // The engine's fc bucket (flat [0, OFF_CONV1_W)) with the fc Adadelta step and the w1 / w1t bf16
+  // shadow refresh fused into the gather phase (launch_xgmi_fc_fused).
+  void allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada);
   // device error flag (a stage wait timed out on this rank); synchronous read
   int error() const;
   void set_timeout_seconds(double s);
@@ -64,6 +67,7 @@ class XgmiComm {
   std::vector<int*> peer_flags_;
   std::vector<float*> peer_stage_;
   std::vector<void*> opened_;   // IPC mappings to close
+  XgmiArgs args(int channel, int64_t offset, int64_t count) const;
 };
 
 }  // namespace mnist

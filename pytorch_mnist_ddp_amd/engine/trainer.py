@@ -136,6 +136,8 @@ class FusedTrainer:
             if self.xgmi is not None:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
+                # fc Adadelta fused into the fc bucket's gather phase (MNIST_AMD_XGMI_FUSE_FC=0: separate)
+                self.engine.set_xgmi_fuse_fc(os.environ.get("MNIST_AMD_XGMI_FUSE_FC", "1") == "1")
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None

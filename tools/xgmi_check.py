@@ -136,6 +136,17 @@ def _fault_check(torch, dist, world, rank, dev, x, s) -> str:
 
 
 def _engine_check(torch, dist, world, rank, dev, steps) -> str:
+    """Fused-fc-update and separate-update xGMI schedules must give the same bits."""
+    res = []
+    for fuse in ("1", "0"):
+        os.environ["MNIST_AMD_XGMI_FUSE_FC"] = fuse
+        res.append(_engine_run(torch, dist, world, rank, dev, steps))
+    os.environ.pop("MNIST_AMD_XGMI_FUSE_FC")
+    assert torch.equal(res[0][0], res[1][0]), "fused fc update differs from the separate update"
+    return res[0][1] + ", fused == separate fc update"
+
+
+def _engine_run(torch, dist, world, rank, dev, steps):
     from pytorch_mnist_ddp_amd.data.datasets import load_mnist
     from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream
     from pytorch_mnist_ddp_amd.engine.state import ModelState
@@ -163,7 +174,7 @@ def _engine_check(torch, dist, world, rank, dev, steps) -> str:
     assert torch.isfinite(losses).all(), "non-finite loss"
     first, last = float(losses[:5].mean()), float(losses[-5:].mean())
     assert last < first, f"loss did not decrease ({first:.4f} -> {last:.4f})"
-    return f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical)"
+    return p, f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical)"
 
 
 def main() -> int:
