@@ -171,8 +171,11 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                                       bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
         model_for_save = ddp
         comm, comm2 = create_rccl_comms(world, rank, gpu)
-    optimizer = Adadelta(model.parameters(), lr=args.lr, model_state=ms)
-    scheduler = StepLR(optimizer, step_size=1, gamma=args.gamma)
+    # The optimizer here is the engine's fused Adadelta kernel (state in `ms`); StepLR(step_size=1)
+    # (reference mnist_ddp.py:178, :189) reduces to lr <- lr * gamma after every epoch, computed in
+    # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
+    # (No torch.optim object: constructing one imports torch._dynamo, ~1.6 s inside the timed run.)
+    lr = float(args.lr)
     graph_steps = args.log_interval if args.graph_steps is None else args.graph_steps
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
@@ -189,7 +192,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             train_stream.set_epoch(epoch)
         consume_loader_base_seed()          # iter(train_loader)
         idx = train_stream.epoch_indices()
-        trainer.set_lr(optimizer.param_groups[0]["lr"])
+        trainer.set_lr(lr)
 
         def log_fn(batch_idx, blen, loss, epoch=epoch):
             _check_finite(loss, epoch, batch_idx)
@@ -214,11 +217,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             trainer.synchronize()
             assert_params_in_sync([ms.param])
         _json_log(args.json_log, rec)
-        for p in optimizer.param_groups[0]["params"]:      # keep torch-format optimizer bookkeeping
-            st_ = optimizer.state[p]
-            if "step" in st_:
-                st_["step"] += st.steps
-        scheduler.step()
+        lr = lr * args.gamma                                   # scheduler.step()
     trainer.synchronize()
     _save(args, model_for_save, distributed, rank, ddp_script)
 
