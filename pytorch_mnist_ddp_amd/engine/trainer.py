@@ -195,6 +195,25 @@ class FusedTrainer:
         self.rng_base += 2 * steps
         t0 = time.perf_counter()
         logged = {}
+        # Logged losses are read one chunk late: the chunk after a logged step is enqueued before the
+        # host waits for that step (an event, not the whole stream), so the GPU never idles while the
+        # host reads the loss and prints.  Lines come out in the same order with the same values.
+        pending = []
+
+        def flush_one():
+            ev, b_idx, blen = pending.pop(0)
+            ev.synchronize()
+            loss = float(self.loss_log[b_idx].item())
+            logged[b_idx] = loss
+            log_fn(b_idx, blen, loss)
+
+        def note(b_idx, blen):
+            ev = torch.cuda.Event()
+            ev.record(self.compute)
+            while pending:
+                flush_one()
+            pending.append((ev, b_idx, blen))
+
         # chunk boundaries: when logging, end a chunk right after every logged step
         chunk = self.graph_steps if self.graph_steps > 0 else max(1, log_interval)
         done = 0
@@ -210,17 +229,13 @@ class FusedTrainer:
             self._run(n_here, self.B)
             done += n_here
             if log_fn is not None and (done - 1) % log_interval == 0:
-                self.compute.synchronize()
-                loss = float(self.loss_log[done - 1].item())
-                logged[done - 1] = loss
-                log_fn(done - 1, self.B, loss)
+                note(done - 1, self.B)
         if last:
             self._run(1, last)
             if log_fn is not None and full % log_interval == 0:
-                self.compute.synchronize()
-                loss = float(self.loss_log[full].item())
-                logged[full] = loss
-                log_fn(full, last, loss)
+                note(full, last)
+        while pending:
+            flush_one()
         if sync:
             self.compute.synchronize()
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
