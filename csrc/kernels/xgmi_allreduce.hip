@@ -326,60 +326,71 @@ __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
     }
   }
   if (!xgmi_stage(a, 1, b, e)) return;
-  // ---- phase 2: every shard's units of this WG: gathered sums + local optimizer state, all in flight
+  // ---- phase 2: every shard's units of this WG, PG shards at a time: gathered sums + local
+  // optimizer state all in flight per group.  PG bounds the registers (~100 VGPRs) so this kernel,
+  // which runs on the comm stream beside the conv backward, co-resides with wgrad / dgrad
+  // workgroups instead of taking whole CUs from them.
   const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
-  f4 g[W][UMAX][2];
-  float4 pr[W][UMAX][2], sq[W][UMAX][2], ac[W][UMAX][2];
+  constexpr int PG = W < 2 ? W : 2;
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
-    const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
+  for (int p0 = 0; p0 < W; p0 += PG) {
+    f4 g[PG][UMAX][2];
+    float4 pr[PG][UMAX][2], sq[PG][UMAX][2], ac[PG][UMAX][2];
 #pragma unroll
-    for (int m = 0; m < UMAX; ++m) {
-      const int u = fcu_lo(p, W) + b + m * G;
-      if (u >= fcu_lo(p + 1, W)) continue;
+    for (int pp = 0; pp < PG; ++pp) {
+      const int p = p0 + pp;
+      if (p >= W) break;
+      const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
-        if (q < 0) continue;
-        g[p][m][h] = ld_sys(src, q);
-        pr[p][m][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
-        sq[p][m][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
-        ac[p][m][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
+      for (int m = 0; m < UMAX; ++m) {
+        const int u = fcu_lo(p, W) + b + m * G;
+        if (u >= fcu_lo(p + 1, W)) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int q = fcu_f4(u, h, tid);
+          if (q < 0) continue;
+          g[pp][m][h] = ld_sys(src, q);
+          pr[pp][m][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
+          sq[pp][m][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
+          ac[pp][m][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
+        }
       }
     }
-  }
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
+    for (int pp = 0; pp < PG; ++pp) {
+      const int p = p0 + pp;
+      if (p >= W) break;
 #pragma unroll
-    for (int m = 0; m < UMAX; ++m) {
-      const int u = fcu_lo(p, W) + b + m * G;
-      if (u >= fcu_lo(p + 1, W)) continue;
-      float v8[8];
+      for (int m = 0; m < UMAX; ++m) {
+        const int u = fcu_lo(p, W) + b + m * G;
+        if (u >= fcu_lo(p + 1, W)) continue;
+        float v8[8];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
-        if (q < 0) continue;
-        float4 P = pr[p][m][h], S = sq[p][m][h], A = ac[p][m][h];
-        const f4 G4 = g[p][m][h];
-        ad.step(P.x, G4.x, S.x, A.x);
-        ad.step(P.y, G4.y, S.y, A.y);
-        ad.step(P.z, G4.z, S.z, A.z);
-        ad.step(P.w, G4.w, S.w, A.w);
-        reinterpret_cast<float4*>(a.ada.param)[q] = P;
-        reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
-        reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
-        v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
-      }
-      if (u < FCU_TILES) {                                          // bf16 shadows of the fc1 tile
-        const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
-        const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
-        uint4 lo4;
-        lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
-        lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
-        *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
-        uint16_t* t = ts[p * UMAX + m];
+        for (int h = 0; h < 2; ++h) {
+          const int q = fcu_f4(u, h, tid);
+          if (q < 0) continue;
+          float4 P = pr[pp][m][h], S = sq[pp][m][h], A = ac[pp][m][h];
+          const f4 G4 = g[pp][m][h];
+          ad.step(P.x, G4.x, S.x, A.x);
+          ad.step(P.y, G4.y, S.y, A.y);
+          ad.step(P.z, G4.z, S.z, A.z);
+          ad.step(P.w, G4.w, S.w, A.w);
+          reinterpret_cast<float4*>(a.ada.param)[q] = P;
+          reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
+          reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
+          v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
+        }
+        if (u < FCU_TILES) {                                        // bf16 shadows of the fc1 tile
+          const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+          const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
+          uint4 lo4;
+          lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
+          lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
+          *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
+          uint16_t* t = ts[p * UMAX + m];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[(ic + j) * FCU_TS + ol] = f2bf(v8[j]);
+          for (int j = 0; j < 8; ++j) t[(ic + j) * FCU_TS + ol] = f2bf(v8[j]);
+        }
       }
     }
   }
