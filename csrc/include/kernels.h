@@ -170,7 +170,7 @@ void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const 
                         int64_t n, uint8_t* dst_u8, int32_t* dst_labels, hipStream_t s);
 // device-counter stream hand-offs (engine DDP schedule 3)
 void launch_stream_signal(int* ctr, hipStream_t s);
-void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s);
+void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s, double timeout_s = 60.0);
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 

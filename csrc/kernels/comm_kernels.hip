@@ -46,14 +46,14 @@ __global__ void stream_signal_kernel(int* ctr) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* err) {
+__global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* err, uint64_t timeout_ticks) {
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();               // 100 MHz
   while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(2);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {      // ~60 s
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -64,8 +64,8 @@ __global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* e
 void launch_stream_signal(int* ctr, hipStream_t s) {
   hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
 }
-void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s) {
-  hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(64), 0, s, a, b, delta, err);
+void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s, double timeout_s) {
+  hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(64), 0, s, a, b, delta, err, (uint64_t)(timeout_s * 1e8));
 }
 
 }  // namespace mnist

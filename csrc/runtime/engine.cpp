@@ -377,6 +377,21 @@ void Engine::broadcast_params(int root) {
   refresh_shadows();
 }
 
+bool Engine::probe_stream_handoff(double timeout_s) {
+  // scratch counters sync_[8..11]: [8] a, [9] b, [10] zero, [11] error
+  HIP_OK(hipMemsetAsync(sync_ + 8, 0, 4 * sizeof(int), compute_));
+  HIP_OK(hipStreamSynchronize(compute_));
+  launch_stream_wait(sync_ + 8, sync_ + 10, 1, sync_ + 11, compute_, timeout_s);   // compute waits ...
+  launch_stream_signal(sync_ + 8, comm_stream_);                                     // ... for comm
+  launch_stream_wait(sync_ + 9, sync_ + 10, 1, sync_ + 11, comm_stream_, timeout_s); // comm waits ...
+  launch_stream_signal(sync_ + 9, compute_);                                          // ... for compute
+  HIP_OK(hipStreamSynchronize(compute_));
+  HIP_OK(hipStreamSynchronize(comm_stream_));
+  int err = 0;
+  HIP_OK(hipMemcpy(&err, sync_ + 11, sizeof(int), hipMemcpyDeviceToHost));
+  return err == 0;
+}
+
 void Engine::synchronize() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));

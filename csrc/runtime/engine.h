@@ -80,6 +80,11 @@ class Engine {
   //   kernels) instead of captured cross-queue edges; only each chunk's first fork and last join
   //   are graph edges
   void set_dist_schedule(int s) { dist_sched_ = s; }
+  // Schedule 3 spins on one stream until the other signals; that is only deadlock-free when the
+  // compute and comm streams sit on different hardware queues (HIP shares queues beyond
+  // GPU_MAX_HW_QUEUES).  Each stream waits (spin kernel, `timeout_s`) for a signal enqueued on the
+  // other afterwards; true if both hand-offs completed.  Eager, no graph; call before training.
+  bool probe_stream_handoff(double timeout_s);
   // single GPU: fold the fc Adadelta step into fc_bwd (FcUpdate; bitwise equal either way, off by
   // default: measured 87.2 vs 85.9 us/step at B = 200)
   void set_fuse_fc_update(bool on) { fuse_fc_update_ = on; }

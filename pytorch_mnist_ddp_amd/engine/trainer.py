@@ -138,6 +138,25 @@ class FusedTrainer:
                 self.engine.attach_xgmi(self.xgmi)
                 # fc Adadelta fused into the fc bucket's gather phase (MNIST_AMD_XGMI_FUSE_FC=0: separate)
                 self.engine.set_xgmi_fuse_fc(os.environ.get("MNIST_AMD_XGMI_FUSE_FC", "1") == "1")
+        # schedule 3 spins on one stream for the other: make sure they sit on different hardware
+        # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
+        uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)
+        if uses_sched3:
+            ok = bool(self.engine.probe_stream_handoff(2.0))
+            if world_size > 1:
+                from ..parallel.distributed import _all_ok
+                ok = _all_ok(ok, dev)
+            if not ok and comm is None:
+                raise RuntimeError("DDP schedule 3 unusable (compute/comm streams share a hardware queue) "
+                                   "and no RCCL communicator to fall back to")
+            if not ok:
+                if rank == 0:
+                    print("[engine] compute/comm streams share a hardware queue: DDP schedule 3 disabled",
+                          flush=True)
+                self.engine.set_dist_schedule(2 if comm2 is not None else 1)
+                if self.xgmi is not None:
+                    self.engine.attach_xgmi(None)
+                    self.xgmi = None
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None

@@ -110,3 +110,11 @@ def test_torch_profiler_sees_native_kernels(cuda_device):
     names = " ".join({e.name for e in prof.events()})
     for k in ("trunk_fwd", "fc1_fwd", "head_train", "fc_bwd", "conv2_wgrad", "conv2_dgrad", "adadelta"):
         assert k in names, k
+
+
+def test_stream_handoff_probe(cuda_device):
+    """The schedule-3 precondition check: compute and comm streams progress independently (each
+    waits on a device counter the other signals afterwards) and the probe is repeatable."""
+    _, ms, t = _trainer(cuda_device, graph_steps=0)
+    assert t.engine.probe_stream_handoff(2.0)
+    assert t.engine.probe_stream_handoff(2.0)
