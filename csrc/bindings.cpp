@@ -243,7 +243,7 @@ PYBIND11_MODULE(_C, m) {
       .def("attach_comm", &Engine::attach_comm)
       .def("attach_comm2", &Engine::attach_comm2)
       .def("attach_xgmi", &Engine::attach_xgmi)
-      .def("set_xgmi_fuse_fc", &Engine::set_xgmi_fuse_fc)
+      .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_concurrent", &Engine::set_concurrent)
       .def("set_dist_schedule", &Engine::set_dist_schedule)

@@ -176,7 +176,7 @@ void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStre
 
 // direct xGMI all-reduce (reduce-scatter + all-gather over IPC-mapped peer buckets; xgmi_allreduce.hip)
 constexpr int XGMI_MAX_RANKS = 8;          // one node
-constexpr int XGMI_MAX_WG = 256;           // flag slots per (stage, rank)
+constexpr int XGMI_MAX_WG = 512;           // flag slots per (stage, rank)
 constexpr int XGMI_FLAG_INTS = 2 * XGMI_MAX_RANKS * XGMI_MAX_WG;   // [stage][src rank][wg]
 struct XgmiArgs {
   const float* in[XGMI_MAX_RANKS];   // every rank's input bucket (peer mappings; own = local)
@@ -205,5 +205,9 @@ void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s);
 // 64x32 fc1.weight tiles as the unit of work; needs a.ada and a.nvec == OFF_CONV1_W / 4)
 int xgmi_fc_fused_workgroups(int world);
 void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s);
+// the engine's conv bucket [OFF_CONV1_W, PARAM_TOTAL): conv gradient slab reduce (conv_grad_reduce's
+// partition and order) + one-shot all-reduce through the staging slots + Adadelta + conv2 shadows,
+// one launch (needs a.ada; a.nvec == (PARAM_TOTAL - OFF_CONV1_W) / 4; c.grad is not written)
+void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 
 }  // namespace mnist

@@ -22,6 +22,7 @@
 // later call then returns at once and the host raises (XgmiComm::check).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "conv_grad_reduce.h"
 
 namespace mnist {
 
@@ -425,6 +426,113 @@ void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s) {
     case 6: hipLaunchKernelGGL(xgmi_fc_fused_kernel<6>, g, blk, 0, s, a); break;
     case 7: hipLaunchKernelGGL(xgmi_fc_fused_kernel<7>, g, blk, 0, s, a); break;
     case 8: hipLaunchKernelGGL(xgmi_fc_fused_kernel<8>, g, blk, 0, s, a); break;
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv bucket, fully fused: WG b runs conv_grad_reduce's WG b (same slab partition and summation
+// order -> the same bits), keeps its <= 4 finished gradients per lane in registers, publishes them
+// into this rank's staging slot (call parity; 4-byte write-through stores at their bucket index),
+// hands off once (stage 0: WG b of every rank is done with the same indices), then sums every
+// rank's values at those indices in rank order and applies Ada::step + the conv2 bf16 shadows.
+// Replaces conv_grad_reduce + the one-shot all-reduce: one launch less on the DDP critical path.
+namespace {
+__device__ __forceinline__ void st_sys1(__amdgpu_buffer_rsrc_t r, int64_t i, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)(i * 4), 0, SYS);
+}
+__device__ __forceinline__ float ld_sys1(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4), 0, SYS));
+}
+}  // namespace
+
+template <int W>
+__global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a, ConvBwdArgs c, int B) {
+  __shared__ float4 red[256];
+  __shared__ int s_epoch, s_err;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    const int e = a.ctr[b] + 1;
+    a.ctr[b] = e;
+    s_epoch = e;
+    s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // (s_err is read after the reduce's barriers; a poisoned communicator skips the exchange)
+  float vals[4];
+  int64_t idx[4];
+  int nv = 0;
+  reduce_conv_grads(c, B, b, red, [&](int64_t el, float v) {
+    vals[nv] = v;
+    idx[nv] = el - a.ada_base;
+    ++nv;
+  });
+  __syncthreads();
+  if (s_err) return;
+  const int e = s_epoch, r = a.rank;
+  const int64_t slot = (e & 1) * a.slot_floats;
+  const int64_t bytes = a.nvec * 16;
+  {
+    const __amdgpu_buffer_rsrc_t mine = rsrc(a.stage[r] + slot, bytes);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nv) st_sys1(mine, idx[k], vals[k]);
+  }
+  // the update's local state, loaded before the hand-off wait
+  float pr[4], sq[4], ac[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < nv) {
+      const int64_t el = a.ada_base + idx[k];
+      pr[k] = a.ada.param[el];
+      sq[k] = a.ada.square_avg[el];
+      ac[k] = a.ada.acc_delta[el];
+    }
+  if (!xgmi_stage(a, 0, b, e)) return;
+  if (b == 0 && tid == 0 && a.ada.state_inc) a.ada.state_inc->step += 1;   // end-of-step marker
+  if (nv == 0) return;
+  __amdgpu_buffer_rsrc_t src[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) src[p] = rsrc(a.stage[p] + slot, p == r ? 0 : bytes);   // own: registers
+  float v[4][W];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int p = 0; p < W; ++p) v[k][p] = ld_sys1(src[p], k < nv ? idx[k] : 0);
+  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= nv) break;
+    float g = (r == 0) ? vals[k] : v[k][0];
+#pragma unroll
+    for (int p = 1; p < W; ++p) g += (p == r) ? vals[k] : v[k][p];
+    const int64_t el = a.ada_base + idx[k];
+    float P = pr[k], S = sq[k], A = ac[k];
+    ad.step(P, g, S, A);
+    a.ada.param[el] = P;
+    a.ada.square_avg[el] = S;
+    a.ada.acc_delta[el] = A;
+    const int rel = (int)(el - OFF_CONV2_W);
+    if (rel >= 0 && rel < C2 * C1 * 9) {
+      const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
+      const uint16_t h = f2bf(P);
+      a.ada.w2f[(co * 9 + t) * C1 + ci] = h;
+      a.ada.w2d[(t * C1 + ci) * C2 + co] = h;
+    }
+  }
+}
+
+void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
+  static_assert(RED_WGS <= XGMI_MAX_WG, "one flag slot per reduce workgroup");
+  const dim3 g(RED_WGS), blk(256);
+  switch (a.world) {
+    case 1: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<1>, g, blk, 0, s, a, c, B); break;
+    case 2: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<2>, g, blk, 0, s, a, c, B); break;
+    case 3: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<3>, g, blk, 0, s, a, c, B); break;
+    case 4: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<4>, g, blk, 0, s, a, c, B); break;
+    case 5: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<5>, g, blk, 0, s, a, c, B); break;
+    case 6: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<6>, g, blk, 0, s, a, c, B); break;
+    case 7: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<7>, g, blk, 0, s, a, c, B); break;
+    case 8: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<8>, g, blk, 0, s, a, c, B); break;
     default: break;
   }
 }

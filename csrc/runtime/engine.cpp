@@ -177,7 +177,7 @@ void Engine::enqueue_step(int batch, bool last) {
     cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
     launch_conv_wgrad(cbs, B, compute_);
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    if (xgmi_ && xgmi_fuse_fc_) {   // fc bucket all-reduce with the fc Adadelta step fused
+    if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
       if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
@@ -187,10 +187,14 @@ void Engine::enqueue_step(int batch, bool last) {
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
     side_pending_ = true;
     launch_conv_dgrad(cb, B, compute_);
-    launch_conv_grad_reduce(cb, B, compute_);
-    if (xgmi_) {   // conv bucket all-reduce with the conv Adadelta step fused into its gather phase
-      xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_, &adc);
+    if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
+      xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc);
+    } else if (xgmi_) {              // separate launches (reference for the fused kernels' bits)
+      launch_conv_grad_reduce(cb, B, compute_);
+      xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);
+      launch_adadelta(adc, ADA_CONV, compute_);
     } else {
+      launch_conv_grad_reduce(cb, B, compute_);
       comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
       launch_adadelta(adc, ADA_CONV, compute_);
     }

@@ -68,8 +68,9 @@ class Engine {
   // of the RCCL all-reduces of schedule 3; RCCL stays attached for the parameter broadcast
   void attach_xgmi(std::shared_ptr<XgmiComm> x);
   static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1;
-  // xGMI: fold the fc Adadelta step into the fc bucket's gather phase (default on)
-  void set_xgmi_fuse_fc(bool on) { xgmi_fuse_fc_ = on; }
+  // xGMI: fold the Adadelta steps into the all-reduce kernels (fc: gather phase; conv: slab reduce
+  // + one-shot + update in one launch).  Off = separate reduce / all-reduce / update launches.
+  void set_xgmi_fuse_update(bool on) { xgmi_fuse_update_ = on; }
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
   void set_concurrent(bool on) { concurrent_ = on; }
   // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
@@ -126,7 +127,7 @@ class Engine {
   int dist_sched_ = 1;
   std::shared_ptr<RcclComm> comm_, comm2_;
   std::shared_ptr<XgmiComm> xgmi_;
-  bool xgmi_fuse_fc_ = true;
+  bool xgmi_fuse_update_ = true;
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error

@@ -44,6 +44,9 @@ class XgmiComm {
   // The engine's fc bucket (flat [0, OFF_CONV1_W)) with the fc Adadelta step and the w1 / w1t bf16
   // shadow refresh fused into the gather phase (launch_xgmi_fc_fused).
   void allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada);
+  // The engine's conv bucket straight from the conv gradient slabs: slab reduce + one-shot
+  // all-reduce + Adadelta + conv2 shadows in one launch (launch_xgmi_conv_reduce_fused).
+  void conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hipStream_t stream, const AdadeltaArgs& ada);
   // device error flag (a stage wait timed out on this rank); synchronous read
   int error() const;
   void set_timeout_seconds(double s);

@@ -136,8 +136,8 @@ class FusedTrainer:
             if self.xgmi is not None:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
-                # fc Adadelta fused into the fc bucket's gather phase (MNIST_AMD_XGMI_FUSE_FC=0: separate)
-                self.engine.set_xgmi_fuse_fc(os.environ.get("MNIST_AMD_XGMI_FUSE_FC", "1") == "1")
+                # Adadelta fused into the all-reduce kernels (MNIST_AMD_XGMI_FUSE=0: separate launches)
+                self.engine.set_xgmi_fuse_update(os.environ.get("MNIST_AMD_XGMI_FUSE", "1") == "1")
         # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)

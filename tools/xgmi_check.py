@@ -136,14 +136,14 @@ def _fault_check(torch, dist, world, rank, dev, x, s) -> str:
 
 
 def _engine_check(torch, dist, world, rank, dev, steps) -> str:
-    """Fused-fc-update and separate-update xGMI schedules must give the same bits."""
+    """Fused (all-reduce + update kernels) and separate-launch xGMI schedules must give the same bits."""
     res = []
     for fuse in ("1", "0"):
-        os.environ["MNIST_AMD_XGMI_FUSE_FC"] = fuse
+        os.environ["MNIST_AMD_XGMI_FUSE"] = fuse
         res.append(_engine_run(torch, dist, world, rank, dev, steps))
-    os.environ.pop("MNIST_AMD_XGMI_FUSE_FC")
-    assert torch.equal(res[0][0], res[1][0]), "fused fc update differs from the separate update"
-    return res[0][1] + ", fused == separate fc update"
+    os.environ.pop("MNIST_AMD_XGMI_FUSE")
+    assert torch.equal(res[0][0], res[1][0]), "fused updates differ from the separate launches"
+    return res[0][1] + ", fused == separate launches"
 
 
 def _engine_run(torch, dist, world, rank, dev, steps):
