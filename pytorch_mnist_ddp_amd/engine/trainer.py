@@ -120,17 +120,28 @@ class FusedTrainer:
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
         self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
         want = allreduce == "xgmi" and (comm is not None or world_size > 1)
-        want = want or (allreduce == "auto" and comm is not None and world_size > 1)
+        probe_always = os.environ.get("MNIST_AMD_PROBE_ALWAYS", "0") == "1"   # tests: probe at world 1
+        want = want or (allreduce == "auto" and comm is not None and (world_size > 1 or probe_always))
         if want:
             from ..parallel.distributed import choose_allreduce, create_xgmi_comm
             self.grad_out = torch.zeros_like(mstate.grad)
             self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad, self.grad_out)
             if self.xgmi is not None and allreduce == "auto":
                 split = mstate.bucket_split
+                # the RCCL schedule's separate conv update (fused away on the xGMI side) is timed on
+                # a scratch copy of the optimizer state, so the probe leaves the model untouched
+                scratch = {k: getattr(mstate, k).clone() for k in ("param", "square_avg", "acc_delta", "w2f", "w2d")}
+                p_ = native.ptr
+                upd = [lambda: C.adadelta(p_(scratch["param"]), p_(mstate.grad), p_(scratch["square_avg"]),
+                                          p_(scratch["acc_delta"]), p_(mstate.lr), mstate.rho, mstate.eps,
+                                          mstate.weight_decay, p_(scratch["w2f"]), p_(scratch["w2d"]),
+                                          p_(mstate.w1), p_(mstate.w1t), 0, 2, True,
+                                          int(torch.cuda.current_stream(dev).cuda_stream))]
                 with torch.cuda.stream(self.compute):
                     pick, self.allreduce_timings = choose_allreduce(
                         comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad, self.grad_out,
-                        (0, split), (split, mstate.grad.numel() - split), dev)
+                        (0, split), (split, mstate.grad.numel() - split), dev, rccl_extra=upd)
+                del scratch
                 if pick != "xgmi":
                     self.xgmi = None
             if self.xgmi is not None:

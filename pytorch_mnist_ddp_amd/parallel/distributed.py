@@ -218,17 +218,20 @@ def time_bucket_allreduce(calls, device, iters: int = 20, warmup: int = 3) -> fl
 
 
 def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad_in: torch.Tensor, grad_out: torch.Tensor,
-                     fc_range: tuple[int, int], conv_range: tuple[int, int], device) -> tuple[str, dict]:
+                     fc_range: tuple[int, int], conv_range: tuple[int, int], device,
+                     rccl_extra=None) -> tuple[str, dict]:
     """Measure one step's two bucket all-reduces with RCCL and with the direct xGMI kernel on this
     node and return the faster (``"rccl"`` / ``"xgmi"``) plus the timings - the same decision on
-    every rank (timings are maxima over ranks).  Buffers are zeroed afterwards."""
+    every rank (timings are maxima over ranks).  ``rccl_extra`` (zero-argument launchers) is work
+    only the RCCL schedule has on its critical path - the separate conv-bucket update that the xGMI
+    kernels fuse - and is timed into the RCCL side.  Buffers are zeroed afterwards."""
     from ..ops import native
     s = torch.cuda.current_stream(device).cuda_stream
     gp = native.ptr(grad_in)
     with torch.no_grad():
         grad_in.zero_()
     rc = [lambda: rccl_fc.allreduce_sum(gp + 4 * fc_range[0], fc_range[1], 0, s),
-          lambda: rccl_conv.allreduce_sum(gp + 4 * conv_range[0], conv_range[1], 0, s)]
+          lambda: rccl_conv.allreduce_sum(gp + 4 * conv_range[0], conv_range[1], 0, s)] + list(rccl_extra or [])
     xc = [lambda: xgmi.allreduce(1, fc_range[0], fc_range[1], s),
           lambda: xgmi.allreduce(0, conv_range[0], conv_range[1], s)]
     t_r = time_bucket_allreduce(rc, device)

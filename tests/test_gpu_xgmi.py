@@ -48,3 +48,20 @@ def test_allreduce_auto_choice_plumbing_world1(cuda_device):
         assert int(gin.abs().sum().item()) == 0 and int(gout.abs().sum().item()) == 0
     finally:
         dist.destroy_process_group()
+
+
+def test_trainer_auto_probe_path_world1(tmp_path):
+    """The trainer's --allreduce auto path (probe of both implementations on scratch optimizer
+    state, forced at world 1) runs and leaves training bit-identical to a plain RCCL run."""
+    outs = {}
+    for name, env in (("auto", {"MNIST_AMD_PROBE_ALWAYS": "1"}), ("rccl", {"MNIST_AMD_ALLREDUCE": "rccl"})):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr",
+               "127.0.0.1", "--master-port", str(29600 + len(outs)), os.path.join(ROOT, "bench.py"),
+               "--force-comm", "--no-full-run", "--steps", "40", "--warmup", "10"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
+                           env=dict(os.environ, PYTHONPATH=ROOT, **env))
+        assert r.returncode == 0, r.stderr[-3000:]
+        import json
+        outs[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert outs["auto"]["config"]["allreduce_probe_us"]["rccl_us"] > 0
+    assert outs["auto"]["last_train_loss"] == outs["rccl"]["last_train_loss"]
