@@ -145,10 +145,16 @@ class FusedTrainer:
                 if pick != "xgmi":
                     self.xgmi = None
             if self.xgmi is not None:
+                from ..parallel.distributed import ranks_share_a_device
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
-                # Adadelta fused into the all-reduce kernels (MNIST_AMD_XGMI_FUSE=0: separate launches)
-                self.engine.set_xgmi_fuse_update(os.environ.get("MNIST_AMD_XGMI_FUSE", "1") == "1")
+                # Adadelta fused into the all-reduce kernels (MNIST_AMD_XGMI_FUSE=0: separate launches;
+                # default off when ranks share a GPU, where the fused grids cannot all be resident)
+                fuse_env = os.environ.get("MNIST_AMD_XGMI_FUSE")
+                fuse = fuse_env == "1" if fuse_env is not None else not ranks_share_a_device(dev)
+                if fuse_env is None and not fuse and rank == 0:
+                    print("[xgmi] ranks share a GPU: Adadelta update runs as separate launches", flush=True)
+                self.engine.set_xgmi_fuse_update(fuse)
         # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)

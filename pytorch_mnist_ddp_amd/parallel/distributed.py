@@ -109,6 +109,20 @@ def _all_ok(flag: bool, device) -> bool:
     return bool(t.item())
 
 
+def ranks_share_a_device(device) -> bool:
+    """True when two ranks of the default process group drive the same physical GPU (the one-GPU
+    multi-process rehearsal).  The fused xGMI kernels wait per workgroup on their peers, so every
+    rank's grid must be resident at once: 4 ranks x 512 workgroups of the 106-VGPR fused fc kernel
+    exceed one GPU's 1024 slots (docs/DEBUGGING.md); with one GPU per rank they always fit."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return False
+    p = torch.cuda.get_device_properties(torch.device(device))
+    ident = "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
+    ids = [None] * dist.get_world_size()
+    dist.all_gather_object(ids, ident)
+    return len(set(ids)) < len(ids)
+
+
 def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, grad_out: torch.Tensor,
                      tag: str | None = None, channels: int = 2, verify: bool = True, oneshot_max: int = 32768):
     """Direct xGMI all-reduce communicator over ``grad_in`` -> ``grad_out`` (csrc/runtime/xgmi_comm.h).

@@ -194,3 +194,37 @@ def test_allreduce_choice_is_collective_gloo():
     for p in procs:
         p.join(60)
     assert [r[1:] for r in res] == [(True, False, 3.0), (True, False, 3.0)]
+
+
+class _FakeProps:
+    def __init__(self, uuid):
+        self.uuid, self.pci_domain_id, self.pci_bus_id, self.pci_device_id = uuid, 0, 0, 0
+
+
+def _share_worker(rank, world, port, q):
+    from pytorch_mnist_ddp_amd.parallel import distributed as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", world_size=world, rank=rank)
+    try:
+        # device identity is faked (no GPU here): distinct GPUs per rank, then all ranks on one GPU
+        torch.cuda.get_device_properties = lambda d: _FakeProps(f"gpu{rank}")
+        distinct = D.ranks_share_a_device("cpu")
+        torch.cuda.get_device_properties = lambda d: _FakeProps("gpu0")
+        shared = D.ranks_share_a_device("cpu")
+        q.put((rank, distinct, shared))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ranks_share_a_device_detection_gloo():
+    """The fused xGMI schedule is turned off by default only when ranks share a GPU
+    (engine/trainer.py, docs/DEBUGGING.md): the detection must agree on every rank."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_share_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert [r[1:] for r in res] == [(False, True)] * world

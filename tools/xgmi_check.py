@@ -139,13 +139,16 @@ def _engine_check(torch, dist, world, rank, dev, steps) -> str:
     """Fused (all-reduce + update kernels) and separate-launch xGMI schedules must give the same bits."""
     res = []
     modes = os.environ.get("XGMI_CHECK_FUSE_MODES", "1,0").split(",")
-    for fuse in modes:
-        os.environ["MNIST_AMD_XGMI_FUSE"] = fuse
+    for fuse in modes:                   # "1" / "0" pin the schedule; "auto" = the trainer's default
+        if fuse == "auto":
+            os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
+        else:
+            os.environ["MNIST_AMD_XGMI_FUSE"] = fuse
         try:
             res.append(_engine_run(torch, dist, world, rank, dev, steps))
         except Exception as e:
             raise RuntimeError(f"engine run with MNIST_AMD_XGMI_FUSE={fuse}: {e}") from e
-    os.environ.pop("MNIST_AMD_XGMI_FUSE")
+    os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
     if len(res) == 1:
         return res[0][1] + f", fuse={modes[0]} only"
     assert torch.equal(res[0][0], res[1][0]), "fused updates differ from the separate launches"
@@ -194,6 +197,9 @@ def main() -> int:
                     help="last rank skips one call: the others must time out cleanly (run last; poisons the comm)")
     args = ap.parse_args()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.same_device and args.world > 2:
+        # the fused grids of > 2 ranks cannot all be resident on one GPU (docs/DEBUGGING.md)
+        os.environ.setdefault("XGMI_CHECK_FUSE_MODES", "auto")
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
