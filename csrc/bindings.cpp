@@ -188,12 +188,22 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
       .def(py::init([](int world, int rank, int device, uintptr_t in, uintptr_t out, int64_t numel, int channels,
-                       int64_t oneshot_max) {
+                       int64_t oneshot_max, int co_ranks, double budget) {
              return std::make_shared<XgmiComm>(world, rank, device, P<float>(in), P<float>(out), numel, channels,
-                                               oneshot_max);
+                                               oneshot_max, co_ranks, budget);
            }),
            py::arg("world_size"), py::arg("rank"), py::arg("device"), py::arg("in_ptr"), py::arg("out_ptr"),
-           py::arg("numel"), py::arg("channels") = 2, py::arg("oneshot_max") = 32768)
+           py::arg("numel"), py::arg("channels") = 2, py::arg("oneshot_max") = 32768, py::arg("co_ranks") = 1,
+           py::arg("budget") = 0.5)
+      .def_property_readonly("grids", [](const XgmiComm& c) {
+        const XgmiGrids& g = c.grids();
+        py::dict d;
+        d["fc_fused"] = g.fc_fused; d["conv_fused"] = g.conv_fused; d["twoshot"] = g.twoshot; d["oneshot"] = g.oneshot;
+        d["cap_fc_fused"] = g.cap_fc_fused; d["cap_conv_fused"] = g.cap_conv_fused;
+        d["cap_twoshot"] = g.cap_twoshot; d["cap_oneshot"] = g.cap_oneshot;
+        d["load_fused"] = g.load_fused; d["load_separate"] = g.load_separate;
+        return d;
+      })
       .def("record", [](const XgmiComm& c) {
         auto v = c.record();
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
@@ -260,6 +270,9 @@ PYBIND11_MODULE(_C, m) {
       .def("refresh_shadows", &Engine::refresh_shadows)
       .def("broadcast_params", &Engine::broadcast_params)
       .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("errors", &Engine::errors)
+      .def("check_errors", &Engine::check_errors)
+      .def_static("describe_xgmi_error", &Engine::describe_xgmi_error)
       .def_property_readonly("workspace_bytes", &Engine::workspace_bytes);
 
   m.def("roctx_push", [](const std::string& s) { roctx_push(s.c_str()); });

@@ -195,7 +195,24 @@ struct XgmiArgs {
   int fuse_ada;
   int64_t ada_base;
   AdadeltaArgs ada;
+  int max_wg;                        // residency cap on the launch grid (XgmiGrids; every rank the same)
 };
+// Every xGMI kernel's workgroup b spins until workgroup b of every peer arrives, so the workgroups
+// that can be spinning at the same moment - on one GPU: the fc-bucket kernel on the comm stream and
+// the conv-bucket kernel on the compute stream, times the ranks that share the GPU - must all be
+// resident at once.  The kernels loop over their index sets (any grid >= a small minimum works) and
+// the grids are sized from the occupancy API: co_ranks * sum(grid_k / (occupancy_k * CUs)) <= budget
+// for each pair that runs concurrently.  Kernel ids in the error code (XgmiComm::error):
+enum XgmiKernelId { XGMI_K_TWOSHOT = 1, XGMI_K_ONESHOT = 2, XGMI_K_FC_FUSED = 3, XGMI_K_CONV_FUSED = 4 };
+struct XgmiGrids {
+  int fc_fused, conv_fused;          // fused schedule: fc (comm stream) || conv (compute stream)
+  int twoshot, oneshot;              // separate launches: two-shot fc || one-shot conv (caps)
+  int cap_fc_fused, cap_conv_fused, cap_twoshot, cap_oneshot;   // resident WGs per GPU (occupancy x CUs)
+  double load_fused, load_separate;  // co_ranks * sum(grid / cap) of each concurrent pair
+};
+// Throws std::runtime_error when even the minimum grids cannot be co-resident (caller falls back).
+XgmiGrids xgmi_plan_grids(int world, int co_ranks, int64_t oneshot_max_floats, double budget);
+constexpr int XGMI_CONV_VB_MAX = 8;        // conv fused: virtual reduce blocks per workgroup (grid >= 39)
 int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada);
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
 // small buckets: one-shot variant - copy-in to a staging slot (alternating by call parity), ONE

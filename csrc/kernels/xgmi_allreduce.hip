@@ -20,6 +20,9 @@
 // stores; flags are system-scope atomics carrying a per-WG call counter (monotonic, no reset, so
 // graph replays need no host work).  A wait that exceeds the timeout sets *err and returns; every
 // later call then returns at once and the host raises (XgmiComm::check).
+#include <stdexcept>
+#include <string>
+
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 #include "conv_grad_reduce.h"
@@ -42,9 +45,9 @@ __device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, int64_t i, f4 v
 }
 
 // Stage hand-off of workgroup b: lane p (< world) publishes this WG's call counter into rank p's
-// flag slot [stage][my rank][b], then polls its own slot [stage][p][b].  Returns false (and sets
-// *err) on timeout.
-__device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e) {
+// flag slot [stage][my rank][b], then polls its own slot [stage][p][b].  Returns false on timeout
+// and records the first failure as *err = kid << 24 | stage << 16 | peer << 12 | b (XgmiComm::error).
+__device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e, int kid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
   __syncthreads();
   bool ok = true;
@@ -57,7 +60,9 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e) {
     while (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int zero = 0;
+        __hip_atomic_compare_exchange_strong(a.err, &zero, (kid << 24) | (stage << 16) | (p << 12) | b,
+                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = false;
         break;
       }
@@ -114,7 +119,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
   const int64_t bytes = a.nvec * 16;
   const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
 
-  if (!xgmi_stage(a, 0, b, e)) return;
+  if (!xgmi_stage(a, 0, b, e, XGMI_K_TWOSHOT)) return;
   // ---- phase 1: shard r of the sum -> my output
   {
     __amdgpu_buffer_rsrc_t in[W];
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
       if (i2 < hi) st_sys(out, i2, t);
     }
   }
-  if (!xgmi_stage(a, 1, b, e)) return;
+  if (!xgmi_stage(a, 1, b, e, XGMI_K_TWOSHOT)) return;
   // ---- phase 2: every other rank's reduced shard -> my output (the same index set per WG)
   if (!a.fuse_ada) {
     __amdgpu_buffer_rsrc_t src[W];
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
       }
     }
   }
-  if (!xgmi_stage(a, 0, b, e)) return;
+  if (!xgmi_stage(a, 0, b, e, XGMI_K_ONESHOT)) return;
   __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) src[p] = rsrc(a.stage[p] + slot, p == r ? 0 : bytes);   // own: registers
@@ -237,8 +242,18 @@ __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
   }
 }
 
+namespace {
+inline int clamp_grid(int64_t natural, int lo, int cap) {
+  int64_t g = natural < cap ? natural : cap;
+  if (g < lo) g = lo;
+  if (g > XGMI_MAX_WG) g = XGMI_MAX_WG;
+  return (int)(g < 1 ? 1 : g);
+}
+}  // namespace
+
 void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
-  const dim3 g((unsigned)((a.nvec + 255) / 256 < XGMI_MAX_WG ? (a.nvec + 255) / 256 : XGMI_MAX_WG)), blk(256);
+  // <= 4 float4 per lane (KMAX): the grid may shrink to nvec / 1024 workgroups, never below
+  const dim3 g(clamp_grid((a.nvec + 255) / 256, (int)((a.nvec + 1023) / 1024), a.max_wg)), blk(256);
   switch (a.world) {
     case 1: hipLaunchKernelGGL(xgmi_oneshot_kernel<1>, g, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(xgmi_oneshot_kernel<2>, g, blk, 0, s, a); break;
@@ -255,13 +270,14 @@ void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 // fc bucket with the fc Adadelta step fused (two-shot).  The unit of work is a 64(o) x 32(i) tile
 // of fc1.weight (576 tiles) plus one pseudo-tile for the tail (fc1.b, fc2.w, fc2.b; 368 float4):
-// shard p = units [p*577/W, (p+1)*577/W).  Phase 1: WG b reduces units b, b+G, .. of shard r (rank
-// order) into its output bucket; stage 1; phase 2: WG b gathers units b, b+G, .. of EVERY shard
-// (all loads in flight at once), applies Ada::step with the gathered sums as gradients and writes
-// param / square_avg / acc_delta plus the bf16 shadows w1 [128][9216] and w1t [9216][128] (tile
-// transposed through LDS) - exactly the adadelta kernel's fc1 tile math, so bitwise equal to the
-// all-reduce + separate update it replaces.  The fc branch of the DDP step loses a launch and a
-// 4.7 MB gradient re-read.
+// shard p = units [p*577/W, (p+1)*577/W).  Workgroup b owns units lo_p + b + m*G of every shard p
+// (G = grid, any size: the residency planner may shrink it).  Phase 1: WG b reduces its units of
+// shard r (rank order) into its output bucket; stage 1; phase 2: WG b gathers its units of EVERY
+// shard, two at a time (gathered sums + local optimizer state in flight together), applies Ada::step
+// with the gathered sums as gradients and writes param / square_avg / acc_delta plus the bf16 shadows
+// w1 [128][9216] and w1t [9216][128] (tile transposed through LDS) - exactly the adadelta kernel's
+// fc1 tile math, so bitwise equal to the all-reduce + separate update it replaces.  The fc branch
+// of the DDP step loses a launch and a 4.7 MB gradient re-read.
 namespace {
 constexpr int FCU_TILES = 2 * (NFLAT / 32);                      // 576
 constexpr int FCU_UNITS = FCU_TILES + 1;                         // + tail
@@ -283,9 +299,10 @@ __device__ __forceinline__ int fcu_f4(int u, int h, int tid) {
 
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
-  constexpr int UMAX = W == 1 ? 3 : W == 2 ? 2 : 1;              // units per shard per WG (host grid)
+  constexpr int PU = W <= 2 ? 2 : 1;                             // phase-1 units in flight per lane
+  constexpr int PG = 2;                                          // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;
-  __shared__ __attribute__((aligned(16))) uint16_t ts[W * UMAX][32 * FCU_TS];
+  __shared__ __attribute__((aligned(16))) uint16_t ts[PG][32 * FCU_TS];
   const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
   if (tid == 0) {
     const int e = a.ctr[b] + 1;
@@ -298,115 +315,109 @@ __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
   const int e = s_epoch, r = a.rank;
   const int64_t bytes = a.nvec * 16;
   const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
-  if (!xgmi_stage(a, 0, b, e)) return;
+  if (!xgmi_stage(a, 0, b, e, XGMI_K_FC_FUSED)) return;
   // ---- phase 1: my shard's units, rank-order sums -> my output
   {
     __amdgpu_buffer_rsrc_t in[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) in[p] = rsrc(a.in[p], bytes);
     const int lo = fcu_lo(r, W), hi = fcu_lo(r + 1, W);
+    for (int u0 = lo + b; u0 < hi; u0 += PU * G) {
+      f4 v[PU][2][W];
+      int q[PU][2];
 #pragma unroll
-    for (int m = 0; m < UMAX; ++m) {
-      const int u = lo + b + m * G;
-      if (u >= hi) break;
-      f4 v[2][W];
+      for (int j = 0; j < PU; ++j) {
+        const int u = u0 + j * G;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
+        for (int h = 0; h < 2; ++h) {
+          q[j][h] = u < hi ? fcu_f4(u, h, tid) : -1;
 #pragma unroll
-        for (int p = 0; p < W; ++p) v[h][p] = ld_sys(in[p], q < 0 ? a.nvec : q);   // q < 0: past the end -> 0
+          for (int p = 0; p < W; ++p) v[j][h][p] = ld_sys(in[p], q[j][h] < 0 ? a.nvec : q[j][h]);   // -1: 0
+        }
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
-        f4 t = v[h][0];
+      for (int j = 0; j < PU; ++j)
 #pragma unroll
-        for (int p = 1; p < W; ++p) t += v[h][p];
-        if (q >= 0) st_sys(out, q, t);
-      }
+        for (int h = 0; h < 2; ++h) {
+          f4 t = v[j][h][0];
+#pragma unroll
+          for (int p = 1; p < W; ++p) t += v[j][h][p];
+          if (q[j][h] >= 0) st_sys(out, q[j][h], t);
+        }
     }
   }
-  if (!xgmi_stage(a, 1, b, e)) return;
-  // ---- phase 2: every shard's units of this WG, PG shards at a time: gathered sums + local
-  // optimizer state all in flight per group.  PG bounds the registers (~100 VGPRs) so this kernel,
-  // which runs on the comm stream beside the conv backward, co-resides with wgrad / dgrad
-  // workgroups instead of taking whole CUs from them.
+  if (!xgmi_stage(a, 1, b, e, XGMI_K_FC_FUSED)) return;
+  // ---- phase 2: items j = p + W*m (unit lo_p + b + m*G of shard p), PG per pass; consecutive items
+  // come from different shards, i.e. different peers' links.  Workgroup-uniform loop bounds (the
+  // LDS transpose needs the barriers).
   const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
-  constexpr int PG = W < 2 ? W : 2;
+  const int M = ((FCU_UNITS + W - 1) / W + G - 1) / G;         // units per shard per WG (upper bound)
+  for (int j0 = 0; j0 < W * M; j0 += PG) {
+    int uu[PG], pp[PG];
+    f4 g[PG][2];
+    float4 pr[PG][2], sq[PG][2], ac[PG][2];
 #pragma unroll
-  for (int p0 = 0; p0 < W; p0 += PG) {
-    f4 g[PG][UMAX][2];
-    float4 pr[PG][UMAX][2], sq[PG][UMAX][2], ac[PG][UMAX][2];
-#pragma unroll
-    for (int pp = 0; pp < PG; ++pp) {
-      const int p = p0 + pp;
-      if (p >= W) break;
+    for (int k = 0; k < PG; ++k) {
+      const int j = j0 + k, p = j % W, m = j / W;
+      const int u = fcu_lo(p, W) + b + m * G;
+      uu[k] = (j < W * M && u < fcu_lo(p + 1, W)) ? u : -1;
+      pp[k] = p;
+      if (uu[k] < 0) continue;
       const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
 #pragma unroll
-      for (int m = 0; m < UMAX; ++m) {
-        const int u = fcu_lo(p, W) + b + m * G;
-        if (u >= fcu_lo(p + 1, W)) continue;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int q = fcu_f4(u, h, tid);
-          if (q < 0) continue;
-          g[pp][m][h] = ld_sys(src, q);
-          pr[pp][m][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
-          sq[pp][m][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
-          ac[pp][m][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
-        }
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+        if (q < 0) continue;
+        g[k][h] = ld_sys(src, q);
+        pr[k][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
+        sq[k][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
+        ac[k][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
       }
     }
 #pragma unroll
-    for (int pp = 0; pp < PG; ++pp) {
-      const int p = p0 + pp;
-      if (p >= W) break;
+    for (int k = 0; k < PG; ++k) {
+      const int u = uu[k];
+      if (u < 0) continue;
+      float v8[8];
 #pragma unroll
-      for (int m = 0; m < UMAX; ++m) {
-        const int u = fcu_lo(p, W) + b + m * G;
-        if (u >= fcu_lo(p + 1, W)) continue;
-        float v8[8];
+      for (int h = 0; h < 2; ++h) {
+        const int q = fcu_f4(u, h, tid);
+        if (q < 0) continue;
+        float4 P = pr[k][h], S = sq[k][h], A = ac[k][h];
+        const f4 G4 = g[k][h];
+        ad.step(P.x, G4.x, S.x, A.x);
+        ad.step(P.y, G4.y, S.y, A.y);
+        ad.step(P.z, G4.z, S.z, A.z);
+        ad.step(P.w, G4.w, S.w, A.w);
+        reinterpret_cast<float4*>(a.ada.param)[q] = P;
+        reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
+        reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
+        v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
+      }
+      if (u < FCU_TILES) {                                        // bf16 shadows of the fc1 tile
+        const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+        const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
+        uint4 lo4;
+        lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
+        lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
+        *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
+        uint16_t* t = ts[k];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int q = fcu_f4(u, h, tid);
-          if (q < 0) continue;
-          float4 P = pr[pp][m][h], S = sq[pp][m][h], A = ac[pp][m][h];
-          const f4 G4 = g[pp][m][h];
-          ad.step(P.x, G4.x, S.x, A.x);
-          ad.step(P.y, G4.y, S.y, A.y);
-          ad.step(P.z, G4.z, S.z, A.z);
-          ad.step(P.w, G4.w, S.w, A.w);
-          reinterpret_cast<float4*>(a.ada.param)[q] = P;
-          reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
-          reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
-          v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
-        }
-        if (u < FCU_TILES) {                                        // bf16 shadows of the fc1 tile
-          const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
-          const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
-          uint4 lo4;
-          lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
-          lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
-          *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
-          uint16_t* t = ts[p * UMAX + m];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) t[(ic + j) * FCU_TS + ol] = f2bf(v8[j]);
-        }
+        for (int jj = 0; jj < 8; ++jj) t[(ic + jj) * FCU_TS + ol] = f2bf(v8[jj]);
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
-#pragma unroll
-    for (int m = 0; m < UMAX; ++m) {
-      const int u = fcu_lo(p, W) + b + m * G;
-      if (u >= fcu_lo(p + 1, W) || u >= FCU_TILES) continue;
+    for (int k = 0; k < PG; ++k) {
+      const int u = uu[k];
+      if (u < 0 || u >= FCU_TILES) continue;
       const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
       const int il = tid >> 3, oc = (tid & 7) * 8;
       *reinterpret_cast<uint4*>(a.ada.w1t + (int64_t)(32 * it + il) * NH + 64 * ot + oc) =
-          *reinterpret_cast<const uint4*>(ts[p * UMAX + m] + il * FCU_TS + oc);
+          *reinterpret_cast<const uint4*>(ts[k] + il * FCU_TS + oc);
     }
+    __syncthreads();                                              // ts is rewritten by the next pass
+    (void)pp;
   }
 }
 
@@ -416,7 +427,7 @@ int xgmi_fc_fused_workgroups(int world) {
 }
 
 void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s) {
-  const dim3 g(xgmi_fc_fused_workgroups(a.world)), blk(256);
+  const dim3 g(clamp_grid(xgmi_fc_fused_workgroups(a.world), 1, a.max_wg)), blk(256);
   switch (a.world) {
     case 1: hipLaunchKernelGGL(xgmi_fc_fused_kernel<1>, g, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(xgmi_fc_fused_kernel<2>, g, blk, 0, s, a); break;
@@ -431,12 +442,14 @@ void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// conv bucket, fully fused: WG b runs conv_grad_reduce's WG b (same slab partition and summation
-// order -> the same bits), keeps its <= 4 finished gradients per lane in registers, publishes them
-// into this rank's staging slot (call parity; 4-byte write-through stores at their bucket index),
-// hands off once (stage 0: WG b of every rank is done with the same indices), then sums every
-// rank's values at those indices in rank order and applies Ada::step + the conv2 bf16 shadows.
-// Replaces conv_grad_reduce + the one-shot all-reduce: one launch less on the DDP critical path.
+// conv bucket, fully fused: the 309 blocks of conv_grad_reduce's partition become virtual blocks
+// vb = b, b + G, .. of workgroup b (same slab partition and summation order per block -> the same
+// bits).  Each virtual block's <= 64 finished gradients go to LDS slots (k*64 + lane*4 + r), are
+// published into this rank's staging slot (call parity; 4-byte write-through stores at their bucket
+// index), ONE hand-off (stage 0: WG b of every rank is done with the same indices), then every rank's
+// values at those indices are summed in rank order and Ada::step + the conv2 bf16 shadows applied -
+// one slot per lane (<= 512 slots: XGMI_CONV_VB_MAX virtual blocks).  Replaces conv_grad_reduce +
+// the one-shot all-reduce + the conv update: one launch on the DDP critical path.
 namespace {
 __device__ __forceinline__ void st_sys1(__amdgpu_buffer_rsrc_t r, int64_t i, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)(i * 4), 0, SYS);
@@ -444,67 +457,75 @@ __device__ __forceinline__ void st_sys1(__amdgpu_buffer_rsrc_t r, int64_t i, flo
 __device__ __forceinline__ float ld_sys1(__amdgpu_buffer_rsrc_t r, int64_t i) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4), 0, SYS));
 }
+constexpr int CONV_SLOTS = XGMI_CONV_VB_MAX * 64;
+constexpr int CONV_SLOTS_PER_LANE = CONV_SLOTS / 256;
 }  // namespace
 
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a, ConvBwdArgs c, int B) {
   __shared__ float4 red[256];
+  __shared__ float s_val[CONV_SLOTS];
+  __shared__ int s_idx[CONV_SLOTS];
   __shared__ int s_epoch, s_err;
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
+  const int nvb = (RED_WGS - b + G - 1) / G;                   // <= XGMI_CONV_VB_MAX (host grid >= 39)
+#pragma unroll
+  for (int k = 0; k < CONV_SLOTS_PER_LANE; ++k) s_idx[tid + 256 * k] = -1;
   if (tid == 0) {
     const int e = a.ctr[b] + 1;
     a.ctr[b] = e;
     s_epoch = e;
     s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // (s_err is read after the reduce's barriers; a poisoned communicator skips the exchange)
-  float vals[4];
-  int64_t idx[4];
-  int nv = 0;
-  reduce_conv_grads(c, B, b, red, [&](int64_t el, float v) {
-    vals[nv] = v;
-    idx[nv] = el - a.ada_base;
-    ++nv;
-  });
+  // (the reduce's first barrier orders the slot initialisation before any sink write)
+  for (int k = 0; k < nvb; ++k) {
+    int nv = 0;
+    reduce_conv_grads(c, B, b + k * G, red, [&](int64_t el, float v) {   // lanes 0..15, <= 4 each
+      const int q = k * 64 + tid * 4 + nv;
+      s_idx[q] = (int)(el - a.ada_base);
+      s_val[q] = v;
+      ++nv;
+    });
+  }
   __syncthreads();
   if (s_err) return;
   const int e = s_epoch, r = a.rank;
   const int64_t slot = (e & 1) * a.slot_floats;
   const int64_t bytes = a.nvec * 16;
+  int idx[CONV_SLOTS_PER_LANE];
+  float val[CONV_SLOTS_PER_LANE], pr[CONV_SLOTS_PER_LANE], sq[CONV_SLOTS_PER_LANE], ac[CONV_SLOTS_PER_LANE];
   {
     const __amdgpu_buffer_rsrc_t mine = rsrc(a.stage[r] + slot, bytes);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (k < nv) st_sys1(mine, idx[k], vals[k]);
-  }
-  // the update's local state, loaded before the hand-off wait
-  float pr[4], sq[4], ac[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (k < nv) {
-      const int64_t el = a.ada_base + idx[k];
-      pr[k] = a.ada.param[el];
+    for (int k = 0; k < CONV_SLOTS_PER_LANE; ++k) {
+      const int q = tid + 256 * k;
+      idx[k] = q < nvb * 64 ? s_idx[q] : -1;
+      if (idx[k] < 0) continue;
+      val[k] = s_val[q];
+      st_sys1(mine, idx[k], val[k]);
+      const int64_t el = a.ada_base + idx[k];                   // the update's local state, loaded
+      pr[k] = a.ada.param[el];                                  // before the hand-off wait
       sq[k] = a.ada.square_avg[el];
       ac[k] = a.ada.acc_delta[el];
     }
-  if (!xgmi_stage(a, 0, b, e)) return;
+  }
+  if (!xgmi_stage(a, 0, b, e, XGMI_K_CONV_FUSED)) return;
   if (b == 0 && tid == 0 && a.ada.state_inc) a.ada.state_inc->step += 1;   // end-of-step marker
-  if (nv == 0) return;
   __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) src[p] = rsrc(a.stage[p] + slot, p == r ? 0 : bytes);   // own: registers
-  float v[4][W];
+  float v[CONV_SLOTS_PER_LANE][W];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < CONV_SLOTS_PER_LANE; ++k)
 #pragma unroll
-    for (int p = 0; p < W; ++p) v[k][p] = ld_sys1(src[p], k < nv ? idx[k] : 0);
+    for (int p = 0; p < W; ++p) v[k][p] = ld_sys1(src[p], idx[k] < 0 ? 0 : idx[k]);
   const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (k >= nv) break;
-    float g = (r == 0) ? vals[k] : v[k][0];
+  for (int k = 0; k < CONV_SLOTS_PER_LANE; ++k) {
+    if (idx[k] < 0) continue;
+    float g = (r == 0) ? val[k] : v[k][0];
 #pragma unroll
-    for (int p = 1; p < W; ++p) g += (p == r) ? vals[k] : v[k][p];
+    for (int p = 1; p < W; ++p) g += (p == r) ? val[k] : v[k][p];
     const int64_t el = a.ada_base + idx[k];
     float P = pr[k], S = sq[k], A = ac[k];
     ad.step(P, g, S, A);
@@ -521,9 +542,13 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
   }
 }
 
+namespace {
+constexpr int CONV_FUSED_MIN_WG = (RED_WGS + XGMI_CONV_VB_MAX - 1) / XGMI_CONV_VB_MAX;   // 39
+}
+
 void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
   static_assert(RED_WGS <= XGMI_MAX_WG, "one flag slot per reduce workgroup");
-  const dim3 g(RED_WGS), blk(256);
+  const dim3 g(clamp_grid(RED_WGS, CONV_FUSED_MIN_WG, a.max_wg)), blk(256);
   switch (a.world) {
     case 1: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<1>, g, blk, 0, s, a, c, B); break;
     case 2: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<2>, g, blk, 0, s, a, c, B); break;
@@ -548,7 +573,7 @@ int xgmi_workgroups(int64_t nvec, int world, bool fuse_ada) {
 }
 
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
-  const dim3 g(xgmi_workgroups(a.nvec, a.world, a.fuse_ada != 0)), blk(256);
+  const dim3 g(clamp_grid(xgmi_workgroups(a.nvec, a.world, a.fuse_ada != 0), 1, a.max_wg)), blk(256);
   switch (a.world) {
     case 1: hipLaunchKernelGGL(xgmi_allreduce_kernel<1>, g, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(xgmi_allreduce_kernel<2>, g, blk, 0, s, a); break;
@@ -560,6 +585,73 @@ void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
     case 8: hipLaunchKernelGGL(xgmi_allreduce_kernel<8>, g, blk, 0, s, a); break;
     default: break;   // the host rejects world sizes outside 1..XGMI_MAX_RANKS
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Residency planner (see XgmiGrids in kernels.h).
+namespace {
+template <int W>
+void occupancies(int* fc, int* conv, int* two, int* one) {
+  auto occ = [](const void* f) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess || n < 1) n = 1;
+    return n;
+  };
+  *fc = occ(reinterpret_cast<const void*>(&xgmi_fc_fused_kernel<W>));
+  *conv = occ(reinterpret_cast<const void*>(&xgmi_conv_reduce_fused_kernel<W>));
+  *two = occ(reinterpret_cast<const void*>(&xgmi_allreduce_kernel<W>));
+  *one = occ(reinterpret_cast<const void*>(&xgmi_oneshot_kernel<W>));
+}
+
+// shrink grids a (min amin, cap ca) and b so that co * (a/ca + b/cb) <= budget; returns the load
+double fit_pair(int* a, int amin, int ca, int* b, int bmin, int cb, int co, double budget) {
+  auto load = [&] { return co * ((double)*a / ca + (double)*b / cb); };
+  if (load() > budget) {
+    const double s = budget / load();
+    *a = (int)(*a * s) > amin ? (int)(*a * s) : amin;
+    *b = (int)(*b * s) > bmin ? (int)(*b * s) : bmin;
+  }
+  return load();
+}
+}  // namespace
+
+XgmiGrids xgmi_plan_grids(int world, int co_ranks, int64_t oneshot_max_floats, double budget) {
+  if (world < 1 || world > XGMI_MAX_RANKS) throw std::runtime_error("xgmi_plan_grids: bad world size");
+  if (co_ranks < 1) co_ranks = 1;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    throw std::runtime_error("xgmi_plan_grids: cannot query the device");
+  int ofc = 1, oconv = 1, otwo = 1, oone = 1;
+  switch (world) {
+    case 1: occupancies<1>(&ofc, &oconv, &otwo, &oone); break;
+    case 2: occupancies<2>(&ofc, &oconv, &otwo, &oone); break;
+    case 3: occupancies<3>(&ofc, &oconv, &otwo, &oone); break;
+    case 4: occupancies<4>(&ofc, &oconv, &otwo, &oone); break;
+    case 5: occupancies<5>(&ofc, &oconv, &otwo, &oone); break;
+    case 6: occupancies<6>(&ofc, &oconv, &otwo, &oone); break;
+    case 7: occupancies<7>(&ofc, &oconv, &otwo, &oone); break;
+    default: occupancies<8>(&ofc, &oconv, &otwo, &oone); break;
+  }
+  XgmiGrids g{};
+  g.cap_fc_fused = ofc * cus;
+  g.cap_conv_fused = oconv * cus;
+  g.cap_twoshot = otwo * cus;
+  g.cap_oneshot = oone * cus;
+  const int one_nat = (int)((oneshot_max_floats / 4 + 255) / 256);
+  const int one_min = (int)((oneshot_max_floats / 4 + 1023) / 1024);
+  g.fc_fused = xgmi_fc_fused_workgroups(world);
+  g.conv_fused = RED_WGS;
+  g.twoshot = XGMI_MAX_WG;                                       // cap: launches use min(natural, cap)
+  g.oneshot = one_nat < XGMI_MAX_WG ? (one_nat > one_min ? one_nat : one_min) : XGMI_MAX_WG;
+  g.load_fused = fit_pair(&g.fc_fused, 8, g.cap_fc_fused, &g.conv_fused, CONV_FUSED_MIN_WG, g.cap_conv_fused,
+                          co_ranks, budget);
+  g.load_separate = fit_pair(&g.twoshot, 8, g.cap_twoshot, &g.oneshot, one_min > 1 ? one_min : 1, g.cap_oneshot,
+                             co_ranks, budget);
+  if (g.load_fused > 1.0 || g.load_separate > 1.0)
+    throw std::runtime_error("xgmi: the spinning all-reduce grids of " + std::to_string(co_ranks) +
+                             " ranks per GPU cannot all be resident");
+  return g;
 }
 
 }  // namespace mnist

@@ -396,14 +396,33 @@ bool Engine::probe_stream_handoff(double timeout_s) {
   return err == 0;
 }
 
+std::pair<int, int> Engine::errors() const {
+  int err = 0;
+  HIP_OK(hipMemcpy(&err, sync_ + 2, sizeof(int), hipMemcpyDeviceToHost));
+  return {err, xgmi_ ? xgmi_->error() : 0};
+}
+
+std::string Engine::describe_xgmi_error(int code) {
+  static const char* names[] = {"?", "two-shot all-reduce", "one-shot all-reduce", "fused fc all-reduce+Adadelta",
+                                "fused conv reduce+all-reduce+Adadelta"};
+  const int kid = (code >> 24) & 0xff;
+  return std::string(names[kid >= 1 && kid <= 4 ? kid : 0]) + " kernel, stage " + std::to_string((code >> 16) & 0xf) +
+         ", waiting for peer rank " + std::to_string((code >> 12) & 0xf) + ", workgroup " + std::to_string(code & 0xfff);
+}
+
+void Engine::check_errors() const {
+  const auto e = errors();
+  if (e.first) throw std::runtime_error("engine: a schedule-3 stream hand-off timed out (results invalid)");
+  if (e.second)
+    throw std::runtime_error("engine: an xGMI all-reduce stage timed out (results invalid): " +
+                             describe_xgmi_error(e.second));
+}
+
 void Engine::synchronize() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
   if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
-  int err = 0;
-  HIP_OK(hipMemcpy(&err, sync_ + 2, sizeof(int), hipMemcpyDeviceToHost));
-  if (err) throw std::runtime_error("engine: a schedule-3 stream hand-off timed out (results invalid)");
-  if (xgmi_ && xgmi_->error()) throw std::runtime_error("engine: an xGMI all-reduce stage timed out (results invalid)");
+  check_errors();
 }
 
 }  // namespace mnist

@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <map>
 #include <memory>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -105,7 +106,12 @@ class Engine {
   // --- misc
   void refresh_shadows();
   void broadcast_params(int root);                   // DDP construction: rank-0 params to all
-  void synchronize();
+  void synchronize();                                // all streams, then check_errors()
+  // device error flags: (schedule-3 hand-off timeout, xGMI error code); a 4-byte D2H each, call
+  // after the work of interest has completed (e.g. once per epoch)
+  std::pair<int, int> errors() const;
+  void check_errors() const;                         // throws with a decoded message
+  static std::string describe_xgmi_error(int code);
   int64_t workspace_bytes() const { return ws_bytes_; }
 
   // single-op entry points used by the numerics tests / module API

@@ -21,6 +21,7 @@ struct Record {
   int64_t in_off, out_off;
   int64_t numel, oneshot_max;
   int32_t world, rank, channels, pid, device;
+  int32_t grid_fc, grid_conv, grid_two, grid_one;   // residency-planned grids (must agree across ranks)
   char host[64];                 // IPC mappings only exist between the GPUs of one node
 };
 
@@ -34,7 +35,7 @@ void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
 }  // namespace
 
 XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
-                   int64_t oneshot_max)
+                   int64_t oneshot_max, int co_ranks, double budget)
     : world_(world), rank_(rank), device_(device), channels_(channels), in_(in), out_(out), numel_(numel),
       oneshot_max_(oneshot_max) {
   // the one-shot kernel keeps <= 4 float4 per lane of <= XGMI_MAX_WG workgroups
@@ -45,6 +46,7 @@ XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64
   if (channels < 1) throw std::runtime_error("xgmi: need at least one channel");
   if (((uintptr_t)in | (uintptr_t)out) & 15) throw std::runtime_error("xgmi: buffers must be 16-byte aligned");
   ok(hipSetDevice(device), "hipSetDevice");
+  grids_ = xgmi_plan_grids(world, co_ranks, oneshot_max, budget);   // throws when not co-resident
   ok(hipMalloc(&flags_, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMalloc(flags)");
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
@@ -92,6 +94,10 @@ std::vector<uint8_t> XgmiComm::record() const {
   r.channels = channels_;
   r.pid = (int32_t)getpid();
   r.device = device_;
+  r.grid_fc = grids_.fc_fused;
+  r.grid_conv = grids_.conv_fused;
+  r.grid_two = grids_.twoshot;
+  r.grid_one = grids_.oneshot;
   gethostname(r.host, sizeof(r.host) - 1);
   const uint8_t* b = reinterpret_cast<const uint8_t*>(&r);
   return std::vector<uint8_t>(b, b + sizeof(r));
@@ -122,6 +128,9 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
     if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_ ||
         r.oneshot_max != oneshot_max_)
       throw std::runtime_error("xgmi: peer record does not match this communicator");
+    if (r.grid_fc != grids_.fc_fused || r.grid_conv != grids_.conv_fused || r.grid_two != grids_.twoshot ||
+        r.grid_one != grids_.oneshot)
+      throw std::runtime_error("xgmi: ranks planned different kernel grids (mixed GPUs or co_ranks?)");
     char host[64] = {0};
     gethostname(host, sizeof(host) - 1);
     if (strncmp(host, r.host, sizeof(host)) != 0)
@@ -166,6 +175,7 @@ XgmiArgs XgmiComm::args(int channel, int64_t offset, int64_t count) const {
   a.rank = rank_;
   a.nvec = count / 4;
   a.timeout_ticks = timeout_ticks_;
+  a.max_wg = XGMI_MAX_WG;
   return a;
 }
 
@@ -174,6 +184,7 @@ void XgmiComm::allreduce_fc_fused(int channel, hipStream_t stream, const Adadelt
   a.fuse_ada = 1;
   a.ada_base = OFF_FC1_W;
   a.ada = ada;
+  a.max_wg = grids_.fc_fused;
   launch_xgmi_fc_fused(a, stream);
 }
 
@@ -184,6 +195,7 @@ void XgmiComm::conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hi
   a.fuse_ada = 1;
   a.ada_base = OFF_CONV1_W;
   a.ada = ada;
+  a.max_wg = grids_.conv_fused;
   launch_xgmi_conv_reduce_fused(a, conv, B, stream);
 }
 
@@ -195,8 +207,13 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
     a.ada_base = offset;
     a.ada = *ada;
   }
-  if (count <= oneshot_max_) launch_xgmi_allreduce_oneshot(a, stream);
-  else launch_xgmi_allreduce(a, stream);
+  if (count <= oneshot_max_) {
+    a.max_wg = grids_.oneshot;
+    launch_xgmi_allreduce_oneshot(a, stream);
+  } else {
+    a.max_wg = grids_.twoshot;
+    launch_xgmi_allreduce(a, stream);
+  }
 }
 
 int XgmiComm::error() const {

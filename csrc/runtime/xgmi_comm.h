@@ -25,8 +25,11 @@ class XgmiComm {
   // support IPC export: hipMalloc or blocks of torch's caching allocator)
   // Buckets of at most `oneshot_max` floats use the one-shot kernel (one hand-off per call; staging
   // slots allocated here, 2 per channel); larger ones the two-shot reduce-scatter + all-gather.
+  // co_ranks: how many ranks drive this rank's GPU (1 in production; > 1 in the one-GPU multi-process
+  // rehearsal) - the kernel grids are sized so every rank's spinning workgroups fit at once
+  // (xgmi_plan_grids, `budget` = fraction of the GPU's workgroup slots they may take).
   XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
-           int64_t oneshot_max = 32768);
+           int64_t oneshot_max = 32768, int co_ranks = 1, double budget = 0.5);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -47,8 +50,10 @@ class XgmiComm {
   // The engine's conv bucket straight from the conv gradient slabs: slab reduce + one-shot
   // all-reduce + Adadelta + conv2 shadows in one launch (launch_xgmi_conv_reduce_fused).
   void conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hipStream_t stream, const AdadeltaArgs& ada);
-  // device error flag (a stage wait timed out on this rank); synchronous read
+  // device error code (0 = ok; else the first stage wait that timed out on this rank:
+  // kernel id << 24 | stage << 16 | peer << 12 | workgroup); synchronous read
   int error() const;
+  const XgmiGrids& grids() const { return grids_; }
   void set_timeout_seconds(double s);
   int world_size() const { return world_; }
   int rank() const { return rank_; }
@@ -64,6 +69,7 @@ class XgmiComm {
   int* ctr_ = nullptr;       // [channels][XGMI_MAX_WG], local
   int* err_ = nullptr;
   uint64_t timeout_ticks_;
+  XgmiGrids grids_;
   bool connected_ = false;
   std::vector<const float*> peer_in_;
   std::vector<float*> peer_out_;

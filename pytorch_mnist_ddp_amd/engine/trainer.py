@@ -119,43 +119,42 @@ class FusedTrainer:
         if allreduce not in ("rccl", "xgmi", "auto"):
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
         self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
+        self.xgmi_validation = None
         want = allreduce == "xgmi" and (comm is not None or world_size > 1)
         probe_always = os.environ.get("MNIST_AMD_PROBE_ALWAYS", "0") == "1"   # tests: probe at world 1
         want = want or (allreduce == "auto" and comm is not None and (world_size > 1 or probe_always))
+        # Adadelta fused into the xGMI kernels (default; MNIST_AMD_XGMI_FUSE=0: separate launches).
+        # Decided before the probe: only a fused schedule saves the RCCL side's separate conv update.
+        self.xgmi_fuse = os.environ.get("MNIST_AMD_XGMI_FUSE", "1") != "0"
         if want:
             from ..parallel.distributed import choose_allreduce, create_xgmi_comm
             self.grad_out = torch.zeros_like(mstate.grad)
             self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad, self.grad_out)
             if self.xgmi is not None and allreduce == "auto":
                 split = mstate.bucket_split
-                # the RCCL schedule's separate conv update (fused away on the xGMI side) is timed on
-                # a scratch copy of the optimizer state, so the probe leaves the model untouched
-                scratch = {k: getattr(mstate, k).clone() for k in ("param", "square_avg", "acc_delta", "w2f", "w2d")}
-                p_ = native.ptr
-                upd = [lambda: C.adadelta(p_(scratch["param"]), p_(mstate.grad), p_(scratch["square_avg"]),
-                                          p_(scratch["acc_delta"]), p_(mstate.lr), mstate.rho, mstate.eps,
-                                          mstate.weight_decay, p_(scratch["w2f"]), p_(scratch["w2d"]),
-                                          p_(mstate.w1), p_(mstate.w1t), 0, 2, True,
-                                          int(torch.cuda.current_stream(dev).cuda_stream))]
+                upd = []
+                if self.xgmi_fuse:
+                    # the RCCL schedule's separate conv update (fused away on the xGMI side) is timed
+                    # on a scratch copy of the optimizer state, so the probe leaves the model untouched
+                    scratch = {k: getattr(mstate, k).clone() for k in ("param", "square_avg", "acc_delta", "w2f", "w2d")}
+                    p_ = native.ptr
+                    upd = [lambda: C.adadelta(p_(scratch["param"]), p_(mstate.grad), p_(scratch["square_avg"]),
+                                              p_(scratch["acc_delta"]), p_(mstate.lr), mstate.rho, mstate.eps,
+                                              mstate.weight_decay, p_(scratch["w2f"]), p_(scratch["w2d"]),
+                                              p_(mstate.w1), p_(mstate.w1t), 0, 2, True,
+                                              int(torch.cuda.current_stream(dev).cuda_stream))]
                 with torch.cuda.stream(self.compute):
                     pick, self.allreduce_timings = choose_allreduce(
                         comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad, self.grad_out,
                         (0, split), (split, mstate.grad.numel() - split), dev, rccl_extra=upd)
-                del scratch
+                upd = None
                 if pick != "xgmi":
                     self.xgmi = None
             if self.xgmi is not None:
-                from ..parallel.distributed import ranks_share_a_device
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
-                # Adadelta fused into the all-reduce kernels (MNIST_AMD_XGMI_FUSE=0: separate launches;
-                # default off when ranks share a GPU, where the fused grids cannot all be resident)
-                fuse_env = os.environ.get("MNIST_AMD_XGMI_FUSE")
-                fuse = fuse_env == "1" if fuse_env is not None else not ranks_share_a_device(dev)
-                if fuse_env is None and not fuse and rank == 0:
-                    print("[xgmi] ranks share a GPU: Adadelta update runs as separate launches", flush=True)
-                self.engine.set_xgmi_fuse_update(fuse)
-        # schedule 3 spins on one stream for the other: make sure they sit on different hardware
+                self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
+                # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)
         if uses_sched3:
@@ -174,10 +173,77 @@ class FusedTrainer:
                 if self.xgmi is not None:
                     self.engine.attach_xgmi(None)
                     self.xgmi = None
+        if self.xgmi is not None and os.environ.get("MNIST_AMD_XGMI_VALIDATE", "1") != "0":
+            ok, self.xgmi_validation = self._validate_xgmi_schedule(train)
+            if not ok:
+                if comm is None:
+                    raise RuntimeError(f"xGMI schedule failed its startup validation ({self.xgmi_validation}) "
+                                       "and no RCCL communicator to fall back to")
+                if rank == 0:
+                    print(f"[xgmi] startup validation failed ({self.xgmi_validation}): using RCCL", flush=True)
+                self.engine.attach_xgmi(None)
+                self.xgmi = None
+                self.engine.set_dist_schedule(sched if comm2 is not None else 1)
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None
         self.use_graphs = self.graph_steps > 0
+
+    # ------------------------------------------------------------------ startup validation
+    def _validate_xgmi_schedule(self, train: MNISTData, steps: int = 3) -> tuple[bool, str]:
+        """Run the exact xGMI DDP schedule the trainer will use (eager schedule-3 steps, dropout off,
+        5 s stage timeouts) on scratch copies of the optimizer state before training starts; with the
+        fused kernels also the separate-launch schedule, which must give the same bits.  Passes when no
+        rank timed out, fused == separate, and every rank holds the same parameters afterwards; the
+        verdict is collective (MIN over ranks).  The model state is restored either way."""
+        from ..parallel.distributed import _all_ok, params_fingerprint_equal
+        ms, eng = self.ms, self.engine
+        steps = max(1, min(steps, self.steps_per_epoch))
+        keys = ("param", "square_avg", "acc_delta")
+        snap = {k: getattr(ms, k).clone() for k in keys}
+        idx = torch.arange(steps * self.B, dtype=torch.int64) % max(1, len(train))
+        modes = [True, False] if self.xgmi_fuse else [False]
+        results, why = [], "ok"
+        self.xgmi.set_timeout_seconds(5.0)
+        try:
+            for fuse in modes:
+                with torch.no_grad():
+                    for k in keys:
+                        getattr(ms, k).copy_(snap[k])
+                torch.cuda.synchronize(self.device)
+                eng.refresh_shadows()
+                eng.set_xgmi_fuse_update(fuse)
+                self.upload_indices(idx)
+                eng.begin_epoch(self.seed, 0, 0, FLAG_NO_DROPOUT)
+                eng.train_steps(steps, self.B, self.B)
+                eng.synchronize()                       # raises on a stage / hand-off timeout
+                results.append(ms.param.clone())
+            if len(results) == 2 and not torch.equal(results[0], results[1]):
+                why = "fused kernels differ from the separate launches"
+            elif not torch.isfinite(results[0]).all():
+                why = "non-finite parameters"
+        except RuntimeError as e:
+            why = str(e)
+        ok = why == "ok"
+        if ok and self.world > 1 and not params_fingerprint_equal(results[0], self.device):
+            ok, why = False, "parameters differ across ranks"
+        ok = _all_ok(ok, self.device) if self.world > 1 else ok
+        if not ok and why == "ok":
+            why = "another rank failed"
+        with torch.no_grad():
+            for k in keys:
+                getattr(ms, k).copy_(snap[k])
+        torch.cuda.synchronize(self.device)
+        eng.refresh_shadows()
+        eng.set_xgmi_fuse_update(self.xgmi_fuse)
+        self.xgmi.set_timeout_seconds(60.0)
+        torch.cuda.synchronize(self.device)
+        return ok, why if not ok else f"ok ({steps} steps, {'fused == separate' if len(modes) == 2 else 'separate'})"
+
+    def check_errors(self) -> None:
+        """Raise if a device-side hand-off or xGMI stage wait timed out (the per-epoch check; a 4-byte
+        D2H per flag after the epoch's work has completed)."""
+        self.engine.check_errors()
 
     # ------------------------------------------------------------------ helpers
     def set_lr(self, lr: float) -> None:
@@ -274,6 +340,8 @@ class FusedTrainer:
             flush_one()
         if sync:
             self.compute.synchronize()
+            if self.xgmi is not None or self.comm is not None:
+                self.check_errors()        # fail at the first bad epoch, not after the last one
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
 
     # ------------------------------------------------------------------ raw step stream (bench)

@@ -109,29 +109,52 @@ def _all_ok(flag: bool, device) -> bool:
     return bool(t.item())
 
 
-def ranks_share_a_device(device) -> bool:
-    """True when two ranks of the default process group drive the same physical GPU (the one-GPU
-    multi-process rehearsal).  The fused xGMI kernels wait per workgroup on their peers, so every
-    rank's grid must be resident at once: 4 ranks x 512 workgroups of the 106-VGPR fused fc kernel
-    exceed one GPU's 1024 slots (docs/DEBUGGING.md); with one GPU per rank they always fit."""
+def params_fingerprint_equal(t: torch.Tensor, device) -> bool:
+    """True when every rank's fp32 tensor ``t`` is bitwise identical (all-gather of a fingerprint)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return False
+        return True
+    from .ddp import params_fingerprint
+    fp = params_fingerprint([t])
+    if dist.get_backend() != "nccl":
+        fp = fp.cpu()
+    allv = [torch.zeros_like(fp) for _ in range(dist.get_world_size())]
+    dist.all_gather(allv, fp)
+    return all(torch.equal(v, allv[0]) for v in allv)
+
+
+def _device_identity(device) -> str:
     p = torch.cuda.get_device_properties(torch.device(device))
-    ident = "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
+    return "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
+
+
+def ranks_per_device(device) -> int:
+    """Largest number of ranks of the default process group that drive one physical GPU (1 in the
+    production layout; > 1 in the one-GPU multi-process rehearsal).  The xGMI kernels wait per
+    workgroup on their peers, so the residency planner (``xgmi_plan_grids``) sizes their grids for
+    this many ranks' spinning workgroups on one GPU."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 1
     ids = [None] * dist.get_world_size()
-    dist.all_gather_object(ids, ident)
-    return len(set(ids)) < len(ids)
+    dist.all_gather_object(ids, _device_identity(device))
+    return max(ids.count(i) for i in ids)
+
+
+def ranks_share_a_device(device) -> bool:
+    """True when two ranks of the default process group drive the same physical GPU."""
+    return ranks_per_device(device) > 1
 
 
 def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, grad_out: torch.Tensor,
-                     tag: str | None = None, channels: int = 2, verify: bool = True, oneshot_max: int = 32768):
+                     tag: str | None = None, channels: int = 2, verify: bool = True, oneshot_max: int = 32768,
+                     co_ranks: int | None = None):
     """Direct xGMI all-reduce communicator over ``grad_in`` -> ``grad_out`` (csrc/runtime/xgmi_comm.h).
 
     Every rank exports IPC handles of its two buffers and its flag blocks through the c10d store and
     maps every peer's.  With ``verify`` each channel is then exercised on a rank-dependent pattern
     whose sum is exact in fp32 (5 s stage timeout), and the ranks agree on the outcome.  Returns the
     communicator, or ``None`` on every rank when any rank failed to map its peers or to verify
-    (callers then keep the RCCL all-reduce)."""
+    (callers then keep the RCCL all-reduce).  ``co_ranks`` (default: measured with
+    :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning workgroups are resident."""
     from ..ops import native
     global _xgmi_seq
     C = native.load()
@@ -140,10 +163,12 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
     _xgmi_seq += 1
     dev = torch.device(device)
     numel = grad_in.numel()
+    if co_ranks is None:
+        co_ranks = ranks_per_device(dev)
     x = None
     try:
         x = C.XgmiComm(world_size, rank, dev.index or 0, native.ptr(grad_in), native.ptr(grad_out), numel, channels,
-                       oneshot_max)
+                       oneshot_max, co_ranks)
         if world_size > 1:
             store = dist.distributed_c10d._get_default_store()
             store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())

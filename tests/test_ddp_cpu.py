@@ -197,27 +197,35 @@ def test_allreduce_choice_is_collective_gloo():
 
 
 class _FakeProps:
-    def __init__(self, uuid):
-        self.uuid, self.pci_domain_id, self.pci_bus_id, self.pci_device_id = uuid, 0, 0, 0
+    def __init__(self, uuid, bus=0):
+        self.uuid, self.pci_domain_id, self.pci_bus_id, self.pci_device_id = uuid, 0, bus, 0
 
 
 def _share_worker(rank, world, port, q):
     from pytorch_mnist_ddp_amd.parallel import distributed as D
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", world_size=world, rank=rank)
     try:
-        # device identity is faked (no GPU here): distinct GPUs per rank, then all ranks on one GPU
-        torch.cuda.get_device_properties = lambda d: _FakeProps(f"gpu{rank}")
-        distinct = D.ranks_share_a_device("cpu")
-        torch.cuda.get_device_properties = lambda d: _FakeProps("gpu0")
-        shared = D.ranks_share_a_device("cpu")
-        q.put((rank, distinct, shared))
+        out = []
+        # device identity is faked (no GPU here)
+        cases = [
+            lambda d: _FakeProps(f"gpu{rank}"),              # distinct uuids
+            lambda d: _FakeProps("gpu0"),                    # one GPU for every rank
+            lambda d: _FakeProps("", bus=rank),              # no uuid, distinct PCI bus ids
+            lambda d: _FakeProps("same", bus=7),             # identical uuid + PCI ids everywhere
+            lambda d: _FakeProps("", bus=rank // 2),         # two ranks per GPU (rank 2 alone)
+        ]
+        for fake in cases:
+            torch.cuda.get_device_properties = fake
+            out.append((D.ranks_share_a_device("cpu"), D.ranks_per_device("cpu")))
+        q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-def test_ranks_share_a_device_detection_gloo():
-    """The fused xGMI schedule is turned off by default only when ranks share a GPU
-    (engine/trainer.py, docs/DEBUGGING.md): the detection must agree on every rank."""
+def test_ranks_per_device_detection_gloo():
+    """The xGMI residency planner sizes its grids for ranks_per_device() ranks on one GPU
+    (parallel/distributed.py, kernels.h XgmiGrids): the count must agree on every rank and use the
+    PCI ids when the uuid is empty."""
     world, port = 3, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -227,4 +235,5 @@ def test_ranks_share_a_device_detection_gloo():
     res = sorted(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(60)
-    assert [r[1:] for r in res] == [(False, True)] * world
+    expect = [(False, 1), (True, 3), (False, 1), (True, 3), (True, 2)]
+    assert [r[1] for r in res] == [expect] * world

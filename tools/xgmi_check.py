@@ -64,7 +64,9 @@ def worker(rank: int, world: int, port: int, args, q) -> None:
         gout = torch.zeros(n, device=dev)
         x = create_xgmi_comm(world, rank, dev, gin, gout)
         assert x is not None, "self-test failed"
-        msgs.append("selftest ok")
+        g = x.grids
+        msgs.append(f"selftest ok (grids fc={g['fc_fused']} conv={g['conv_fused']} two={g['twoshot']} "
+                    f"one={g['oneshot']}, load {g['load_fused']:.2f}/{g['load_separate']:.2f})")
         s = torch.cuda.current_stream()
         ranges = [(FC_N, CONV_N), (0, FC_N)]     # channel 0 = conv bucket, 1 = fc bucket
         for it in range(3):
@@ -168,7 +170,7 @@ def _engine_run(torch, dist, world, rank, dev, steps):
     sampler = DistributedIndexStream(len(train), world, rank, shuffle=True, seed=0)
     tr = FusedTrainer(ms, train, None, B, 1000, num_samples=steps * B, world_size=world, rank=rank,
                       seed=1, graph_steps=10, dropout=False, allreduce="xgmi")
-    assert tr.allreduce == "xgmi", "engine fell back to RCCL"
+    assert tr.allreduce == "xgmi", f"engine fell back to RCCL ({tr.xgmi_validation})"
     sampler.set_epoch(1)
     idx = sampler.epoch_indices()[: steps * B]
     tr.start_stream(idx, gather=True)
@@ -183,7 +185,8 @@ def _engine_run(torch, dist, world, rank, dev, steps):
     assert torch.isfinite(losses).all(), "non-finite loss"
     first, last = float(losses[:5].mean()), float(losses[-5:].mean())
     assert last < first, f"loss did not decrease ({first:.4f} -> {last:.4f})"
-    return p, f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical)"
+    return p, (f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical; "
+               f"startup validation {tr.xgmi_validation})")
 
 
 def main() -> int:
@@ -197,9 +200,6 @@ def main() -> int:
                     help="last rank skips one call: the others must time out cleanly (run last; poisons the comm)")
     args = ap.parse_args()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if args.same_device and args.world > 2:
-        # the fused grids of > 2 ranks cannot all be resident on one GPU (docs/DEBUGGING.md)
-        os.environ.setdefault("XGMI_CHECK_FUSE_MODES", "auto")
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
