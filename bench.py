@@ -12,9 +12,21 @@ NLL loss, backward, DDP gradient averaging over RCCL, Adadelta update.  W untime
 then exactly K steps bracketed by barrier + device synchronize on both sides; the reported
 time is the max over ranks; ``value`` is the whole-job images/s (N * B * K / t).
 
-With ``--full-run`` (default on) it then also times the README's complete workload in-process:
-20 epochs of train + per-epoch rank-0 test-set evaluation (10k images) - the reference's
-"Total cost time" minus interpreter/import start-up - and reports it as ``wallclock_20ep_s``.
+With ``--full-run`` (default on) it then also measures the README's complete workload twice:
+
+* ``total_cost_time_s`` - the reference's own metric, measured the reference's way: rank 0 launches
+  ``mnist_ddp.py --batch-size B --epochs 20 --synthetic`` as a child job at the same N (plain
+  ``python`` for N=1, ``torch.distributed.run`` for N>1, README.md:41-51) and reports the max over
+  its ranks of the script's ``Total cost time`` line (mnist_ddp.py:200-203: PG init, data load, DDP
+  construction, 20 x (train with the rank-0 loss prints every 10 batches + rank-0 eval));
+* ``wallclock_20ep_s`` - the same 20 epochs timed in-process on already-built trainers (excludes
+  PG init, data build, model init and communicator setup; no per-10-batch log syncs).
+
+After the timed steps every rank's parameters are fingerprinted and compared (``params_in_sync``;
+the run fails if they differ), and the JSON names the all-reduce actually used (``allreduce``,
+``rccl_world``, probe timings, the xGMI startup validation and kernel grids).
+``--cpu`` instead measures the reference's CPU config (``mnist.py --no-cuda``, batch 64) on this
+host's CPU cores against BASELINE.md's 3,518 img/s anchor.
 
 Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
@@ -25,8 +37,12 @@ import argparse
 import json
 import math
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -40,19 +56,110 @@ from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream  # noqa: 
 from pytorch_mnist_ddp_amd.engine.state import ModelState  # noqa: E402
 from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer  # noqa: E402
 from pytorch_mnist_ddp_amd.models.net import Net  # noqa: E402
-from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comms  # noqa: E402
+from pytorch_mnist_ddp_amd.parallel.distributed import (_max_over_ranks, broadcast_,  # noqa: E402
+                                                        create_rccl_comms)
 
 METRIC = "images/sec + 20-epoch wallclock, MNIST CNN DDP at 1/2/4/8 MI355X"
+CPU_ANCHOR_IMG_S = 3518.0      # torch fp32 CPU train step, B=64, 8 vCPU dev box
+_LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+               "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 900.0, extra=()) -> dict:
+    """The reference's README command at this N (mnist_ddp.py, README.md:41-51) as a child job;
+    returns the max over ranks of its ``Total cost time`` print, the child's wall time and the last
+    printed test accuracy."""
+    script = os.path.join(ROOT, "mnist_ddp.py")
+    sargs = ["--batch-size", str(batch), "--epochs", str(epochs), "--synthetic", *extra]
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC")}
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    if world == 1:
+        cmd = [sys.executable, script] + sargs
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script] + sargs
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    wall = time.perf_counter() - t0
+    times = [float(x) for x in re.findall(r"Total cost time:([0-9.eE+-]+) ms", r.stdout)]
+    accs = re.findall(r"Accuracy: (\d+)/(\d+)", r.stdout)
+    out = {"cmd": " ".join(["python"] + cmd[1:]).replace(ROOT + "/", ""), "rc": r.returncode,
+           "total_cost_time_s": round(max(times), 3) if times else None, "ranks_reporting": len(times),
+           "child_wall_s": round(wall, 2),
+           "test_acc": round(int(accs[-1][0]) / int(accs[-1][1]), 4) if accs else None}
+    if r.returncode != 0 or len(times) != world:
+        out["stderr_tail"] = r.stderr[-1500:]
+    return out
+
+
+def cpu_bench(steps: int, warmup: int, batch: int = 64) -> int:
+    """Reference config 1 (mnist.py --no-cuda, batch 64): the module engine's fp32 CPU train step."""
+    import torch.nn.functional as F
+    from pytorch_mnist_ddp_amd.optim import Adadelta
+    torch.manual_seed(1)
+    net = Net()
+    opt = Adadelta(net.parameters(), lr=1.0)
+    train = load_mnist(train=True, synthetic_data=True, verbose=False)
+    x_all = ((train.images[: (warmup + steps) * batch].float() / 255.0 - 0.1307) / 0.3081).reshape(-1, 1, 28, 28)
+    y_all = train.targets[: (warmup + steps) * batch].long()
+
+    def step(i):
+        x, y = x_all[i * batch:(i + 1) * batch], y_all[i * batch:(i + 1) * batch]
+        opt.zero_grad()
+        loss = F.nll_loss(net(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+    def timed():
+        net.train()
+        for i in range(warmup):
+            step(i)
+        t0 = time.perf_counter()
+        for i in range(warmup, warmup + steps):
+            loss = step(i)
+        return time.perf_counter() - t0, loss
+    dt, loss = timed()
+    img_s = batch * steps / dt
+    # the same loop with stock torch.optim.Adadelta on this host (the anchor was measured elsewhere)
+    torch.manual_seed(1)
+    net = Net()
+    opt = torch.optim.Adadelta(net.parameters(), lr=1.0)
+    dt_stock, _ = timed()
+    print(json.dumps({"metric": "images/sec, MNIST CNN train step on CPU (mnist.py --no-cuda config)",
+                      "value": round(img_s, 1), "unit": "images/s", "n_gpus": 0, "steps": steps, "warmup": warmup,
+                      "ms_per_step": round(1000 * dt / steps, 3), "higher_is_better": True, "scaling": "strong",
+                      "vs_baseline": round(img_s / CPU_ANCHOR_IMG_S, 3), "dtype": "fp32",
+                      "data": "synthetic 28x28 uint8 (normalised on the host); random-init weights",
+                      "config": {"model": "mnist_cnn", "global_batch": batch, "seq_len": None, "parallelism": "none",
+                                 "threads": torch.get_num_threads()},
+                      "stock_torch_img_s": round(batch * steps / dt_stock, 1),
+                      "vs_stock_torch_same_host": round(dt_stock / dt, 3),
+                      "last_train_loss": round(float(loss.item()), 4)}), flush=True)
+    return 0
 # reference README.md:55-59 (20-epoch wallclock at B=200/GPU) -> images/s = 20*60000/t
 BASELINE_WALLCLOCK = {1: 242.3, 2: 137.1, 4: 73.6}
 TRAIN_N, TEST_N, EPOCHS = 60000, 10000, 20
 
 
+def _broadcast_params(tr, comm) -> None:
+    if comm is not None:
+        tr.engine.broadcast_params(0)            # framework RCCL communicator (+ shadow refresh)
+    else:
+        broadcast_(tr.ms.param, 0)               # torch.distributed (host-staged on gloo)
+        tr.engine.refresh_shadows()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=None)
-    ap.add_argument("--steps", type=int, default=600)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 600; --cpu: 200)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default 50; --cpu: 10)")
     ap.add_argument("--batch-size", type=int, default=200, help="per-GPU batch (README config: 200)")
     ap.add_argument("--graph-steps", type=int, default=25, help="steps per captured hipGraph (0 = eager)")
     ap.add_argument("--single-bucket", action="store_true", help="one all-reduce per step (no overlap)")
@@ -64,7 +171,16 @@ def main() -> int:
     ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
                     help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernel, or "
                          "auto (time both at startup, keep the faster)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (gloo + --allreduce xgmi: no RCCL, e.g. MNIST_AMD_ONE_GPU=1 rehearsals)")
+    ap.add_argument("--cpu", action="store_true", help="reference CPU config (mnist.py --no-cuda, batch 64)")
+    ap.add_argument("--no-script-run", dest="script_run", action="store_false",
+                    help="skip the mnist_ddp.py child job (total_cost_time_s)")
     args = ap.parse_args()
+    if args.cpu:
+        return cpu_bench(200 if args.steps is None else args.steps, 10 if args.warmup is None else args.warmup)
+    args.steps = 600 if args.steps is None else args.steps
+    args.warmup = 50 if args.warmup is None else args.warmup
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -74,11 +190,14 @@ def main() -> int:
             print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run with {args.gpus} procs",
                   file=sys.stderr)
             return 2
+    if os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
+        local = 0                      # one-GPU multi-rank rehearsal (gloo + xgmi only)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
     if use_pg:
-        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank, device_id=dev)
+        kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
+        dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank, **kw)
     t_setup = time.perf_counter()
 
     B = args.batch_size
@@ -91,12 +210,14 @@ def main() -> int:
     steps_per_epoch = math.ceil(len(sampler) / B)
     num_samples = max(total * B, steps_per_epoch * B)
     ms = ModelState(net, dev, lr=1.0)
-    comm, comm2 = create_rccl_comms(world, rank, local) if use_pg else (None, None)
+    # RCCL communicators for the gradient all-reduce / its probe (none when the xGMI kernels are forced)
+    rccl = use_pg and args.allreduce != "xgmi"
+    comm, comm2 = create_rccl_comms(world, rank, local) if rccl else (None, None)
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
                       two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
-    if comm is not None:
-        tr.engine.broadcast_params(0)     # DDP construction semantics: rank-0 weights everywhere
+    if use_pg:                        # DDP construction semantics: rank-0 weights everywhere
+        _broadcast_params(tr, comm)
 
     # flat index stream = consecutive DistributedSampler epochs, full batches only
     parts, ep = [], 1
@@ -126,12 +247,20 @@ def main() -> int:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if use_pg:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(elapsed, dev)
     final_loss = float(tr.loss_log[(total - 1) % tr.loss_log.numel()].item()) if tr.loss_log.numel() else float("nan")
     img_s = world * B * args.steps / elapsed
+    # DDP correctness of the timed run: every rank must hold bitwise identical parameters
+    in_sync = True
+    if use_pg:
+        from pytorch_mnist_ddp_amd.parallel.distributed import params_fingerprint_equal
+        in_sync = params_fingerprint_equal(ms.param, dev)
+    comm_info = {"allreduce": tr.allreduce if world > 1 or comm is not None else None,
+                 "rccl_world": comm.world_size if comm is not None else None,
+                 "allreduce_probe_us": tr.allreduce_timings or None,
+                 "xgmi_validation": tr.xgmi_validation,
+                 "xgmi_grids": ({k: v for k, v in tr.xgmi.grids.items() if not k.startswith("cap")}
+                                if tr.xgmi is not None else None)}
 
     # ---- the README workload end to end: 20 epochs train + rank-0 eval, fresh model
     wall = None
@@ -145,8 +274,8 @@ def main() -> int:
         tr2 = FusedTrainer(ms2, train, test, B, 1000, num_samples=len(sampler), world_size=world, rank=rank,
                            comm=comm, seed=args.seed, graph_steps=args.graph_steps,
                            two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
-        if comm is not None:
-            tr2.engine.broadcast_params(0)
+        if use_pg:
+            _broadcast_params(tr2, comm)
         if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
@@ -167,10 +296,30 @@ def main() -> int:
             dist.barrier()
         w1 = time.perf_counter()
         wall = w1 - w0
+        wall = _max_over_ranks(wall, dev)
+
+    # ---- the reference's own metric, measured the reference's way (child job at the same N)
+    script = None
+    if args.full_run and args.script_run:
+        torch.cuda.synchronize()
         if use_pg:
-            t = torch.tensor([wall], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            wall = float(t.item())
+            dist.barrier()
+        if rank == 0:
+            try:
+                extra = []     # non-default transport choices carry over to the child job
+                if args.dist_backend != "nccl":
+                    extra += ["--dist-backend", args.dist_backend]
+                if args.allreduce != "auto":
+                    extra += ["--allreduce", args.allreduce]
+                script = run_reference_script(world, B, args.epochs, extra=extra)
+            except Exception as e:  # noqa: BLE001 - reported in the JSON
+                script = {"error": f"{type(e).__name__}: {e}"}
+        if use_pg:   # the other ranks wait on the store (host-side), leaving their GPUs to the child job
+            store = dist.distributed_c10d._get_default_store()
+            if rank == 0:
+                store.set("bench/script_done", "1")
+            else:
+                store.wait(["bench/script_done"], timedelta(seconds=1200))
 
     base = BASELINE_WALLCLOCK.get(world)
     base_img_s = (EPOCHS * TRAIN_N / base) if base else None
@@ -192,11 +341,17 @@ def main() -> int:
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
                        "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
-                       "allreduce": tr.allreduce if world > 1 or comm is not None else None,
-                       "allreduce_probe_us": tr.allreduce_timings or None},
+                       **comm_info},
+            "params_in_sync": in_sync,
+            "total_cost_time_s": script.get("total_cost_time_s") if script else None,
+            "reference_script": script,
             "wallclock_20ep_s": round(wall, 3) if wall is not None else None,
+            "wallclock_20ep_note": "in-process 20 epochs on built trainers: excludes PG init, data build, "
+                                   "model/comm setup, log syncs (total_cost_time_s is the reference's timer)",
             "baseline_wallclock_20ep_s": base,
-            "vs_baseline_wallclock": round(base / wall, 1) if (wall and base) else None,
+            "vs_baseline_wallclock": (round(base / script["total_cost_time_s"], 1)
+                                      if (base and script and script.get("total_cost_time_s")) else None),
+            "vs_baseline_wallclock_inprocess": round(base / wall, 1) if (wall and base) else None,
             "final_test_acc": round(acc, 4) if acc is not None else None,
             "last_train_loss": round(final_loss, 4),
             "setup_s": round(t0 - t_setup, 2),
@@ -205,6 +360,9 @@ def main() -> int:
     if use_pg:
         dist.barrier()
         dist.destroy_process_group()
+    if not in_sync:
+        print("bench.py: DDP desync - ranks hold different parameters after the timed steps", file=sys.stderr)
+        return 1
     return 0
 
 

@@ -14,6 +14,8 @@ behaviour):
 * ``--dtype {bf16,fp32}``: bf16 = the MI355X kernels (bf16 MFMA operands, fp32 accumulation,
   fp32 master weights / optimizer state / gradient all-reduce); fp32 = stock torch fp32 ops on
   the GPU (module engine) for exact-parity debugging.
+* ``--dist-backend``: process-group backend override (``gloo`` + ``--allreduce xgmi`` needs no
+  RCCL at all, e.g. several ranks on one GPU).
 * ``--check-sync``: all-gather a parameter checksum after every epoch (DDP desync detector).
 * ``--graph-steps``: training steps captured per HIP graph (0 = eager launches).
 * ``--profile``: roctx ranges + per-epoch device timing; ``--json-log``: machine
@@ -73,6 +75,9 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
     g.add_argument('--allreduce', choices=['auto', 'rccl', 'xgmi'], default=None,
                    help='DDP gradient all-reduce of the fused engine: RCCL, the direct xGMI kernel, or auto '
                         '(default; times both at startup and keeps the faster)')
+    g.add_argument('--dist-backend', dest='pg_backend', choices=['nccl', 'gloo'], default=None,
+                   help='torch.distributed backend for bootstrap / construction collectives (default: nccl = '
+                        'RCCL on GPU, gloo with --no-cuda); gloo + --allreduce xgmi runs DDP without RCCL')
     g.add_argument('--profile', action='store_true', default=False,
                    help='emit roctx ranges and per-epoch device timings')
     g.add_argument('--json-log', default=None, help='append per-epoch JSON metrics to this file')

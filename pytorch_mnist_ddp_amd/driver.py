@@ -13,6 +13,7 @@ Two execution engines, same flags / log lines / checkpoints / RNG consumption:
 from __future__ import annotations
 
 import json
+import os
 import sys
 import time
 
@@ -164,13 +165,19 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     ms = ModelState(model, device, lr=args.lr)
     model_for_save = model
     comm = comm2 = None
+    two_buckets = True
+    allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
     if distributed:
-        from .parallel.ddp import DistributedDataParallel
+        from .parallel.ddp import DistributedDataParallel, engine_bucket_layout
         from .parallel.distributed import create_rccl_comms
         ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
                                       bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
         model_for_save = ddp
-        comm, comm2 = create_rccl_comms(world, rank, gpu)
+        two_buckets = engine_bucket_layout(ddp.bucket_indices)   # raises on a layout the engine cannot run
+        if allreduce == "xgmi" and not two_buckets:
+            raise ValueError("--allreduce xgmi needs the two-bucket layout (default --bucket-cap-mb/--first-bucket-mb)")
+        if allreduce != "xgmi":              # xgmi-only DDP needs no RCCL communicator at all
+            comm, comm2 = create_rccl_comms(world, rank, gpu)
     # The optimizer here is the engine's fused Adadelta kernel (state in `ms`); StepLR(step_size=1)
     # (reference mnist_ddp.py:178, :189) reduces to lr <- lr * gamma after every epoch, computed in
     # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
@@ -180,7 +187,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
-                           comm2=comm2, allreduce=getattr(args, 'allreduce', None))
+                           comm2=comm2, allreduce=allreduce, two_buckets=two_buckets)
     if distributed and rank == 0 and trainer.allreduce_timings:
         print(f"| gradient all-reduce: {trainer.allreduce} (probe us/step: {trainer.allreduce_timings})", flush=True)
     trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper

@@ -120,9 +120,11 @@ class FusedTrainer:
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
         self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
         self.xgmi_validation = None
+        if allreduce == "xgmi" and not two_buckets:
+            raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
         want = allreduce == "xgmi" and (comm is not None or world_size > 1)
         probe_always = os.environ.get("MNIST_AMD_PROBE_ALWAYS", "0") == "1"   # tests: probe at world 1
-        want = want or (allreduce == "auto" and comm is not None and (world_size > 1 or probe_always))
+        want = want or (allreduce == "auto" and comm is not None and two_buckets and (world_size > 1 or probe_always))
         # Adadelta fused into the xGMI kernels (default; MNIST_AMD_XGMI_FUSE=0: separate launches).
         # Decided before the probe: only a fused schedule saves the RCCL side's separate conv update.
         self.xgmi_fuse = os.environ.get("MNIST_AMD_XGMI_FUSE", "1") != "0"
@@ -194,19 +196,23 @@ class FusedTrainer:
         """Run the exact xGMI DDP schedule the trainer will use (eager schedule-3 steps, dropout off,
         5 s stage timeouts) on scratch copies of the optimizer state before training starts; with the
         fused kernels also the separate-launch schedule, which must give the same bits.  Passes when no
-        rank timed out, fused == separate, and every rank holds the same parameters afterwards; the
-        verdict is collective (MIN over ranks).  The model state is restored either way."""
-        from ..parallel.distributed import _all_ok, params_fingerprint_equal
+        rank timed out, fused == separate, and every rank holds the same parameters afterwards.  Every
+        mode's verdict is collective (all ranks stop at the first failing mode, so no rank is left
+        waiting in kernels its peers never launch) and the message names every failing rank.  The
+        model state is restored either way."""
+        from ..parallel.distributed import gather_strings, params_fingerprint_equal
         ms, eng = self.ms, self.engine
         steps = max(1, min(steps, self.steps_per_epoch))
         keys = ("param", "square_avg", "acc_delta")
         snap = {k: getattr(ms, k).clone() for k in keys}
         idx = torch.arange(steps * self.B, dtype=torch.int64) % max(1, len(train))
         modes = [True, False] if self.xgmi_fuse else [False]
-        results, why = [], "ok"
+        results, why = [], ""
         self.xgmi.set_timeout_seconds(5.0)
-        try:
-            for fuse in modes:
+        for fuse in modes:
+            mode = "fused" if fuse else "separate"
+            t0 = time.perf_counter()
+            try:
                 with torch.no_grad():
                     for k in keys:
                         getattr(ms, k).copy_(snap[k])
@@ -218,18 +224,20 @@ class FusedTrainer:
                 eng.train_steps(steps, self.B, self.B)
                 eng.synchronize()                       # raises on a stage / hand-off timeout
                 results.append(ms.param.clone())
-            if len(results) == 2 and not torch.equal(results[0], results[1]):
-                why = "fused kernels differ from the separate launches"
-            elif not torch.isfinite(results[0]).all():
-                why = "non-finite parameters"
-        except RuntimeError as e:
-            why = str(e)
-        ok = why == "ok"
-        if ok and self.world > 1 and not params_fingerprint_equal(results[0], self.device):
-            ok, why = False, "parameters differ across ranks"
-        ok = _all_ok(ok, self.device) if self.world > 1 else ok
-        if not ok and why == "ok":
-            why = "another rank failed"
+                if not torch.isfinite(results[-1]).all():
+                    why = f"{mode}: non-finite parameters"
+            except RuntimeError as e:
+                why = f"{mode}: {e} (after {time.perf_counter() - t0:.1f} s)"
+            msgs = gather_strings(why)                  # collective: every rank stops at the same mode
+            if any(msgs):
+                why = "; ".join(f"rank {r}: {m}" for r, m in enumerate(msgs) if m)
+                break
+        if not why and len(results) == 2 and not torch.equal(results[0], results[1]):
+            why = f"rank {self.rank}: fused kernels differ from the separate launches"
+        if self.world > 1:
+            ok_fp = not why and params_fingerprint_equal(results[0], self.device)
+            msgs = gather_strings(why or ("" if ok_fp else f"rank {self.rank}: parameters differ across ranks"))
+            why = "; ".join(sorted(set(m for m in msgs if m)))
         with torch.no_grad():
             for k in keys:
                 getattr(ms, k).copy_(snap[k])
@@ -238,7 +246,9 @@ class FusedTrainer:
         eng.set_xgmi_fuse_update(self.xgmi_fuse)
         self.xgmi.set_timeout_seconds(60.0)
         torch.cuda.synchronize(self.device)
-        return ok, why if not ok else f"ok ({steps} steps, {'fused == separate' if len(modes) == 2 else 'separate'})"
+        if why:
+            return False, why
+        return True, f"ok ({steps} steps, {'fused == separate' if len(modes) == 2 else 'separate'})"
 
     def check_errors(self) -> None:
         """Raise if a device-side hand-off or xGMI stage wait timed out (the per-epoch check; a 4-byte

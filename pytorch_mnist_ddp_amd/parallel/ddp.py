@@ -49,6 +49,26 @@ def compute_bucket_assignment(sizes_bytes: list[int], caps_bytes: list[int]) -> 
     return buckets
 
 
+# Net parameter indices (registration order): conv1.w, conv1.b, conv2.w, conv2.b, fc1.w, fc1.b, fc2.w, fc2.b
+_FC_PARAMS, _CONV_PARAMS = frozenset({4, 5, 6, 7}), frozenset({0, 1, 2, 3})
+
+
+def engine_bucket_layout(bucket_indices: list[list[int]]) -> bool:
+    """Map a DDP bucket assignment of the reference ``Net`` onto the fused engine's schedules:
+    True = two buckets {fc2.*, fc1.*} then {conv2.*, conv1.*} (torch DDP's rebuilt layout at the
+    default caps), False = one bucket over every gradient (e.g. a first-bucket cap
+    >= 4.5 MiB).  Any other layout raises: the engine's buckets are fixed kernels, so a layout it
+    cannot run is refused instead of silently ignored (``--engine module`` runs any layout)."""
+    sets = [frozenset(b) for b in bucket_indices]
+    if sets == [_FC_PARAMS, _CONV_PARAMS]:
+        return True
+    if sets == [_FC_PARAMS | _CONV_PARAMS]:
+        return False
+    raise ValueError(f"the fused engine runs the DDP bucket layouts {{fc}},{{conv}} (default caps) and a single "
+                     f"bucket; --bucket-cap-mb/--first-bucket-mb give {[sorted(b) for b in bucket_indices]} "
+                     f"(parameter indices) - use --engine module for arbitrary buckets")
+
+
 class BucketReducer:
     def __init__(self, params: list[torch.Tensor], buckets: list[list[int]], world_size: int,
                  process_group=None, comm=None):
@@ -245,7 +265,12 @@ class DistributedDataParallel(nn.Module):
             return
         flat = torch.cat([t.reshape(-1) for t in tensors])
         src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
-        dist.broadcast(flat, src=src, group=self.process_group)
+        if flat.is_cuda and dist.get_backend(self.process_group) != "nccl":
+            host = flat.cpu()                    # gloo bootstrap on GPU ranks: stage through the host
+            dist.broadcast(host, src=src, group=self.process_group)
+            flat.copy_(host)
+        else:
+            dist.broadcast(flat, src=src, group=self.process_group)
         o = 0
         for t in tensors:
             t.copy_(flat[o:o + t.numel()].view_as(t))

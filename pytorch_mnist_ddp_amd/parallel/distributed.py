@@ -41,16 +41,18 @@ def init_distributed_mode(args) -> None:
         return
 
     args.distributed = True
+    if use_cuda and os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
+        args.gpu = 0        # rehearsal knob: every rank on GPU 0 (needs --dist-backend gloo --allreduce xgmi)
     if use_cuda:
         torch.cuda.set_device(args.gpu)
-        args.dist_backend = "nccl"
+        args.dist_backend = getattr(args, "pg_backend", None) or "nccl"
     else:
         args.dist_backend = "gloo"
     print(f"| distributed init (rank {args.rank}): {args.dist_url}, local rank:{args.gpu}, "
           f"world size:{args.world_size}", flush=True)
     kwargs = dict(backend=args.dist_backend, init_method=args.dist_url, world_size=args.world_size,
                   rank=args.rank, timeout=timedelta(minutes=10))
-    if use_cuda:
+    if use_cuda and args.dist_backend == "nccl":
         kwargs["device_id"] = torch.device("cuda", args.gpu)
     dist.init_process_group(**kwargs)
 
@@ -120,6 +122,28 @@ def params_fingerprint_equal(t: torch.Tensor, device) -> bool:
     allv = [torch.zeros_like(fp) for _ in range(dist.get_world_size())]
     dist.all_gather(allv, fp)
     return all(torch.equal(v, allv[0]) for v in allv)
+
+
+def gather_strings(msg: str) -> list[str]:
+    """Every rank's ``msg`` in rank order (collective)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [msg]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, msg)
+    return [str(m) for m in out]
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> None:
+    """In-place broadcast of a (device) tensor over the default process group; GPU tensors are
+    staged through the host when the backend is gloo."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    if t.is_cuda and dist.get_backend() != "nccl":
+        host = t.cpu()
+        dist.broadcast(host, src=src)
+        t.copy_(host)
+    else:
+        dist.broadcast(t, src=src)
 
 
 def _device_identity(device) -> str:

@@ -1,0 +1,87 @@
+"""T3 rehearsal of the multi-GPU DDP path on ONE MI355X (several ranks share GPU 0; gloo process
+group for bootstrap, the direct xGMI all-reduce kernels for the gradients - RCCL cannot put two ranks
+on one GPU, so these runs need none):
+
+* W ranks on disjoint shards == the world-1 engine on the concatenated batch (tools/ddp_equivalence.py);
+* ``mnist_ddp.py`` end to end at world 2 on the fused engine: rank-0-only train / test lines, the
+  ``world * batch_idx * len(data)`` sample counter, ``module.``-prefixed checkpoint, ``--check-sync``,
+  a ``Total cost time`` line per rank (reference mnist_ddp.py:74-79, :161-203);
+* ``bench.py --gpus 2`` under torchrun: the JSON proves correctness, not just speed (params_in_sync,
+  the all-reduce used, the reference-script total_cost_time_s)."""
+import json
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(**kw):
+    return dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_ONE_GPU="1", **kw)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_matches_world1_large_batch(cuda_device, world):
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "ddp_equivalence.py"), "--world", str(world),
+           "--same-device", "--steps", "10", "--timeout", "200"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, env=_env())
+    print(r.stdout[-2000:])
+    assert r.returncode == 0 and "DDP_EQUIVALENCE PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+
+
+@pytest.mark.timeout(240)
+def test_mnist_ddp_world2_xgmi_without_rccl(cuda_device, tmp_path):
+    n_train, B, W = 8000, 200, 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(W),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "mnist_ddp.py"),
+           "--batch-size", str(B), "--epochs", "2", "--synthetic", "--synthetic-train-size", str(n_train),
+           "--synthetic-test-size", "1000", "--dist-backend", "gloo", "--allreduce", "xgmi", "--check-sync",
+           "--save-model"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, cwd=tmp_path, env=_env())
+    out = r.stdout
+    assert r.returncode == 0, (out[-3000:], r.stderr[-3000:])
+    # every rank prints its init line and the timer; only rank 0 prints train / test lines
+    assert len(re.findall(r"\| distributed init \(rank \d\): env://", out)) == W
+    assert len(re.findall(r"Total cost time:[0-9.]+ ms", out)) == W
+    train = re.findall(r"Train Epoch: (\d+) \[(\d+)/(\d+) \((\d+)%\)\]\tLoss: ([0-9.]+)", out)
+    steps = n_train // W // B                                   # 20 per rank per epoch
+    assert len(train) == 2 * len(range(0, steps, 10))           # rank 0 only, every 10 batches
+    assert [int(t[1]) for t in train[:2]] == [0, W * 10 * B]    # world * batch_idx * len(data)
+    assert all(int(t[2]) == n_train for t in train)
+    assert len(re.findall(r"Test set: Average loss: [0-9.]+, Accuracy: \d+/1000", out)) == 2
+    import torch
+    sd = torch.load(tmp_path / "mnist_cnn.pt", map_location="cpu", weights_only=True)
+    assert sorted(sd) == sorted("module." + k for k in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
+                                                        "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
+    assert all(v.dtype == torch.float32 for v in sd.values())
+
+
+@pytest.mark.timeout(240)
+def test_bench_world2_reports_correctness(cuda_device, tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--epochs", "2", "--dist-backend", "gloo",
+           "--allreduce", "xgmi"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, cwd=tmp_path, env=_env())
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["params_in_sync"] is True
+    assert j["config"]["allreduce"] == "xgmi" and j["config"]["rccl_world"] is None
+    assert j["config"]["xgmi_validation"].startswith("ok")
+    rs = j["reference_script"]
+    assert rs["rc"] == 0 and rs["ranks_reporting"] == 2, rs
+    assert j["total_cost_time_s"] > 0

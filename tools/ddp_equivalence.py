@@ -1,0 +1,171 @@
+"""DDP == large-batch equivalence of the fused engine.
+
+    python tools/ddp_equivalence.py --world 4 [--steps 10] [--batch 200] [--same-device]
+
+W ranks train ``--steps`` steps on disjoint B-row shards of one global index stream (step s, rank r:
+rows [s*W*B + r*B, s*W*B + (r+1)*B)) with the xGMI all-reduce (gloo process group, no RCCL;
+``--same-device`` puts every rank on GPU 0), dropout off.  Rank 0 then trains the world-1 engine on
+the concatenated W*B rows of every step.  Mean-NLL gradients averaged over W equal shards equal the
+gradient of the mean over the W*B batch, so the parameters must agree up to fp32 summation order
+(the kernels pre-scale by 1/W and reduce in a different partition) and the bf16 rounding ties that
+order flips.  Two checks: (a) the step-1 all-reduced gradient (separate-launch schedule, where it is
+materialised) against the world-1 gradient of the W*B batch, ||g_W - g_1|| / ||g_1|| <= max(1e-3,
+2 x noise) - Adadelta normalises its step, so gradient scale errors only show here; (b) parameters
+after S fused steps, ||p_W - p_1|| / ||p_1|| <= max(1e-3, 3 x noise).  The noise floors are the same
+world-1 runs with the rows of every batch permuted (shards in reverse order).
+Also checked: every rank holds bitwise identical parameters, and the loss log matches per step.
+Exit code 0 = pass.  (Reference semantics: mnist_ddp.py:161-173 - DistributedSampler shards +
+DistributedDataParallel averaging.)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import socket
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _train(torch, dev, world, rank, B, steps, rows, allreduce, fuse=True, grads=False):
+    """Train ``steps`` steps; returns (params, loss log, averaged gradient of the last step or None).
+    ``grads``: world 1 runs the DDP schedule over a world-1 RCCL communicator (gradients land in the
+    flat grad buffer), world W the separate-launch xGMI schedule (reduced gradients in grad_out)."""
+    from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+    from pytorch_mnist_ddp_amd.engine.state import ModelState
+    from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+    from pytorch_mnist_ddp_amd.models.net import Net
+    from pytorch_mnist_ddp_amd.ops import native
+    torch.manual_seed(1)
+    ms = ModelState(Net(), dev, lr=1.0)
+    train = load_mnist(train=True, synthetic_data=True, verbose=False)
+    comm = comm2 = None
+    if grads and world == 1:
+        C = native.load()
+        comm, comm2 = (C.RcclComm(C.RcclComm.unique_id(), 1, 0, dev.index or 0) for _ in range(2))
+    os.environ["MNIST_AMD_XGMI_FUSE"] = "1" if fuse else "0"
+    try:
+        tr = FusedTrainer(ms, train, None, B, 1000, num_samples=steps * B, world_size=world, rank=rank, seed=1,
+                          graph_steps=5, dropout=False, allreduce=allreduce, comm=comm, comm2=comm2)
+    finally:
+        os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
+    if world > 1:
+        assert tr.allreduce == "xgmi", f"xGMI unavailable ({tr.xgmi_validation})"
+    tr.start_stream(rows, gather=True)
+    tr.run_steps(steps)
+    tr.synchronize()
+    g = None
+    if grads:
+        g = (tr.grad_out if world > 1 else ms.grad).clone().cpu()
+    return ms.param.clone(), tr.loss_log[:steps].clone(), g
+
+
+def worker(rank, world, port, args, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    d = 0 if args.same_device else rank % torch.cuda.device_count()
+    torch.cuda.set_device(d)
+    dev = torch.device("cuda", d)
+    dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+    try:
+        W, B, S = world, args.batch, args.steps
+        g = torch.Generator().manual_seed(123)
+        stream = torch.randperm(60000, generator=g)[: S * W * B].view(S, W, B)
+        # (a) one step, separate launches: the all-reduced gradient itself (Adadelta's normalised
+        #     update hides gradient scale errors, so compare the gradients directly)
+        _, _, gW = _train(torch, dev, W, rank, B, 1, stream[:1, rank, :].reshape(-1), "xgmi", fuse=False, grads=True)
+        # (b) S steps of the default (fused) schedule
+        p, losses, _ = _train(torch, dev, W, rank, B, S, stream[:, rank, :].reshape(-1), "xgmi")
+        allp = [torch.zeros_like(p.cpu()) for _ in range(W)]
+        dist.all_gather(allp, p.cpu())
+        same = all(torch.equal(allp[0], t) for t in allp)
+        alll = [torch.zeros_like(losses.cpu()) for _ in range(W)]
+        dist.all_gather(alll, losses.cpu())
+        msg = None
+        if rank == 0:
+            _, _, g1 = _train(torch, dev, 1, 0, W * B, 1, stream[:1].reshape(-1), "rccl", grads=True)
+            _, _, g1r = _train(torch, dev, 1, 0, W * B, 1, stream[:1].flip(1).reshape(-1), "rccl", grads=True)
+            grel = float((gW - g1).norm() / g1.norm())
+            gnoise = float((g1r - g1).norm() / g1.norm())
+            gtol = max(args.grad_tol, 2.0 * gnoise)
+            p1, l1, _ = _train(torch, dev, 1, 0, W * B, S, stream.reshape(-1), "rccl")
+            p1, l1 = p1.cpu(), l1.cpu()
+            # noise floor: the same world-1 batches with the shards in reverse order (a permutation of
+            # the rows of every batch changes nothing but fp32 summation order / bf16 tie rounding)
+            p1r, l1r, _ = _train(torch, dev, 1, 0, W * B, S, stream.flip(1).reshape(-1), "rccl")
+            p1r, l1r = p1r.cpu(), l1r.cpu()
+            rel = float((allp[0] - p1).norm() / p1.norm())
+            noise = float((p1r - p1).norm() / p1.norm())
+            mx = float((allp[0] - p1).abs().max())
+            lw = torch.stack(alll).mean(0)                     # per-step mean of the shard losses
+            lrel = float(((lw - l1).abs() / l1.abs()).max())
+            lnoise = float(((l1r - l1).abs() / l1.abs()).max())
+            tol = max(args.tol, 3.0 * noise)
+            ok = same and grel <= gtol and rel <= tol and lrel <= max(1e-3, 2.0 * lnoise)
+            msg = (f"{'PASS' if ok else 'FAIL'}: W={W} B={B} steps={S}: ranks identical={same}, "
+                   f"step-1 averaged gradient ||g_W - g_1||/||g_1|| = {grel:.2e} (noise {gnoise:.2e}, "
+                   f"tol {gtol:.2e}), "
+                   f"||p_W - p_1||/||p_1|| = {rel:.2e} (noise floor {noise:.2e}, tol {tol:.2e}), "
+                   f"max|dp| = {mx:.2e}, loss rel err {lrel:.2e} (noise {lnoise:.2e}), "
+                   f"loss {float(l1[0]):.4f} -> {float(l1[-1]):.4f}")
+            q.put((ok, msg))
+        dist.barrier()
+    except Exception as e:  # noqa: BLE001
+        q.put((False, f"rank {rank}: {type(e).__name__}: {e}"))
+        time.sleep(2.0)                       # let the other ranks report theirs
+    finally:
+        dist.destroy_process_group()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=200)
+    ap.add_argument("--tol", type=float, default=1e-3, help="parameter tolerance floor (or 3 x noise)")
+    ap.add_argument("--grad-tol", type=float, default=1e-3, help="gradient tolerance floor (or 2 x noise)")
+    ap.add_argument("--same-device", action="store_true")
+    ap.add_argument("--timeout", type=float, default=240.0)
+    args = ap.parse_args()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=worker, args=(r, args.world, port, args, q)) for r in range(args.world)]
+    for p in procs:
+        p.start()
+    deadline = time.time() + args.timeout
+    ok, msg = False, "no result"
+    msgs = []
+    while time.time() < deadline:
+        try:
+            ok, msg = q.get(timeout=1.0)
+            msgs.append(msg)
+            if ok or len(msgs) >= args.world:
+                break
+        except Exception:  # noqa: BLE001 - queue.Empty
+            if any(p.exitcode not in (None, 0) for p in procs) or (msgs and all(p.exitcode is not None for p in procs)):
+                break
+    ok = ok and len(msgs) == 1
+    msg = "\n".join(msgs) if msgs else msg
+    for p in procs:
+        p.join(timeout=max(1.0, deadline - time.time()))
+        if p.is_alive():
+            p.kill()
+    print(msg, flush=True)
+    print("DDP_EQUIVALENCE", "PASS" if ok else "FAIL", flush=True)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
