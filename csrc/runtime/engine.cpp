@@ -26,8 +26,8 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_conv_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_w_, hipEventDisableTiming));
-  HIP_OK(hipStreamCreateWithFlags(&wgrad_stream_, hipStreamNonBlocking));
-  alloc_workspace();
+  alloc_workspace();   // (the wgrad stream of the concurrent schedule is created on demand: every
+                       // stream may take a hardware queue, and queues are a shared resource)
 }
 
 Engine::~Engine() {
@@ -83,6 +83,11 @@ void Engine::alloc_workspace() {
   fcpart_ = reinterpret_cast<float*>(base + o_fp);
   sync_ = reinterpret_cast<int*>(base + o_sy);
   w1t_alt_ = reinterpret_cast<uint16_t*>(base + o_wt);
+}
+
+void Engine::set_concurrent(bool on) {
+  if (on && !wgrad_stream_) HIP_OK(hipStreamCreateWithFlags(&wgrad_stream_, hipStreamNonBlocking));
+  concurrent_ = on;
 }
 
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {

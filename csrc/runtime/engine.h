@@ -73,7 +73,7 @@ class Engine {
   // + one-shot + update in one launch).  Off = separate reduce / all-reduce / update launches.
   void set_xgmi_fuse_update(bool on) { xgmi_fuse_update_ = on; }
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
-  void set_concurrent(bool on) { concurrent_ = on; }
+  void set_concurrent(bool on);      // multi-stream single-GPU graph (creates the wgrad stream)
   // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
   // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute;
   // 2 (needs attach_comm2) = as 1, but the fc branch is joined just before the next step's fc1,

@@ -160,7 +160,8 @@ class FusedTrainer:
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)
         if uses_sched3:
-            ok = bool(self.engine.probe_stream_handoff(2.0))
+            from ..parallel.distributed import STARTUP_TIMEOUT_S
+            ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
             if world_size > 1:
                 from ..parallel.distributed import _all_ok
                 ok = _all_ok(ok, dev)
@@ -194,7 +195,7 @@ class FusedTrainer:
     # ------------------------------------------------------------------ startup validation
     def _validate_xgmi_schedule(self, train: MNISTData, steps: int = 3) -> tuple[bool, str]:
         """Run the exact xGMI DDP schedule the trainer will use (eager schedule-3 steps, dropout off,
-        5 s stage timeouts) on scratch copies of the optimizer state before training starts; with the
+        STARTUP_TIMEOUT_S stage timeouts) on scratch copies of the optimizer state before training starts; with the
         fused kernels also the separate-launch schedule, which must give the same bits.  Passes when no
         rank timed out, fused == separate, and every rank holds the same parameters afterwards.  Every
         mode's verdict is collective (all ranks stop at the first failing mode, so no rank is left
@@ -208,7 +209,8 @@ class FusedTrainer:
         idx = torch.arange(steps * self.B, dtype=torch.int64) % max(1, len(train))
         modes = [True, False] if self.xgmi_fuse else [False]
         results, why = [], ""
-        self.xgmi.set_timeout_seconds(5.0)
+        from ..parallel.distributed import STARTUP_TIMEOUT_S
+        self.xgmi.set_timeout_seconds(STARTUP_TIMEOUT_S)
         for fuse in modes:
             mode = "fused" if fuse else "separate"
             t0 = time.perf_counter()

@@ -17,6 +17,7 @@ TCPStore that ``env://`` already created, every rank joins with ``ncclCommInitRa
 from __future__ import annotations
 
 import os
+import time
 from datetime import timedelta
 
 import torch
@@ -98,6 +99,9 @@ def create_rccl_comms(world_size: int, rank: int, device: int, n: int = 2):
 
 
 _XGMI_KEY = "pytorch_mnist_ddp_amd/xgmi_record"
+# stage-wait timeout of the startup self-test / schedule validation: long enough that a peer delayed
+# by the GPU's queue scheduling (many processes on one GPU in rehearsals) is not mistaken for a hang
+STARTUP_TIMEOUT_S = float(os.environ.get("MNIST_AMD_STARTUP_TIMEOUT", "15"))
 _xgmi_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
 
 
@@ -175,7 +179,7 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
 
     Every rank exports IPC handles of its two buffers and its flag blocks through the c10d store and
     maps every peer's.  With ``verify`` each channel is then exercised on a rank-dependent pattern
-    whose sum is exact in fp32 (5 s stage timeout), and the ranks agree on the outcome.  Returns the
+    whose sum is exact in fp32 (STARTUP_TIMEOUT_S stage timeout), and the ranks agree on the outcome.  Returns the
     communicator, or ``None`` on every rank when any rank failed to map its peers or to verify
     (callers then keep the RCCL all-reduce).  ``co_ranks`` (default: measured with
     :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning workgroups are resident."""
@@ -223,7 +227,7 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
     base = torch.remainder(i, 97.0) * 0.25 - 3.0         # multiples of 1/4 in [-3, 21]: sums are exact
     s_main = torch.cuda.current_stream(grad_in.device)
     side = torch.cuda.Stream(device=grad_in.device)
-    x.set_timeout_seconds(5.0)
+    x.set_timeout_seconds(STARTUP_TIMEOUT_S)
     ok = True
     try:
         for it in range(3):                              # repeated calls exercise the per-WG counters
@@ -233,11 +237,18 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
                 grad_out.fill_(float("nan"))
             torch.cuda.synchronize(grad_in.device)
             streams = [s_main, side]
+            t0 = time.perf_counter()
             for c, (off, cnt) in enumerate(ranges):       # both channels in flight concurrently
                 x.allreduce(c, off, cnt, streams[c % 2].cuda_stream)
             torch.cuda.synchronize(grad_in.device)
+            dt = time.perf_counter() - t0
             expect = base * (scale * world * (world + 1) / 2)
-            if x.error() or not torch.equal(grad_out, expect):
+            code = x.error()
+            if code or not torch.equal(grad_out, expect):
+                from ..ops import native
+                what = (native.load().Engine.describe_xgmi_error(code) + " timed out" if code else
+                        f"{int((grad_out != expect).sum())} wrong sums")
+                print(f"[xgmi] rank {rank}: self-test call {it} failed after {dt:.2f} s: {what}", flush=True)
                 ok = False
                 break
     except RuntimeError as e:

@@ -28,7 +28,8 @@ def _port() -> int:
 
 
 def _env(**kw):
-    return dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_ONE_GPU="1", **kw)
+    # several ranks on one GPU: 2 hardware queues per process (docs/DEBUGGING.md, queue oversubscription)
+    return dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_ONE_GPU="1", GPU_MAX_HW_QUEUES="2", **kw)
 
 
 @pytest.mark.timeout(240)

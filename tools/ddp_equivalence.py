@@ -137,6 +137,11 @@ def main() -> int:
     ap.add_argument("--timeout", type=float, default=240.0)
     args = ap.parse_args()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.same_device and args.world > 1:
+        # W processes on one GPU: 2 hardware queues each keeps the total under the GPU's hardware
+        # queue slots; oversubscribed, the scheduler time-slices queues and the spinning all-reduce
+        # kernels of one rank can wait seconds for a peer's (measured W=4: 70 -> 18 us per fc call)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
