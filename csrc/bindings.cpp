@@ -263,6 +263,7 @@ PYBIND11_MODULE(_C, m) {
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)
+      .def("profile_steps", &Engine::profile_steps, py::call_guard<py::gil_scoped_release>())
       .def("gather_rows", &Engine::gather_rows, py::arg("start"), py::arg("n"))
       .def("replay", &Engine::replay, py::call_guard<py::gil_scoped_release>())
       .def("eval", &Engine::eval)

@@ -25,6 +25,7 @@
 
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../runtime/host_logic.h"
 #include "conv_grad_reduce.h"
 
 namespace mnist {
@@ -603,16 +604,6 @@ void occupancies(int* fc, int* conv, int* two, int* one) {
   *one = occ(reinterpret_cast<const void*>(&xgmi_oneshot_kernel<W>));
 }
 
-// shrink grids a (min amin, cap ca) and b so that co * (a/ca + b/cb) <= budget; returns the load
-double fit_pair(int* a, int amin, int ca, int* b, int bmin, int cb, int co, double budget) {
-  auto load = [&] { return co * ((double)*a / ca + (double)*b / cb); };
-  if (load() > budget) {
-    const double s = budget / load();
-    *a = (int)(*a * s) > amin ? (int)(*a * s) : amin;
-    *b = (int)(*b * s) > bmin ? (int)(*b * s) : bmin;
-  }
-  return load();
-}
 }  // namespace
 
 XgmiGrids xgmi_plan_grids(int world, int co_ranks, int64_t oneshot_max_floats, double budget) {
@@ -644,9 +635,9 @@ XgmiGrids xgmi_plan_grids(int world, int co_ranks, int64_t oneshot_max_floats, d
   g.conv_fused = RED_WGS;
   g.twoshot = XGMI_MAX_WG;                                       // cap: launches use min(natural, cap)
   g.oneshot = one_nat < XGMI_MAX_WG ? (one_nat > one_min ? one_nat : one_min) : XGMI_MAX_WG;
-  g.load_fused = fit_pair(&g.fc_fused, 8, g.cap_fc_fused, &g.conv_fused, CONV_FUSED_MIN_WG, g.cap_conv_fused,
+  g.load_fused = fit_grid_pair(&g.fc_fused, 8, g.cap_fc_fused, &g.conv_fused, CONV_FUSED_MIN_WG, g.cap_conv_fused,
                           co_ranks, budget);
-  g.load_separate = fit_pair(&g.twoshot, 8, g.cap_twoshot, &g.oneshot, one_min > 1 ? one_min : 1, g.cap_oneshot,
+  g.load_separate = fit_grid_pair(&g.twoshot, 8, g.cap_twoshot, &g.oneshot, one_min > 1 ? one_min : 1, g.cap_oneshot,
                              co_ranks, budget);
   if (g.load_fused > 1.0 || g.load_separate > 1.0)
     throw std::runtime_error("xgmi: the spinning all-reduce grids of " + std::to_string(co_ranks) +

@@ -1,4 +1,5 @@
 #include "engine.h"
+#include "host_logic.h"
 
 #include <stdexcept>
 #include <string>
@@ -13,7 +14,6 @@ namespace mnist {
   } while (0)
 
 namespace {
-inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 }  // namespace
 
@@ -42,47 +42,26 @@ Engine::~Engine() {
 }
 
 void Engine::alloc_workspace() {
-  // forward activations (p, fc1 partials) serve the training batch and the eval batch (which may
-  // be the whole test split in one launch); the backward-only buffers only the training batch
-  const int Ma = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
-  const int M = max_batch_;
-  const int Mp = round_up(M, 64), Map = round_up(Ma, 64);
-  const int G = conv_wgrad_groups(max_batch_);   // monotonic in B
-  int64_t off = 0;
-  auto carve = [&](int64_t bytes) { int64_t o = off; off += align256(bytes); return o; };
-  const int64_t o_a1 = carve((int64_t)M * H1 * H1 * C1 * 2);
-  const int64_t o_p = carve((int64_t)Map * NFLAT * 2);
-  const int64_t o_pm = carve((int64_t)M * NFLAT);
-  const int64_t o_z1 = carve((int64_t)FC1_KSPLIT * Ma * NH * 4);
-  const int64_t o_lr = carve((int64_t)M * 4);
-  const int64_t o_dz = carve((int64_t)Mp * NH * 2);
-  const int64_t o_h = carve((int64_t)Mp * NH * 2);
-  const int64_t o_dl = carve((int64_t)Mp * 16 * 2);
-  const int64_t o_g = carve((int64_t)M * DYC_BYTES_PER_IMAGE);   // compact dy records
-  const int64_t o_c1 = carve((int64_t)4 * M * 320 * 4);
-  const int64_t o_w2 = carve((int64_t)G * (18432 + 64) * 4);
-  const int S = fc_bwd_splits(max_batch_);
-  const int64_t o_fp = carve(S > 1 ? (int64_t)S * FCB_PART_STRIDE * 4 : 256);   // large-batch fc partials
-  const int64_t o_sy = carve(256);                                                 // schedule-3 counters
-  const int64_t o_wt = carve((int64_t)NFLAT * NH * 2);                             // alternate w1t
-  ws_bytes_ = off;
+  const WorkspaceLayout L =
+      compute_workspace_layout(max_batch_, max_test_batch_, conv_wgrad_groups(max_batch_), fc_bwd_splits(max_batch_));
+  ws_bytes_ = L.total;
   HIP_OK(hipMalloc(&ws_, ws_bytes_));
   HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
   char* base = static_cast<char*>(ws_);
-  a1_ = reinterpret_cast<uint16_t*>(base + o_a1);
-  p_ = reinterpret_cast<uint16_t*>(base + o_p);
-  pmask_ = reinterpret_cast<uint8_t*>(base + o_pm);
-  z1part_ = reinterpret_cast<float*>(base + o_z1);
-  loss_rows_ = reinterpret_cast<float*>(base + o_lr);
-  dz1_ = reinterpret_cast<uint16_t*>(base + o_dz);
-  h_bf_ = reinterpret_cast<uint16_t*>(base + o_h);
-  dl_bf_ = reinterpret_cast<uint16_t*>(base + o_dl);
-  dyc_ = reinterpret_cast<uint8_t*>(base + o_g);
-  c1part_ = reinterpret_cast<float*>(base + o_c1);
-  w2part_ = reinterpret_cast<float*>(base + o_w2);
-  fcpart_ = reinterpret_cast<float*>(base + o_fp);
-  sync_ = reinterpret_cast<int*>(base + o_sy);
-  w1t_alt_ = reinterpret_cast<uint16_t*>(base + o_wt);
+  a1_ = reinterpret_cast<uint16_t*>(base + L.a1);
+  p_ = reinterpret_cast<uint16_t*>(base + L.p);
+  pmask_ = reinterpret_cast<uint8_t*>(base + L.pmask);
+  z1part_ = reinterpret_cast<float*>(base + L.z1part);
+  loss_rows_ = reinterpret_cast<float*>(base + L.loss_rows);
+  dz1_ = reinterpret_cast<uint16_t*>(base + L.dz1);
+  h_bf_ = reinterpret_cast<uint16_t*>(base + L.h_bf);
+  dl_bf_ = reinterpret_cast<uint16_t*>(base + L.dl_bf);
+  dyc_ = reinterpret_cast<uint8_t*>(base + L.dyc);
+  c1part_ = reinterpret_cast<float*>(base + L.c1part);
+  w2part_ = reinterpret_cast<float*>(base + L.w2part);
+  fcpart_ = reinterpret_cast<float*>(base + L.fcpart);
+  sync_ = reinterpret_cast<int*>(base + L.sync);
+  w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
 }
 
 void Engine::set_concurrent(bool on) {
@@ -110,6 +89,36 @@ void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags)
   // 24 bytes as kernel arguments, ordered on the compute stream (never inside a captured graph):
   // no host sync, so the next epoch is enqueued while the previous one still runs
   launch_set_state(buf_.state, StepState{step0, flags, seed, rng_base}, compute_);
+}
+
+void Engine::phase_begin(const char* name) {
+  if (trace_) roctx_push(name);
+}
+
+void Engine::phase_end() {
+  if (!trace_) return;
+  HIP_OK(hipStreamSynchronize(compute_));
+  if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
+  roctx_pop();
+}
+
+void Engine::profile_steps(int n, int batch, int stride) {
+  if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
+  idx_stride_ = stride;
+  trace_ = true;
+  try {
+    for (int i = 0; i < n; ++i) {
+      roctx_push("train_step");
+      enqueue_step(batch, i == n - 1);
+      HIP_OK(hipStreamSynchronize(compute_));
+      roctx_pop();
+    }
+  } catch (...) {
+    trace_ = false;
+    throw;
+  }
+  trace_ = false;
+  HIP_OK(hipGetLastError());
 }
 
 void Engine::enqueue_step(int batch, bool last) {
@@ -141,6 +150,7 @@ void Engine::enqueue_step(int batch, bool last) {
     tf.wait_b = sync_ + 0;
     tf.wait_err = sync_ + 2;
   }
+  phase_begin("fwd");
   launch_trunk_fwd(tf, B, true, compute_);
   if (side_pending_) {
     if (!hold) HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
@@ -153,6 +163,7 @@ void Engine::enqueue_step(int batch, bool last) {
   ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
+  phase_end();
   const bool dist = comm_ != nullptr || xgmi_ != nullptr;   // world_size 1 + comm: DDP schedule (tests)
   // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t
   // the step started with while role A writes the updated one, so the transposed shadow alternates
@@ -166,7 +177,9 @@ void Engine::enqueue_step(int batch, bool last) {
                       w1t_in_alt_ ? buf_.w1t : w1t_alt_};
     w1t_in_alt_ = !w1t_in_alt_;
   }
+  phase_begin("bwd_fc");
   launch_fc_bwd(fb, B, Bp, compute_);
+  phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
@@ -180,7 +193,10 @@ void Engine::enqueue_step(int batch, bool last) {
     if (xgmi_) ad.grad = adc.grad = xgmi_->out();
     ConvBwdArgs cbs = cb;
     cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
+    phase_begin("bwd_conv_wgrad");
     launch_conv_wgrad(cbs, B, compute_);
+    phase_end();
+    phase_begin("allreduce_fc+update");
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
     if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
@@ -190,8 +206,12 @@ void Engine::enqueue_step(int batch, bool last) {
       launch_adadelta(ad, ADA_FC, comm_stream_);
     }
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
+    phase_end();
     side_pending_ = true;
+    phase_begin("bwd_conv_dgrad");
     launch_conv_dgrad(cb, B, compute_);
+    phase_end();
+    phase_begin("allreduce_conv+update");
     if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
       xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc);
     } else if (xgmi_) {              // separate launches (reference for the fused kernels' bits)
@@ -203,6 +223,7 @@ void Engine::enqueue_step(int batch, bool last) {
       comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
       launch_adadelta(adc, ADA_CONV, compute_);
     }
+    phase_end();
     if (last) {                                              // chunk end: one real join edge
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
@@ -267,12 +288,18 @@ void Engine::enqueue_step(int batch, bool last) {
     if (dist) comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, ms);
     launch_adadelta(ad, ADA_FC, ms);
   }
+  phase_begin("bwd_conv_wgrad");
   launch_conv_wgrad(cb, B, ws);
   if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
+  phase_end();
+  phase_begin("bwd_conv_dgrad");
   launch_conv_dgrad(cb, B, compute_);
   if (ws != compute_) HIP_OK(hipStreamWaitEvent(compute_, ev_w_, 0));
+  phase_end();
   if (one_update) {                     // single GPU: slab reduce + (conv or full) Adadelta in one launch
+    phase_begin("grad_reduce+update");
     launch_adadelta_reduce(adc, cb, B, fuse_fc, compute_);
+    phase_end();
     if (last && w1t_in_alt_) {
       HIP_OK(hipMemcpyAsync(buf_.w1t, w1t_alt_, (size_t)NFLAT * NH * sizeof(uint16_t), hipMemcpyDeviceToDevice,
                             compute_));

@@ -96,6 +96,11 @@ class Engine {
   // enqueue n steps eagerly; `stride` = full batch size (row offset of step s is s*stride)
   void train_steps(int n, int batch, int stride);
   int capture_train(int n, int batch, int stride);   // capture n steps into a graph, returns id
+  // profiling window: n eager steps, each phase (fwd, fc bwd, conv wgrad, fc all-reduce + update,
+  // conv dgrad, conv all-reduce + update) inside its own roctx range and drained before the range
+  // closes, so rocprofv3 --marker-trace attributes device time per phase (serialised: the DDP
+  // overlap is given up inside the window; results are bitwise those of the graph path)
+  void profile_steps(int n, int batch, int stride);
   void replay(int graph_id);
   // device-side DataLoader: pre-gather epoch rows [start, start+n) (needs epoch_u8/epoch_labels);
   // the step kernels then read the batch directly instead of through the index vector
@@ -138,6 +143,9 @@ class Engine {
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   bool fuse_fc_update_ = false;
+  bool trace_ = false;              // profile_steps: roctx range + drain per phase
+  void phase_begin(const char* name);
+  void phase_end();
   uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (fused fc update ping-pong)
   bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;

@@ -102,12 +102,28 @@ void RcclComm::broadcast(void* buf, int64_t count, int dtype, int root, hipStrea
   check(api().Broadcast(buf, buf, (size_t)count, dt(dtype), root, (ncclComm_t)comm_, stream), "ncclBroadcast");
 }
 
+namespace {
+// roctx entry points: the rocprofiler-sdk library (what rocprofv3 --marker-trace intercepts) first,
+// then the legacy libroctx64 (torch ships one), then whatever the process already has loaded
+void* roctx_sym(const char* name) {
+  static void* lib = [] {
+    for (const char* so : {"librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                           "libroctx64.so.4", "libroctx64.so"}) {
+      if (void* h = dlopen(so, RTLD_NOW | RTLD_GLOBAL)) return h;
+    }
+    return (void*)nullptr;
+  }();
+  void* f = lib ? dlsym(lib, name) : nullptr;
+  return f ? f : dlsym(RTLD_DEFAULT, name);
+}
+}  // namespace
+
 void roctx_push(const char* name) {
-  static roctx_push_t f = (roctx_push_t)dlsym(RTLD_DEFAULT, "roctxRangePushA");
+  static roctx_push_t f = (roctx_push_t)roctx_sym("roctxRangePushA");
   if (f) f(name);
 }
 void roctx_pop() {
-  static roctx_pop_t f = (roctx_pop_t)dlsym(RTLD_DEFAULT, "roctxRangePop");
+  static roctx_pop_t f = (roctx_pop_t)roctx_sym("roctxRangePop");
   if (f) f();
 }
 

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "../include/kernels.h"
+#include "host_logic.h"
 
 namespace mnist {
 
@@ -14,16 +15,6 @@ namespace {
 void ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi: ") + what + ": " + hipGetErrorString(e));
 }
-
-// export record of one rank: where its input / output buckets and flag blocks live
-struct Record {
-  hipIpcMemHandle_t in_h, out_h, flags_h, stage_h;
-  int64_t in_off, out_off;
-  int64_t numel, oneshot_max;
-  int32_t world, rank, channels, pid, device;
-  int32_t grid_fc, grid_conv, grid_two, grid_one;   // residency-planned grids (must agree across ranks)
-  char host[64];                 // IPC mappings only exist between the GPUs of one node
-};
 
 void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
   hipDeviceptr_t base = nullptr;
@@ -78,7 +69,7 @@ XgmiComm::~XgmiComm() {
 void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
 
 std::vector<uint8_t> XgmiComm::record() const {
-  Record r;
+  XgmiRecord r;
   memset(&r, 0, sizeof(r));
   export_ptr(in_, &r.in_h, &r.in_off);
   export_ptr(out_, &r.out_h, &r.out_off);
@@ -99,8 +90,7 @@ std::vector<uint8_t> XgmiComm::record() const {
   r.grid_two = grids_.twoshot;
   r.grid_one = grids_.oneshot;
   gethostname(r.host, sizeof(r.host) - 1);
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(&r);
-  return std::vector<uint8_t>(b, b + sizeof(r));
+  return encode_record(r);
 }
 
 void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
@@ -121,20 +111,10 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
     maps.emplace_back(h, p);
     return (char*)p;
   };
+  char host[64] = {0};
+  gethostname(host, sizeof(host) - 1);
   for (int q = 0; q < world_; ++q) {
-    if (records[q].size() != sizeof(Record)) throw std::runtime_error("xgmi: bad record size");
-    Record r;
-    memcpy(&r, records[q].data(), sizeof(r));
-    if (r.rank != q || r.world != world_ || r.numel != numel_ || r.channels != channels_ ||
-        r.oneshot_max != oneshot_max_)
-      throw std::runtime_error("xgmi: peer record does not match this communicator");
-    if (r.grid_fc != grids_.fc_fused || r.grid_conv != grids_.conv_fused || r.grid_two != grids_.twoshot ||
-        r.grid_one != grids_.oneshot)
-      throw std::runtime_error("xgmi: ranks planned different kernel grids (mixed GPUs or co_ranks?)");
-    char host[64] = {0};
-    gethostname(host, sizeof(host) - 1);
-    if (strncmp(host, r.host, sizeof(host)) != 0)
-      throw std::runtime_error("xgmi: ranks span more than one node (peer on " + std::string(r.host) + ")");
+    const XgmiRecord r = decode_record(records[q], q, world_, numel_, channels_, oneshot_max_, grids_, host);
     if (q != rank_ && r.device != device_) {
       int can = 0;
       ok(hipDeviceCanAccessPeer(&can, device_, r.device), "hipDeviceCanAccessPeer");

@@ -79,7 +79,10 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='torch.distributed backend for bootstrap / construction collectives (default: nccl = '
                         'RCCL on GPU, gloo with --no-cuda); gloo + --allreduce xgmi runs DDP without RCCL')
     g.add_argument('--profile', action='store_true', default=False,
-                   help='emit roctx ranges and per-epoch device timings')
+                   help='roctx ranges per epoch (train / eval) and, on the fused engine, a window of '
+                        '--profile-steps eager steps with one range per phase (fwd, bwd, all-reduce, update)')
+    g.add_argument('--profile-steps', type=int, default=20,
+                   help='steps in the --profile window at the start of training (default 20)')
     g.add_argument('--json-log', default=None, help='append per-epoch JSON metrics to this file')
     g.add_argument('--resume', default=None, help='load a state_dict checkpoint before training')
 

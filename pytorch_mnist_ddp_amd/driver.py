@@ -191,6 +191,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     if distributed and rank == 0 and trainer.allreduce_timings:
         print(f"| gradient all-reduce: {trainer.allreduce} (probe us/step: {trainer.allreduce_timings})", flush=True)
     trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper
+    if args.profile:
+        trainer.profile_left = args.profile_steps
     n_train = len(train_data)
     n_batches = num_batches(len(train_stream), args.batch_size)
     log_rank = (not distributed) or rank == 0
@@ -210,7 +212,9 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             st = trainer.train_epoch(epoch, idx, args.log_interval,
                                      dry_run=args.dry_run, log_fn=log_fn if log_rank else None)
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
-               "img_per_s": st.samples / max(st.train_seconds, 1e-9)}
+               "img_per_s": st.samples / max(st.train_seconds, 1e-9), "device_train_s": st.device_seconds}
+        if st.device_seconds:
+            rec["device_img_per_s"] = st.samples / st.device_seconds
         if log_rank:
             consume_loader_base_seed()      # iter(test_loader)
             if isinstance(test_stream, RandomIndexStream):

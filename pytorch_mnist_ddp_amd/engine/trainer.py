@@ -37,6 +37,7 @@ class EpochStats:
     samples: int
     train_seconds: float
     losses: dict = field(default_factory=dict)   # batch_idx -> loss for logged steps
+    device_seconds: float | None = None          # HIP-event time of the epoch's training work
 
 
 class FusedTrainer:
@@ -190,6 +191,8 @@ class FusedTrainer:
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None
+        # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)
+        self.profile_left = 0
         self.use_graphs = self.graph_steps > 0
 
     # ------------------------------------------------------------------ startup validation
@@ -273,6 +276,13 @@ class FusedTrainer:
     def _run(self, n: int, batch: int) -> None:
         if n <= 0:
             return
+        if self.profile_left > 0:        # --profile window: eager steps, one roctx range per phase
+            k = min(n, self.profile_left)
+            self.engine.profile_steps(k, batch, self.B)
+            self.profile_left -= k
+            n -= k
+            if n <= 0:
+                return
         if self.use_graphs:
             self.engine.replay(self._graph(n, batch))
         else:
@@ -304,6 +314,8 @@ class FusedTrainer:
         steps = full + (1 if last else 0)
         if dry_run:
             steps, full, last = 1, (1 if n >= self.B else 0), (0 if n >= self.B else n)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(self.compute)
         self.upload_indices(idx)
         self.engine.begin_epoch(self.seed, self.rng_base, 0, self.flags)
         self.rng_base += 2 * steps
@@ -348,13 +360,16 @@ class FusedTrainer:
             self._run(1, last)
             if log_fn is not None and full % log_interval == 0:
                 note(full, last)
+        ev1.record(self.compute)
         while pending:
             flush_one()
+        dev_s = None
         if sync:
             self.compute.synchronize()
             if self.xgmi is not None or self.comm is not None:
                 self.check_errors()        # fail at the first bad epoch, not after the last one
-        return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged)
+            dev_s = ev0.elapsed_time(ev1) / 1000.0
+        return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged, dev_s)
 
     # ------------------------------------------------------------------ raw step stream (bench)
     def start_stream(self, idx: torch.Tensor, gather: bool = True) -> None:

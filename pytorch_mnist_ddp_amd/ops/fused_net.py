@@ -10,7 +10,9 @@ backward = head_train (generic log_softmax backward from dlogp) -> fc_bwd -> con
 
 Dropout masks come from the same counter-based Philox stream as the engine: the forward draws
 a fresh (seed, offset) pair per call and the backward replays exactly that pair, so masks are
-consistent without being stored (dropout-1's keep bits are in the saved pmask anyway).
+consistent without being stored (dropout-1's keep bits are in the saved pmask anyway).  Per-batch
+activation sets are pooled per batch size (taken by the forward, returned after the backward's
+last launch, or right after an eval forward): no per-step allocation or memset.
 
 The module's parameters are re-pointed at a flat device buffer (``engine.state.ModelState``) on
 the first GPU forward; the bf16 shadow copies the kernels read are refreshed lazily whenever any
@@ -35,6 +37,16 @@ class _FusedState:
         self.versions = self._snapshot()
         self.rng_offset = 0
         self.seed = (torch.initial_seed() * _SEED_MIX) & 0xFFFFFFFFFFFFFFFF
+        self.pool: dict[tuple[int, int], list[StepBuffers]] = {}   # free sets per (batch, stream)
+
+    def take(self, B: int, device) -> StepBuffers:
+        """A per-batch activation set: reused when one is free (kernels are stream ordered on the
+        current stream, so a set released after its last launch can be refilled by the next call)."""
+        free = self.pool.get((B, native.stream_handle()))   # same stream only: ordering is the guard
+        return free.pop() if free else StepBuffers.allocate(B, device)
+
+    def give(self, buf: StepBuffers) -> None:
+        self.pool.setdefault((buf.B, native.stream_handle()), []).append(buf)
 
     def _snapshot(self):
         return tuple((p._version, p.data_ptr()) for p in self.params)
@@ -89,7 +101,7 @@ class FusedNetFunction(torch.autograd.Function):
         if x.shape[1] != 784:
             raise ValueError(f"Net expects [B,1,28,28] inputs, got {tuple(x.shape)}")
         B = x.shape[0]
-        buf = StepBuffers.allocate(B, x.device)
+        buf = st.take(B, x.device)
         state = _step_state(st, training, x.device, flags)
         s = native.stream_handle()
         P = p(ms.param)
@@ -102,7 +114,9 @@ class FusedNetFunction(torch.autograd.Function):
                    p(state), p(logp), B, bool(training), s)
         ctx.training = bool(training)
         ctx.st = st
-        ctx.buf = buf
+        ctx.buf = buf if training else None
+        if not training:
+            st.give(buf)                  # eval: nothing of the set is needed after the forward
         ctx.save_for_backward(x, state)
         return logp
 
@@ -127,6 +141,8 @@ class FusedNetFunction(torch.autograd.Function):
                  p(state), p(grad), p(buf.dyc), 0, 1.0, 1.0 / B, B, round_up(B, 32), s, part=p(buf.fcpart))
         C.conv_bwd(p(buf.dyc), p(buf.a1), p(ms.w2d), P + 4 * o["conv1.weight"], P + 4 * o["conv1.bias"],
                    0, 0, 0, p(state), p(buf.c1part), p(buf.w2part), p(grad), 1.0, B, s, xin=p(x))
+        st.give(buf)                      # last use enqueued: the next forward may refill it
+        ctx.buf = None
         views = [grad[o[n]:o[n] + t.numel()].view(t.shape) for n, t in ms.module.named_parameters()]
         return (None, None, None, None, *views)
 

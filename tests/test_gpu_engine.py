@@ -118,3 +118,44 @@ def test_stream_handoff_probe(cuda_device):
     _, ms, t = _trainer(cuda_device, graph_steps=0)
     assert t.engine.probe_stream_handoff(2.0)
     assert t.engine.probe_stream_handoff(2.0)
+
+
+def test_profile_window_bitwise_equals_graph_and_reports_device_time(cuda_device):
+    """--profile runs the first steps eagerly with one roctx range per phase (Engine.profile_steps,
+    every phase drained before its range closes); the results must be those of the graph path, and
+    the epoch reports its HIP-event device time."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(5))
+    _, ms_g, tg = _trainer(cuda_device, graph_steps=4)
+    _, ms_p, tp = _trainer(cuda_device, graph_steps=4)
+    tp.profile_left = 6
+    sg = tg.train_epoch(1, idx)
+    sp = tp.train_epoch(1, idx)
+    torch.cuda.synchronize()
+    assert tp.profile_left == 0
+    assert torch.equal(ms_g.param, ms_p.param) and torch.equal(tg.loss_log, tp.loss_log)
+    assert sg.device_seconds is not None and 0 < sg.device_seconds <= sg.train_seconds + 1e-3
+
+
+def test_module_path_reuses_step_buffers(cuda_device):
+    """Net.forward on GPU takes its activation set from a per-(batch, stream) pool: no per-step
+    allocation once warm, and results identical to a fresh allocation."""
+    from pytorch_mnist_ddp_amd.ops.fused_net import fused_state
+    import torch.nn.functional as F
+    torch.manual_seed(1)
+    net = Net().to(cuda_device)
+    x = torch.randn(32, 1, 28, 28, device=cuda_device)
+    y = torch.randint(0, 10, (32,), device=cuda_device)
+    net.eval()
+    with torch.no_grad():
+        o1 = net(x)
+        o2 = net(x)
+    assert torch.equal(o1, o2)
+    st = fused_state(net)
+    ids = {id(b) for v in st.pool.values() for b in v}
+    net.train()
+    for _ in range(3):
+        net.zero_grad(set_to_none=True)
+        F.nll_loss(net(x), y).backward()
+    torch.cuda.synchronize()
+    assert {id(b) for v in st.pool.values() for b in v} >= ids      # sets recycled, not replaced
+    assert sum(len(v) for v in st.pool.values()) == 1
