@@ -25,6 +25,48 @@ void check_launch() {
   if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
 }
 
+// ---- minimal DLPack (v0.8 ABI) export of a device fp32 vector; the capsule keeps `owner` alive
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+constexpr uint8_t kDLFloat = 2;
+
+struct DLCtx {
+  std::shared_ptr<void> owner;
+  int64_t shape[1];
+  DLManagedTensor mt;
+};
+
+void dl_deleter(DLManagedTensor* mt) { delete static_cast<DLCtx*>(mt->manager_ctx); }
+
+py::capsule dlpack_f32(float* data, int64_t n, int device, std::shared_ptr<void> owner) {
+  auto* ctx = new DLCtx{std::move(owner), {n}, {}};
+  ctx->mt.dl_tensor = DLTensor{data, DLDevice{kDLROCM, device}, 1, DLDataType{kDLFloat, 32, 1}, ctx->shape, nullptr, 0};
+  ctx->mt.manager_ctx = ctx;
+  ctx->mt.deleter = dl_deleter;
+  return py::capsule(&ctx->mt, "dltensor", [](PyObject* cap) {
+    // an unconsumed capsule still owns the tensor (a consumer renames it to "used_dltensor")
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* mt = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (mt && mt->deleter) mt->deleter(mt);
+    }
+  });
+}
+
 EngineBuffers buffers_from_dict(const py::dict& d) {
   EngineBuffers b;
   auto get = [&](const char* k) -> uintptr_t {
@@ -186,15 +228,20 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world_size", &RcclComm::world_size)
       .def_property_readonly("rank", &RcclComm::rank);
 
-  py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
-      .def(py::init([](int world, int rank, int device, uintptr_t in, uintptr_t out, int64_t numel, int channels,
-                       int64_t oneshot_max, int co_ranks, double budget) {
-             return std::make_shared<XgmiComm>(world, rank, device, P<float>(in), P<float>(out), numel, channels,
-                                               oneshot_max, co_ranks, budget);
+  py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm", py::dynamic_attr())
+      .def(py::init([](int world, int rank, int device, int64_t numel, int channels, int64_t oneshot_max,
+                       int co_ranks, double budget) {
+             return std::make_shared<XgmiComm>(world, rank, device, numel, channels, oneshot_max, co_ranks,
+                                               budget);
            }),
-           py::arg("world_size"), py::arg("rank"), py::arg("device"), py::arg("in_ptr"), py::arg("out_ptr"),
-           py::arg("numel"), py::arg("channels") = 2, py::arg("oneshot_max") = 32768, py::arg("co_ranks") = 1,
-           py::arg("budget") = 0.5)
+           py::arg("world_size"), py::arg("rank"), py::arg("device"), py::arg("numel"), py::arg("channels") = 2,
+           py::arg("oneshot_max") = 32768, py::arg("co_ranks") = 1, py::arg("budget") = 0.5)
+      // the communicator's own buffers as DLPack capsules (torch.utils.dlpack.from_dlpack): zero-copy
+      // fp32 [numel] views that keep the communicator alive
+      .def("dlpack", [](std::shared_ptr<XgmiComm> c, const std::string& which) {
+        if (which != "in" && which != "out") throw std::runtime_error("dlpack: which must be 'in' or 'out'");
+        return dlpack_f32(which == "in" ? c->in() : c->out(), c->numel(), c->device(), c);
+      })
       .def_property_readonly("grids", [](const XgmiComm& c) {
         const XgmiGrids& g = c.grids();
         py::dict d;

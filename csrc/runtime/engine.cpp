@@ -82,6 +82,10 @@ void Engine::attach_comm2(std::shared_ptr<RcclComm> comm) {
 void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
   if (x && x->world_size() != world_) throw std::runtime_error("xgmi world size mismatch");
   if (x && x->world_size() > 1 && !x->connected()) throw std::runtime_error("xgmi communicator not connected");
+  if (x && x->numel() != PARAM_TOTAL) throw std::runtime_error("xgmi communicator must cover the flat gradient");
+  if (!grad_own_) grad_own_ = buf_.grad;
+  // the gradient producers write straight into the communicator's (IPC-exported) input buffer
+  buf_.grad = x ? x->in() : grad_own_;
   xgmi_ = std::move(x);
 }
 

@@ -65,8 +65,9 @@ class Engine {
   // second communicator for the fc bucket: lets it stay in flight across the step boundary
   // (joined only before the next step's fc1) while the conv bucket reduces on the first
   void attach_comm2(std::shared_ptr<RcclComm> comm);
-  // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC over buf.grad -> x->out()) in place
-  // of the RCCL all-reduces of schedule 3; RCCL stays attached for the parameter broadcast
+  // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC over x->in() -> x->out()) in place
+  // of the RCCL all-reduces of schedule 3; while attached the gradient producers write x->in()
+  // instead of buf.grad; RCCL stays attached for the parameter broadcast
   void attach_xgmi(std::shared_ptr<XgmiComm> x);
   static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1;
   // xGMI: fold the Adadelta steps into the all-reduce kernels (fc: gather phase; conv: slab reduce
@@ -138,6 +139,7 @@ class Engine {
   int dist_sched_ = 1;
   std::shared_ptr<RcclComm> comm_, comm2_;
   std::shared_ptr<XgmiComm> xgmi_;
+  float* grad_own_ = nullptr;       // buf_.grad as given (restored when the xGMI comm is detached)
   bool xgmi_fuse_update_ = true;
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start

@@ -25,22 +25,30 @@ void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
 }
 }  // namespace
 
-XgmiComm::XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
-                   int64_t oneshot_max, int co_ranks, double budget)
-    : world_(world), rank_(rank), device_(device), channels_(channels), in_(in), out_(out), numel_(numel),
-      oneshot_max_(oneshot_max) {
+XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels, int64_t oneshot_max,
+                   int co_ranks, double budget)
+    : world_(world), rank_(rank), device_(device), channels_(channels), numel_(numel), oneshot_max_(oneshot_max) {
   // the one-shot kernel keeps <= 4 float4 per lane of <= XGMI_MAX_WG workgroups
   if (oneshot_max < 0 || oneshot_max > 4LL * 4 * 256 * XGMI_MAX_WG || (oneshot_max & 3))
     throw std::runtime_error("xgmi: bad one-shot size");
   if (world < 1 || world > XGMI_MAX_RANKS) throw std::runtime_error("xgmi: world size must be 1..8");
   if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
   if (channels < 1) throw std::runtime_error("xgmi: need at least one channel");
-  if (((uintptr_t)in | (uintptr_t)out) & 15) throw std::runtime_error("xgmi: buffers must be 16-byte aligned");
+  if (numel < 4 || (numel & 3)) throw std::runtime_error("xgmi: numel must be a positive multiple of 4");
   ok(hipSetDevice(device), "hipSetDevice");
   grids_ = xgmi_plan_grids(world, co_ranks, oneshot_max, budget);   // throws when not co-resident
+  // Every buffer a peer maps is this communicator's own hipMalloc allocation (never a block of torch's
+  // caching allocator, which hands the same segment to later tensors), and it is never returned to
+  // the allocator: a later allocation at the same address would carry an IPC handle a peer's import
+  // cache cannot tell from the old one.  Measured on one GPU: exporting caching-allocator blocks gave
+  // a second communicator in the same process stale peer mappings (wrong sums, 1 shard per peer).
+  ok(hipMalloc(&in_, sizeof(float) * numel), "hipMalloc(in)");
+  ok(hipMalloc(&out_, sizeof(float) * numel), "hipMalloc(out)");
   ok(hipMalloc(&flags_, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMalloc(flags)");
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
+  ok(hipMemset(in_, 0, sizeof(float) * numel), "hipMemset");
+  ok(hipMemset(out_, 0, sizeof(float) * numel), "hipMemset");
   ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
   ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
@@ -60,10 +68,9 @@ XgmiComm::~XgmiComm() {
   hipSetDevice(device_);
   hipDeviceSynchronize();
   for (void* p : opened_) hipIpcCloseMemHandle(p);
-  if (flags_) hipFree(flags_);
+  // in_, out_, flags_, stage_ were exported: deliberately not freed (see the constructor)
   if (ctr_) hipFree(ctr_);
   if (err_) hipFree(err_);
-  if (stage_) hipFree(stage_);
 }
 
 void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }

@@ -21,15 +21,15 @@ namespace mnist {
 
 class XgmiComm {
  public:
-  // in / out: this rank's flat input and output buffers of `numel` floats (device allocations that
-  // support IPC export: hipMalloc or blocks of torch's caching allocator)
+  // The communicator owns this rank's flat input and output buffers (`numel` floats each, in() /
+  // out(): the engine's gradient producers write in(), the optimizer reads out()).
   // Buckets of at most `oneshot_max` floats use the one-shot kernel (one hand-off per call; staging
   // slots allocated here, 2 per channel); larger ones the two-shot reduce-scatter + all-gather.
   // co_ranks: how many ranks drive this rank's GPU (1 in production; > 1 in the one-GPU multi-process
   // rehearsal) - the kernel grids are sized so every rank's spinning workgroups fit at once
   // (xgmi_plan_grids, `budget` = fraction of the GPU's workgroup slots they may take).
-  XgmiComm(int world, int rank, int device, float* in, float* out, int64_t numel, int channels,
-           int64_t oneshot_max = 32768, int co_ranks = 1, double budget = 0.5);
+  XgmiComm(int world, int rank, int device, int64_t numel, int channels, int64_t oneshot_max = 32768,
+           int co_ranks = 1, double budget = 0.5);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -57,11 +57,14 @@ class XgmiComm {
   void set_timeout_seconds(double s);
   int world_size() const { return world_; }
   int rank() const { return rank_; }
+  float* in() const { return in_; }
   float* out() const { return out_; }
+  int64_t numel() const { return numel_; }
+  int device() const { return device_; }
 
  private:
   int world_, rank_, device_, channels_;
-  float *in_, *out_;
+  float *in_ = nullptr, *out_ = nullptr;
   int64_t numel_;
   int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
   float* stage_ = nullptr;   // [channels][2][oneshot_max_], IPC exported

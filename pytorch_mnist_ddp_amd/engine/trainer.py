@@ -131,8 +131,7 @@ class FusedTrainer:
         self.xgmi_fuse = os.environ.get("MNIST_AMD_XGMI_FUSE", "1") != "0"
         if want:
             from ..parallel.distributed import choose_allreduce, create_xgmi_comm
-            self.grad_out = torch.zeros_like(mstate.grad)
-            self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad, self.grad_out)
+            self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad.numel())
             if self.xgmi is not None and allreduce == "auto":
                 split = mstate.bucket_split
                 upd = []
@@ -148,7 +147,7 @@ class FusedTrainer:
                                               int(torch.cuda.current_stream(dev).cuda_stream))]
                 with torch.cuda.stream(self.compute):
                     pick, self.allreduce_timings = choose_allreduce(
-                        comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad, self.grad_out,
+                        comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad,
                         (0, split), (split, mstate.grad.numel() - split), dev, rccl_extra=upd)
                 upd = None
                 if pick != "xgmi":
@@ -189,6 +188,9 @@ class FusedTrainer:
                 self.xgmi = None
                 self.engine.set_dist_schedule(sched if comm2 is not None else 1)
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
+        # the all-reduced gradients (xGMI: the communicator's output buffer; the inputs are written
+        # to its input buffer instead of mstate.grad while it is attached)
+        self.grad_out = self.xgmi.grad_out if self.xgmi is not None else None
         self._graphs: dict[tuple[int, int], int] = {}
         self._eval_graph: int | None = None
         # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)

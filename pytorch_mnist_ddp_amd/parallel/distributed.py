@@ -172,17 +172,20 @@ def ranks_share_a_device(device) -> bool:
     return ranks_per_device(device) > 1
 
 
-def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, grad_out: torch.Tensor,
-                     tag: str | None = None, channels: int = 2, verify: bool = True, oneshot_max: int = 32768,
-                     co_ranks: int | None = None):
-    """Direct xGMI all-reduce communicator over ``grad_in`` -> ``grad_out`` (csrc/runtime/xgmi_comm.h).
+def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 2,
+                     verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None):
+    """Direct xGMI all-reduce communicator over ``numel`` floats (csrc/runtime/xgmi_comm.h).
 
-    Every rank exports IPC handles of its two buffers and its flag blocks through the c10d store and
-    maps every peer's.  With ``verify`` each channel is then exercised on a rank-dependent pattern
-    whose sum is exact in fp32 (STARTUP_TIMEOUT_S stage timeout), and the ranks agree on the outcome.  Returns the
-    communicator, or ``None`` on every rank when any rank failed to map its peers or to verify
-    (callers then keep the RCCL all-reduce).  ``co_ranks`` (default: measured with
-    :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning workgroups are resident."""
+    The communicator owns its input / output buffers (``x.grad_in`` / ``x.grad_out``: zero-copy fp32
+    torch views through DLPack).  Every rank exports IPC handles of those buffers and its flag blocks
+    through the c10d store and maps every peer's.  With ``verify`` each channel is then exercised on a
+    rank-dependent pattern whose sum is exact in fp32 (STARTUP_TIMEOUT_S stage timeout), and the ranks
+    agree on the outcome.  Returns the communicator, or ``None`` on every rank when any rank failed
+    to map its peers or to verify (callers then keep the RCCL all-reduce).  ``co_ranks`` (default:
+    measured with :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning
+    workgroups are resident."""
+    from torch.utils.dlpack import from_dlpack
+
     from ..ops import native
     global _xgmi_seq
     C = native.load()
@@ -190,13 +193,13 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
         tag = str(_xgmi_seq)
     _xgmi_seq += 1
     dev = torch.device(device)
-    numel = grad_in.numel()
     if co_ranks is None:
         co_ranks = ranks_per_device(dev)
     x = None
     try:
-        x = C.XgmiComm(world_size, rank, dev.index or 0, native.ptr(grad_in), native.ptr(grad_out), numel, channels,
-                       oneshot_max, co_ranks)
+        x = C.XgmiComm(world_size, rank, dev.index or 0, int(numel), channels, oneshot_max, co_ranks)
+        x.grad_in = from_dlpack(x.dlpack("in"))
+        x.grad_out = from_dlpack(x.dlpack("out"))
         if world_size > 1:
             store = dist.distributed_c10d._get_default_store()
             store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
@@ -210,7 +213,7 @@ def create_xgmi_comm(world_size: int, rank: int, device, grad_in: torch.Tensor, 
     if not _all_ok(ok, dev):
         return None
     if verify:
-        ok = _verify_xgmi(x, world_size, rank, grad_in, grad_out, channels)
+        ok = _verify_xgmi(x, world_size, rank, x.grad_in, x.grad_out, channels)
         if not _all_ok(ok, dev):
             if rank == 0:
                 print("[xgmi] self-test failed: keeping the RCCL all-reduce", flush=True)
@@ -291,19 +294,20 @@ def time_bucket_allreduce(calls, device, iters: int = 20, warmup: int = 3) -> fl
     return _max_over_ranks(t0.elapsed_time(t1) * 1000.0 / iters, device)
 
 
-def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad_in: torch.Tensor, grad_out: torch.Tensor,
-                     fc_range: tuple[int, int], conv_range: tuple[int, int], device,
-                     rccl_extra=None) -> tuple[str, dict]:
+def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad: torch.Tensor, fc_range: tuple[int, int],
+                     conv_range: tuple[int, int], device, rccl_extra=None) -> tuple[str, dict]:
     """Measure one step's two bucket all-reduces with RCCL and with the direct xGMI kernel on this
     node and return the faster (``"rccl"`` / ``"xgmi"``) plus the timings - the same decision on
-    every rank (timings are maxima over ranks).  ``rccl_extra`` (zero-argument launchers) is work
+    every rank (timings are maxima over ranks).  ``grad`` is the RCCL side's flat buffer; the xGMI
+    side runs on the communicator's own buffers.  ``rccl_extra`` (zero-argument launchers) is work
     only the RCCL schedule has on its critical path - the separate conv-bucket update that the xGMI
     kernels fuse - and is timed into the RCCL side.  Buffers are zeroed afterwards."""
     from ..ops import native
     s = torch.cuda.current_stream(device).cuda_stream
-    gp = native.ptr(grad_in)
+    gp = native.ptr(grad)
     with torch.no_grad():
-        grad_in.zero_()
+        grad.zero_()
+        xgmi.grad_in.zero_()
     rc = [lambda: rccl_fc.allreduce_sum(gp + 4 * fc_range[0], fc_range[1], 0, s),
           lambda: rccl_conv.allreduce_sum(gp + 4 * conv_range[0], conv_range[1], 0, s)] + list(rccl_extra or [])
     xc = [lambda: xgmi.allreduce(1, fc_range[0], fc_range[1], s),
@@ -312,8 +316,9 @@ def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad_in: torch.Tensor, grad_out: 
     t_x = time_bucket_allreduce(xc, device)
     err = _max_over_ranks(float(xgmi.error()), device)
     with torch.no_grad():
-        grad_in.zero_()
-        grad_out.zero_()
+        grad.zero_()
+        xgmi.grad_in.zero_()
+        xgmi.grad_out.zero_()
     torch.cuda.synchronize(device)
     pick = "xgmi" if (err == 0 and t_x < t_r) else "rccl"
     return pick, {"rccl_us": round(t_r, 1), "xgmi_us": round(t_x, 1)}

@@ -42,13 +42,17 @@ def test_allreduce_auto_choice_plumbing_world1(cuda_device):
     try:
         c0, c1 = create_rccl_comms(1, 0, 0)
         n, split = 1200000, 1181120
-        gin = torch.randn(n, device=cuda_device)
-        gout = torch.randn(n, device=cuda_device)
-        x = create_xgmi_comm(1, 0, cuda_device, gin, gout)
+        g = torch.randn(n, device=cuda_device)
+        x = create_xgmi_comm(1, 0, cuda_device, n)
         assert x is not None
-        pick, t = choose_allreduce(c1, c0, x, gin, gout, (0, split), (split, n - split), cuda_device)
+        gin, gout = x.grad_in, x.grad_out
+        assert gin.shape == (n,) and gin.is_cuda and gin.data_ptr() != gout.data_ptr()
+        gin.normal_()
+        gout.normal_()
+        pick, t = choose_allreduce(c1, c0, x, g, (0, split), (split, n - split), cuda_device)
         assert pick in ("rccl", "xgmi") and t["rccl_us"] > 0 and t["xgmi_us"] > 0
-        assert int(gin.abs().sum().item()) == 0 and int(gout.abs().sum().item()) == 0
+        for b in (g, gin, gout):
+            assert int(b.abs().sum().item()) == 0
     finally:
         dist.destroy_process_group()
 

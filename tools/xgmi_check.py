@@ -60,10 +60,9 @@ def worker(rank: int, world: int, port: int, args, q) -> None:
     msgs = []
     try:
         n = FC_N + CONV_N
-        gin = torch.zeros(n, device=dev)
-        gout = torch.zeros(n, device=dev)
-        x = create_xgmi_comm(world, rank, dev, gin, gout)
+        x = create_xgmi_comm(world, rank, dev, n)
         assert x is not None, "self-test failed"
+        gin, gout = x.grad_in, x.grad_out            # the communicator's own (IPC-exported) buffers
         g = x.grids
         msgs.append(f"selftest ok (grids fc={g['fc_fused']} conv={g['conv_fused']} two={g['twoshot']} "
                     f"one={g['oneshot']}, load {g['load_fused']:.2f}/{g['load_separate']:.2f})")
