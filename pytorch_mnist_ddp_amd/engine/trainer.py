@@ -411,9 +411,16 @@ class FusedTrainer:
             self.engine.replay(self._eval_graph)
         else:
             self.engine.eval(self.n_test, self.eval_batch)
+        # per-row results to the host (40 + 40 KB) and summed there in float64: no torch reduction
+        # kernel (whose first use loads a code object inside the timed run) and a fixed order
+        rows = torch.empty(self.n_test, dtype=torch.float32, pin_memory=True)
+        hits = torch.empty(self.n_test, dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(self.compute):
+            rows.copy_(self.test_loss_rows, non_blocking=True)
+            hits.copy_(self.test_correct, non_blocking=True)
         self.compute.synchronize()
-        loss_sum = float(self.test_loss_rows.double().sum().item())
-        correct = int(self.test_correct.sum().item())
+        loss_sum = float(rows.double().sum())
+        correct = int(hits.sum())
         return loss_sum, correct, self.n_test
 
     def synchronize(self) -> None:
