@@ -38,7 +38,6 @@ import json
 import math
 import os
 import re
-import socket
 import subprocess
 import sys
 import time
@@ -65,12 +64,6 @@ _LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RA
                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
 
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 900.0, extra=()) -> dict:
     """The reference's README command at this N (mnist_ddp.py, README.md:41-51) as a child job;
     returns the max over ranks of its ``Total cost time`` print, the child's wall time and the last
@@ -82,8 +75,9 @@ def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 9
     if world == 1:
         cmd = [sys.executable, script] + sargs
     else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script] + sargs
+        # --standalone: the launcher binds its own free port (no pick-then-bind race with other jobs)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+               "--nnodes", "1", "--nproc-per-node", str(world), script] + sargs
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     wall = time.perf_counter() - t0

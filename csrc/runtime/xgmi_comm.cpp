@@ -37,14 +37,21 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   if (numel < 4 || (numel & 3)) throw std::runtime_error("xgmi: numel must be a positive multiple of 4");
   ok(hipSetDevice(device), "hipSetDevice");
   grids_ = xgmi_plan_grids(world, co_ranks, oneshot_max, budget);   // throws when not co-resident
-  // Every buffer a peer maps is this communicator's own hipMalloc allocation (never a block of torch's
-  // caching allocator, which hands the same segment to later tensors), and it is never returned to
-  // the allocator: a later allocation at the same address would carry an IPC handle a peer's import
-  // cache cannot tell from the old one.  Measured on one GPU: exporting caching-allocator blocks gave
-  // a second communicator in the same process stale peer mappings (wrong sums, 1 shard per peer).
-  ok(hipMalloc(&in_, sizeof(float) * numel), "hipMalloc(in)");
-  ok(hipMalloc(&out_, sizeof(float) * numel), "hipMalloc(out)");
-  ok(hipMalloc(&flags_, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMalloc(flags)");
+  // Every buffer a peer reads or writes is this communicator's own UNCACHED allocation
+  // (hipDeviceMallocUncached: no L2 allocation on any XCD of any GPU).  The per-XCD L2s are not
+  // coherent: with cached memory a clean line left in one XCD's L2 by an earlier plain access (a
+  // fill, the optimizer's read of the reduced bucket, a previous call's gather) is served to a later
+  // system-scope load from that XCD even after the owner rewrote the bytes write-through - observed
+  // on one GPU as whole shards of stale sums.  Uncached, every load reaches memory.  The buffers are
+  // never returned to the allocator either (never a block of torch's caching allocator): a later
+  // allocation at the same address would carry an IPC handle a peer's import cache cannot tell
+  // from the old one.
+  auto alloc = [](void** p, size_t bytes, const char* what) {
+    ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
+  };
+  alloc(reinterpret_cast<void**>(&in_), sizeof(float) * numel, "hipExtMallocWithFlags(in)");
+  alloc(reinterpret_cast<void**>(&out_), sizeof(float) * numel, "hipExtMallocWithFlags(out)");
+  alloc(reinterpret_cast<void**>(&flags_), sizeof(int) * XGMI_FLAG_INTS * channels, "hipExtMallocWithFlags(flags)");
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
   ok(hipMemset(in_, 0, sizeof(float) * numel), "hipMemset");
@@ -52,7 +59,8 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
   ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
-  ok(hipMalloc(&stage_, sizeof(float) * (2 * oneshot_max + 4) * channels), "hipMalloc(stage)");
+  alloc(reinterpret_cast<void**>(&stage_), sizeof(float) * (2 * oneshot_max + 4) * channels,
+        "hipExtMallocWithFlags(stage)");
   ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   set_timeout_seconds(60.0);
   if (world == 1) {                       // nothing to map: the kernel runs against itself

@@ -11,7 +11,6 @@ on one GPU, so these runs need none):
 import json
 import os
 import re
-import socket
 import subprocess
 import sys
 
@@ -19,12 +18,6 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-
-def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _env(**kw):
@@ -45,8 +38,8 @@ def test_ddp_matches_world1_large_batch(cuda_device, world):
 @pytest.mark.timeout(240)
 def test_mnist_ddp_world2_xgmi_without_rccl(cuda_device, tmp_path):
     n_train, B, W = 8000, 200, 2
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(W),
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "mnist_ddp.py"),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
            "--batch-size", str(B), "--epochs", "2", "--synthetic", "--synthetic-train-size", str(n_train),
            "--synthetic-test-size", "1000", "--dist-backend", "gloo", "--allreduce", "xgmi", "--check-sync",
            "--save-model"]
@@ -71,8 +64,8 @@ def test_mnist_ddp_world2_xgmi_without_rccl(cuda_device, tmp_path):
 
 @pytest.mark.timeout(240)
 def test_bench_world2_reports_correctness(cuda_device, tmp_path):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes", "1", "--nproc-per-node", "2", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "20", "--warmup", "5", "--epochs", "2", "--dist-backend", "gloo",
            "--allreduce", "xgmi"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, cwd=tmp_path, env=_env())
