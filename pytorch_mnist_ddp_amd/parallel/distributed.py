@@ -249,8 +249,21 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
             code = x.error()
             if code or not torch.equal(grad_out, expect):
                 from ..ops import native
-                what = (native.load().Engine.describe_xgmi_error(code) + " timed out" if code else
-                        f"{int((grad_out != expect).sum())} wrong sums")
+                if code:
+                    what = native.load().Engine.describe_xgmi_error(code) + " timed out"
+                else:
+                    bad = grad_out != expect
+                    what = f"{int(bad.sum())} wrong sums"
+                    # where and what: per-range/shard counts, NaN (never written) / zero / stale share
+                    for c, (off, cnt) in enumerate(ranges):
+                        b = bad[off:off + cnt]
+                        sh = (cnt // 4 + world - 1) // world * 4
+                        per = [int(b[q * sh:(q + 1) * sh].sum()) for q in range(world)]
+                        what += f"; ch{c} wrong per shard {per}"
+                    g = grad_out[bad]
+                    e = expect[bad]
+                    what += (f"; nan {int(torch.isnan(g).sum())}, zero {int((g == 0).sum())}, "
+                             f"ratio to expected (median) {float((g / e).nanmedian()):.4g}")
                 print(f"[xgmi] rank {rank}: self-test call {it} failed after {dt:.2f} s: {what}", flush=True)
                 ok = False
                 break
