@@ -49,9 +49,12 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   auto alloc = [](void** p, size_t bytes, const char* what) {
     ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
   };
-  alloc(reinterpret_cast<void**>(&in_), sizeof(float) * numel, "hipExtMallocWithFlags(in)");
-  alloc(reinterpret_cast<void**>(&out_), sizeof(float) * numel, "hipExtMallocWithFlags(out)");
-  alloc(reinterpret_cast<void**>(&flags_), sizeof(int) * XGMI_FLAG_INTS * channels, "hipExtMallocWithFlags(flags)");
+  // every exported buffer ends in a 16-byte signature {magic, rank, pid, buffer id} that peers read
+  // back through their mappings after connect() (a mapping that does not show it is refused)
+  alloc(reinterpret_cast<void**>(&in_), sizeof(float) * numel + kSigBytes, "hipExtMallocWithFlags(in)");
+  alloc(reinterpret_cast<void**>(&out_), sizeof(float) * numel + kSigBytes, "hipExtMallocWithFlags(out)");
+  alloc(reinterpret_cast<void**>(&flags_), sizeof(int) * XGMI_FLAG_INTS * channels + kSigBytes,
+        "hipExtMallocWithFlags(flags)");
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
   ok(hipMemset(in_, 0, sizeof(float) * numel), "hipMemset");
@@ -59,8 +62,12 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
   ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
-  alloc(reinterpret_cast<void**>(&stage_), sizeof(float) * (2 * oneshot_max + 4) * channels,
+  alloc(reinterpret_cast<void**>(&stage_), sizeof(float) * (2 * oneshot_max + 4) * channels + kSigBytes,
         "hipExtMallocWithFlags(stage)");
+  for (int id = 0; id < 4; ++id) {
+    const int32_t sig[4] = {kSigMagic, rank, (int32_t)getpid(), id};
+    ok(hipMemcpy(sig_ptr(id), sig, kSigBytes, hipMemcpyHostToDevice), "hipMemcpy(signature)");
+  }
   ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   set_timeout_seconds(60.0);
   if (world == 1) {                       // nothing to map: the kernel runs against itself
@@ -79,6 +86,17 @@ XgmiComm::~XgmiComm() {
   // in_, out_, flags_, stage_ were exported: deliberately not freed (see the constructor)
   if (ctr_) hipFree(ctr_);
   if (err_) hipFree(err_);
+}
+
+char* XgmiComm::sig_ptr(int id) const { return sig_at(id, in_, out_, flags_, stage_); }
+
+char* XgmiComm::sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const {
+  switch (id) {
+    case 0: return (char*)in + sizeof(float) * numel_;
+    case 1: return (char*)out + sizeof(float) * numel_;
+    case 2: return (char*)flags + sizeof(int) * XGMI_FLAG_INTS * channels_;
+    default: return (char*)stage + sizeof(float) * (2 * oneshot_max_ + 4) * channels_;
+  }
 }
 
 void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
@@ -146,6 +164,18 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
     peer_out_[q] = reinterpret_cast<float*>(open(r.out_h) + r.out_off);
     peer_flags_[q] = reinterpret_cast<int*>(open(r.flags_h));
     peer_stage_[q] = reinterpret_cast<float*>(open(r.stage_h));
+    // read every buffer's signature through the new mapping: it must be peer q's
+    static const char* names[] = {"input", "output", "flag", "staging"};
+    for (int id = 0; id < 4; ++id) {
+      int32_t sig[4] = {0, 0, 0, 0};
+      ok(hipMemcpy(sig, sig_at(id, peer_in_[q], peer_out_[q], peer_flags_[q], peer_stage_[q]), kSigBytes,
+                   hipMemcpyDeviceToHost),
+         "hipMemcpy(peer signature)");
+      if (sig[0] != kSigMagic || sig[1] != q || sig[2] != r.pid || sig[3] != id)
+        throw std::runtime_error("xgmi: the IPC mapping of rank " + std::to_string(q) + "'s " + names[id] +
+                                 " buffer does not show its signature (got rank " + std::to_string(sig[1]) +
+                                 ", pid " + std::to_string(sig[2]) + ", buffer " + std::to_string(sig[3]) + ")");
+    }
   }
   connected_ = true;
 }

@@ -80,6 +80,10 @@ class XgmiComm {
   std::vector<float*> peer_stage_;
   std::vector<void*> opened_;   // IPC mappings to close
   XgmiArgs args(int channel, int64_t offset, int64_t count) const;
+  static constexpr int kSigBytes = 16;
+  static constexpr int32_t kSigMagic = 0x58474d49;   // "XGMI"
+  char* sig_ptr(int id) const;
+  char* sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const;
 };
 
 }  // namespace mnist
