@@ -235,6 +235,10 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
     try:
         for it in range(3):                              # repeated calls exercise the per-WG counters
             scale = float(it + 1)
+            # every rank must be done READING the previous call's output shards before anyone
+            # rewrites its buffers from outside the kernel protocol (the fill below): the kernels only
+            # protect their own next call (its stage 0), not host-side writes
+            barrier()
             with torch.no_grad():
                 grad_in.copy_(base * (scale * (rank + 1)))
                 grad_out.fill_(float("nan"))
