@@ -139,7 +139,10 @@ void Engine::enqueue_step(int batch, bool last) {
   TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
   // the direct xGMI all-reduce runs in schedule 3 (its two channels = the two RCCL communicators)
-  const bool sched3 = (comm_ && comm2_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3;
+  // single GPU with overlap_fc_update_: the same device-counter schedule without a communicator (the
+  // fc Adadelta step on the comm stream under the conv backward, the conv reduce + update in one launch)
+  const bool local3 = !comm_ && !xgmi_ && overlap_fc_update_ && !concurrent_;
+  const bool sched3 = ((comm_ && comm2_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3) || local3;
   if (xgmi_ && !sched3 && !comm_) throw std::runtime_error("xgmi all-reduce needs DDP schedule 3 (or an RCCL comm)");
   if (sched3 && !side_forked_) {       // once per chunk: order the comm stream after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
@@ -206,7 +209,7 @@ void Engine::enqueue_step(int batch, bool last) {
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
       if (xgmi_) xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
-      else comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+      else if (comm2_) comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
     }
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
@@ -218,6 +221,8 @@ void Engine::enqueue_step(int batch, bool last) {
     phase_begin("allreduce_conv+update");
     if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
       xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc);
+    } else if (local3) {             // single GPU: conv slab reduce + conv Adadelta in one launch
+      launch_adadelta_reduce(adc, cb, B, true, compute_);
     } else if (xgmi_) {              // separate launches (reference for the fused kernels' bits)
       launch_conv_grad_reduce(cb, B, compute_);
       xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);

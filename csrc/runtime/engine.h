@@ -91,6 +91,9 @@ class Engine {
   // single GPU: fold the fc Adadelta step into fc_bwd (FcUpdate; bitwise equal either way, off by
   // default: measured 87.2 vs 85.9 us/step at B = 200)
   void set_fuse_fc_update(bool on) { fuse_fc_update_ = on; }
+  // single GPU: run the fc Adadelta step on the comm stream, overlapped with the conv backward, with
+  // the schedule-3 device-counter hand-offs (needs probe_stream_handoff() to pass)
+  void set_overlap_fc_update(bool on) { overlap_fc_update_ = on; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -145,6 +148,7 @@ class Engine {
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   bool fuse_fc_update_ = false;
+  bool overlap_fc_update_ = false;
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
   void phase_begin(const char* name);
   void phase_end();

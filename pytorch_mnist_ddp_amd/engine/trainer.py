@@ -100,6 +100,11 @@ class FusedTrainer:
         if fuse_fc_update is None:
             fuse_fc_update = os.environ.get("MNIST_AMD_FUSE_FC", "0") == "1"
         self.engine.set_fuse_fc_update(bool(fuse_fc_update))
+        # single GPU: fc Adadelta step overlapped with the conv backward on the comm stream
+        # (device-counter hand-offs, schedule-3 style; MNIST_AMD_OVERLAP_FC=1 to enable)
+        self.overlap_fc = (comm is None and world_size == 1 and not fuse_fc_update and not concurrent
+                           and os.environ.get("MNIST_AMD_OVERLAP_FC", "0") == "1")
+        self.engine.set_overlap_fc_update(self.overlap_fc)
         # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
         # device-counter stream hand-offs) when a second communicator is given, else 1
         # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)
@@ -156,15 +161,19 @@ class FusedTrainer:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
                 self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
-                # schedule 3 spins on one stream for the other: make sure they sit on different hardware
+        # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
-        uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3)
+        uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3) or self.overlap_fc
         if uses_sched3:
             from ..parallel.distributed import STARTUP_TIMEOUT_S
             ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
             if world_size > 1:
                 from ..parallel.distributed import _all_ok
                 ok = _all_ok(ok, dev)
+            if not ok and self.overlap_fc:
+                self.overlap_fc = False                  # single GPU: plain serial schedule instead
+                self.engine.set_overlap_fc_update(False)
+                ok = True
             if not ok and comm is None:
                 raise RuntimeError("DDP schedule 3 unusable (compute/comm streams share a hardware queue) "
                                    "and no RCCL communicator to fall back to")

@@ -159,3 +159,19 @@ def test_module_path_reuses_step_buffers(cuda_device):
     torch.cuda.synchronize()
     assert {id(b) for v in st.pool.values() for b in v} >= ids      # sets recycled, not replaced
     assert sum(len(v) for v in st.pool.values()) == 1
+
+
+def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch):
+    """MNIST_AMD_OVERLAP_FC=1: the fc Adadelta step on the comm stream (device-counter hand-offs)
+    gives the bits of the serial single-GPU schedule."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(9))
+    _, ms_s, ts = _trainer(cuda_device, graph_steps=4)
+    monkeypatch.setenv("MNIST_AMD_OVERLAP_FC", "1")
+    _, ms_o, to = _trainer(cuda_device, graph_steps=4)
+    assert to.overlap_fc
+    ts.train_epoch(1, idx)
+    to.train_epoch(1, idx)
+    to.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(ms_s.param, ms_o.param) and torch.equal(ts.loss_log, to.loss_log)
+    assert torch.equal(ms_s.w1t, ms_o.w1t) and torch.equal(ms_s.w2f, ms_o.w2f)
