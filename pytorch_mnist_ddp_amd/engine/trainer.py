@@ -101,9 +101,10 @@ class FusedTrainer:
             fuse_fc_update = os.environ.get("MNIST_AMD_FUSE_FC", "0") == "1"
         self.engine.set_fuse_fc_update(bool(fuse_fc_update))
         # single GPU: fc Adadelta step overlapped with the conv backward on the comm stream
-        # (device-counter hand-offs, schedule-3 style; MNIST_AMD_OVERLAP_FC=1 to enable)
+        # (device-counter hand-offs, schedule-3 style; default on, MNIST_AMD_OVERLAP_FC=0 to disable:
+        # measured 85.2 -> 82.7 us/step at B = 200)
         self.overlap_fc = (comm is None and world_size == 1 and not fuse_fc_update and not concurrent
-                           and os.environ.get("MNIST_AMD_OVERLAP_FC", "0") == "1")
+                           and os.environ.get("MNIST_AMD_OVERLAP_FC", "1") == "1")
         self.engine.set_overlap_fc_update(self.overlap_fc)
         # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
         # device-counter stream hand-offs) when a second communicator is given, else 1

@@ -162,10 +162,12 @@ def test_module_path_reuses_step_buffers(cuda_device):
 
 
 def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch):
-    """MNIST_AMD_OVERLAP_FC=1: the fc Adadelta step on the comm stream (device-counter hand-offs)
+    """MNIST_AMD_OVERLAP_FC (default): the fc Adadelta step on the comm stream (device-counter hand-offs)
     gives the bits of the serial single-GPU schedule."""
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(9))
+    monkeypatch.setenv("MNIST_AMD_OVERLAP_FC", "0")
     _, ms_s, ts = _trainer(cuda_device, graph_steps=4)
+    assert not ts.overlap_fc
     monkeypatch.setenv("MNIST_AMD_OVERLAP_FC", "1")
     _, ms_o, to = _trainer(cuda_device, graph_steps=4)
     assert to.overlap_fc
