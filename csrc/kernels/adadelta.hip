@@ -139,9 +139,22 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
     bid -= 1;
   }
   float* gbuf = c.grad;
+  // the update's optimizer state, loaded before (and in flight with) the slab loads
+  float pp[4], ps[4], pa[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t e = conv_sink_index(bid, threadIdx.x, r);
+    if (e >= 0) {
+      pp[r] = a.param[e];
+      ps[r] = a.square_avg[e];
+      pa[r] = a.acc_delta[e];
+    }
+  }
+  int k = 0;
   reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
     gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
-    float p = a.param[e], sq = a.square_avg[e], acc = a.acc_delta[e];
+    float p = pp[k], sq = ps[k], acc = pa[k];
+    ++k;
     ad.step(p, g, sq, acc);
     a.param[e] = p;
     a.square_avg[e] = sq;

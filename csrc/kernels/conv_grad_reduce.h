@@ -17,6 +17,30 @@ constexpr int RED_W2_WGS = (W2PART_STRIDE / 4 + 15) / 16;   // 289
 constexpr int RED_C1_WGS = 320 / 16;                         // 20
 constexpr int RED_WGS = RED_W2_WGS + RED_C1_WGS;             // 309
 
+// Flat parameter index of the r-th (0..3) value lane `tid` of reduce block `bid` hands to the sink,
+// or -1 (lanes that sink nothing, the padding column).  Shared with callers that prefetch the
+// update's optimizer state before the slab loads complete.
+__device__ __forceinline__ int64_t conv_sink_index(int bid, int tid, int r) {
+  if (bid < RED_W2_WGS) {
+    if ((tid >> 4) != 0) return -1;
+    const int col = bid * 16 + (tid & 15), e = 4 * col;
+    if (e < 18432) {
+      // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
+      const int ln = (e >> 2) & 63, tile = e >> 8;
+      const int mtile = tile / 18, ntile = tile - mtile * 18;
+      const int co0 = 16 * mtile + 4 * (ln >> 4);
+      const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
+      return (int64_t)OFF_CONV2_W + (co0 + r) * 288 + ci * 9 + tap;
+    }
+    if (e < 18432 + C2) return (int64_t)OFF_CONV2_B + (e - 18432) + r;
+    return -1;
+  }
+  if ((tid >> 2) != 0) return -1;
+  const int col = (bid - RED_W2_WGS) * 4 + (tid & 3);
+  const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
+  return kk < 9 ? (int64_t)OFF_CONV1_W + ci * 9 + kk : (int64_t)OFF_CONV1_B + ci;
+}
+
 template <class Sink>
 __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Sink&& sink) {
   const int tid = threadIdx.x;
@@ -50,21 +74,10 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
       }
       __syncthreads();
     }
-    if (sl == 0) {
-      const int e = 4 * col;
+    if (sl == 0 && 4 * col < 18432 + C2) {
       const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
-      if (e < 18432) {
-        // slab element e = ((mtile*18 + ntile)*64 + lane)*4 + r  ->  co, ci, tap
-        const int ln = (e >> 2) & 63, tile = e >> 8;
-        const int mtile = tile / 18, ntile = tile - mtile * 18;
-        const int co0 = 16 * mtile + 4 * (ln >> 4);
-        const int ci = 16 * (ntile & 1) + (ln & 15), tap = ntile >> 1;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sink((int64_t)OFF_CONV2_W + (co0 + r) * 288 + ci * 9 + tap, o[r]);
-      } else if (e < 18432 + C2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sink((int64_t)OFF_CONV2_B + (e - 18432) + r, o[r]);
-      }
+      for (int r = 0; r < 4; ++r) sink(conv_sink_index(bid, tid, r), o[r]);
     }
   } else {
     const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
@@ -95,10 +108,7 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
     if (sl == 0) {
       const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
-        sink(kk < 9 ? (int64_t)OFF_CONV1_W + ci * 9 + kk : (int64_t)OFF_CONV1_B + ci, o[r]);
-      }
+      for (int r = 0; r < 4; ++r) sink(conv_sink_index(bid, tid, r), o[r]);
     }
   }
 }

@@ -7,6 +7,7 @@
 #include "../include/kernels.h"
 
 #include <stdexcept>
+#include <stdlib.h>
 
 namespace mnist {
 
@@ -239,7 +240,7 @@ __device__ __forceinline__ void log_softmax10(const float* x, float* lp) {
 
 __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + wave;
+  const int b = blockIdx.x * (blockDim.x >> 6) + wave;
   if (b >= B) {  // padding rows of the bf16 operands consumed by the backward GEMMs
     a.dz1[(int64_t)b * NH + lane] = 0;
     a.dz1[(int64_t)b * NH + lane + 64] = 0;
@@ -343,8 +344,20 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B, train ? 1 : 0);
 }
 
+// rows (waves) per workgroup: the head is a chain of dependent latencies per row, so at small B one
+// row per workgroup spreads the rows over Bp CUs instead of packing 4 per CU (MNIST_AMD_HEAD_WAVES)
+static int head_waves() {
+  static const int w = [] {
+    const char* e = getenv("MNIST_AMD_HEAD_WAVES");
+    const int v = e ? atoi(e) : 1;
+    return (v == 1 || v == 2 || v == 4) ? v : 1;
+  }();
+  return w;
+}
+
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {
-  hipLaunchKernelGGL(head_train_kernel, dim3(Bp / 4), dim3(256), 0, s, a, B);
+  const int w = Bp >= 2048 ? 4 : head_waves();   // (Bp is a multiple of 32)
+  hipLaunchKernelGGL(head_train_kernel, dim3(Bp / w), dim3(64 * w), 0, s, a, B);
 }
 void launch_head_eval(const HeadArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(head_eval_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B);
