@@ -344,13 +344,14 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B, train ? 1 : 0);
 }
 
-// rows (waves) per workgroup: the head is a chain of dependent latencies per row, so at small B one
-// row per workgroup spreads the rows over Bp CUs instead of packing 4 per CU (MNIST_AMD_HEAD_WAVES)
+// rows (waves) per workgroup (MNIST_AMD_HEAD_WAVES, default 4).  Measured at B = 200: 1 row per
+// workgroup (224 WGs) 82.9 us/step, 2 rows 82.1, 4 rows 82.2 - spreading the rows over more CUs
+// does not pay; the head is bound by its per-row dependent latency chain.
 static int head_waves() {
   static const int w = [] {
     const char* e = getenv("MNIST_AMD_HEAD_WAVES");
-    const int v = e ? atoi(e) : 1;
-    return (v == 1 || v == 2 || v == 4) ? v : 1;
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4) ? v : 4;
   }();
   return w;
 }
