@@ -253,6 +253,7 @@ def main() -> int:
                  "rccl_world": comm.world_size if comm is not None else None,
                  "allreduce_probe_us": tr.allreduce_timings or None,
                  "xgmi_validation": tr.xgmi_validation,
+                 "conv_bucket_split": tr.conv_split,
                  "xgmi_grids": ({k: v for k, v in tr.xgmi.grids.items() if not k.startswith("cap")}
                                 if tr.xgmi is not None else None)}
 

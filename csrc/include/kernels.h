@@ -132,7 +132,7 @@ struct ConvBwdArgs {
   float grad_scale;
   int wgrad_groups;           // G
   const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
-  int* signal_ctr;            // optional: conv2_wgrad adds 1 at kernel start (schedule-3 hand-off)
+  int* signal_ctr;            // optional: conv2_wgrad / conv2_dgrad add 1 at kernel start (schedule-3 hand-offs)
 };
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad
@@ -225,6 +225,17 @@ void launch_xgmi_fc_fused(const XgmiArgs& a, hipStream_t s);
 // the engine's conv bucket [OFF_CONV1_W, PARAM_TOTAL): conv gradient slab reduce (conv_grad_reduce's
 // partition and order) + one-shot all-reduce through the staging slots + Adadelta + conv2 shadows,
 // one launch (needs a.ada; a.nvec == (PARAM_TOTAL - OFF_CONV1_W) / 4; c.grad is not written)
-void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
+// `part` selects reduce blocks [lo, hi) of conv_grad_reduce's partition (RED_W2_WGS = 289 conv2
+// blocks, then 20 conv1 blocks); the conv bucket split runs conv2 right after conv2_wgrad on the comm
+// stream and conv1 after conv2_dgrad, whose launch holds its completion until *wait_a >= *wait_b.
+constexpr int RED_W2_PARTS = 289, RED_ALL_PARTS = 309;   // = conv_grad_reduce.h RED_W2_WGS / RED_WGS
+struct XgmiConvPart {
+  int lo = 0, hi = RED_ALL_PARTS;
+  const int* wait_a = nullptr;
+  const int* wait_b = nullptr;
+  int* wait_err = nullptr;
+};
+void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s,
+                                   const XgmiConvPart& part = XgmiConvPart{});
 
 }  // namespace mnist

@@ -94,6 +94,10 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int strip = blockIdx.x, b = blockIdx.y;
+  // schedule-3 conv bucket split: dgrad's start = conv2_wgrad done (stream order), i.e. the conv2
+  // gradient slabs are final; one lane tells the comm stream (release: wgrad's writes happen-before)
+  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const int r0 = strip * DG_ROWS;
   const int nrows = (strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS;   // 7,7,7,5
   const int npix = nrows * H1;

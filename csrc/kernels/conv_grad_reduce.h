@@ -16,6 +16,7 @@ constexpr int W2PART_STRIDE = 18432 + 64;
 constexpr int RED_W2_WGS = (W2PART_STRIDE / 4 + 15) / 16;   // 289
 constexpr int RED_C1_WGS = 320 / 16;                         // 20
 constexpr int RED_WGS = RED_W2_WGS + RED_C1_WGS;             // 309
+static_assert(RED_W2_WGS == RED_W2_PARTS && RED_WGS == RED_ALL_PARTS, "kernels.h mirrors the partition");
 
 // Flat parameter index of the r-th (0..3) value lane `tid` of reduce block `bid` hands to the sink,
 // or -1 (lanes that sink nothing, the padding column).  Shared with callers that prefetch the

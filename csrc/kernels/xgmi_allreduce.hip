@@ -470,13 +470,14 @@ constexpr int CONV_SLOTS_PER_LANE = CONV_SLOTS / 256;
 }  // namespace
 
 template <int W>
-__global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a, ConvBwdArgs c, int B) {
+__global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a, ConvBwdArgs c, int B, XgmiConvPart part) {
   __shared__ float4 red[256];
   __shared__ float s_val[CONV_SLOTS];
   __shared__ int s_idx[CONV_SLOTS];
   __shared__ int s_epoch, s_err;
   const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
-  const int nvb = (RED_WGS - b + G - 1) / G;                   // <= XGMI_CONV_VB_MAX (host grid >= 39)
+  // reduce blocks [part.lo, part.hi) of conv_grad_reduce's partition, virtual block lo + b + k*G
+  const int nvb = (part.hi - part.lo - b + G - 1) / G;        // <= XGMI_CONV_VB_MAX (host-checked grid)
 #pragma unroll
   for (int k = 0; k < CONV_SLOTS_PER_LANE; ++k) s_idx[tid + 256 * k] = -1;
   if (tid == 0) {
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
   // (the reduce's first barrier orders the slot initialisation before any sink write)
   for (int k = 0; k < nvb; ++k) {
     int nv = 0;
-    reduce_conv_grads(c, B, b + k * G, red, [&](int64_t el, float v) {   // lanes 0..15, <= 4 each
+    reduce_conv_grads(c, B, part.lo + b + k * G, red, [&](int64_t el, float v) {   // lanes 0..15, <= 4 each
       const int q = k * 64 + tid * 4 + nv;
       s_idx[q] = (int)(el - a.ada_base);
       s_val[q] = v;
@@ -548,24 +549,42 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
       a.ada.w2d[(t * C1 + ci) * C2 + co] = h;
     }
   }
+  // split schedule: the conv1 launch (compute stream) completes only once the conv2 launch (comm
+  // stream) has published its update (device counters, as trunk_fwd's hold), so the next trunk_fwd,
+  // which follows it on the compute stream, reads the new conv2 weights
+  if (part.wait_a && b == 0 && tid == 0) {
+    const int target = __hip_atomic_load(part.wait_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(part.wait_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(part.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
 }
 
 namespace {
 constexpr int CONV_FUSED_MIN_WG = (RED_WGS + XGMI_CONV_VB_MAX - 1) / XGMI_CONV_VB_MAX;   // 39
 }
 
-void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
+void launch_xgmi_conv_reduce_fused(const XgmiArgs& a, const ConvBwdArgs& c, int B, hipStream_t s,
+                                   const XgmiConvPart& part) {
   static_assert(RED_WGS <= XGMI_MAX_WG, "one flag slot per reduce workgroup");
-  const dim3 g(clamp_grid(RED_WGS, CONV_FUSED_MIN_WG, a.max_wg)), blk(256);
+  const int n = part.hi - part.lo;
+  if (part.lo < 0 || part.hi > RED_WGS || n < 1) return;
+  const int lo_wg = (n + XGMI_CONV_VB_MAX - 1) / XGMI_CONV_VB_MAX;
+  const dim3 g(clamp_grid(n, lo_wg, a.max_wg)), blk(256);
   switch (a.world) {
-    case 1: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<1>, g, blk, 0, s, a, c, B); break;
-    case 2: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<2>, g, blk, 0, s, a, c, B); break;
-    case 3: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<3>, g, blk, 0, s, a, c, B); break;
-    case 4: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<4>, g, blk, 0, s, a, c, B); break;
-    case 5: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<5>, g, blk, 0, s, a, c, B); break;
-    case 6: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<6>, g, blk, 0, s, a, c, B); break;
-    case 7: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<7>, g, blk, 0, s, a, c, B); break;
-    case 8: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<8>, g, blk, 0, s, a, c, B); break;
+    case 1: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<1>, g, blk, 0, s, a, c, B, part); break;
+    case 2: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<2>, g, blk, 0, s, a, c, B, part); break;
+    case 3: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<3>, g, blk, 0, s, a, c, B, part); break;
+    case 4: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<4>, g, blk, 0, s, a, c, B, part); break;
+    case 5: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<5>, g, blk, 0, s, a, c, B, part); break;
+    case 6: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<6>, g, blk, 0, s, a, c, B, part); break;
+    case 7: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<7>, g, blk, 0, s, a, c, B, part); break;
+    case 8: hipLaunchKernelGGL(xgmi_conv_reduce_fused_kernel<8>, g, blk, 0, s, a, c, B, part); break;
     default: break;
   }
 }

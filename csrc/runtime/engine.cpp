@@ -26,6 +26,7 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_conv_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_w_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_c2_, hipEventDisableTiming));
   alloc_workspace();   // (the wgrad stream of the concurrent schedule is created on demand: every
                        // stream may take a hardware queue, and queues are a shared resource)
 }
@@ -37,6 +38,7 @@ Engine::~Engine() {
   if (ev_conv_) hipEventDestroy(ev_conv_);
   if (ev_done_) hipEventDestroy(ev_done_);
   if (ev_w_) hipEventDestroy(ev_w_);
+  if (ev_c2_) hipEventDestroy(ev_c2_);
   if (wgrad_stream_) hipStreamDestroy(wgrad_stream_);
   if (ws_) hipFree(ws_);
 }
@@ -62,6 +64,12 @@ void Engine::alloc_workspace() {
   fcpart_ = reinterpret_cast<float*>(base + L.fcpart);
   sync_ = reinterpret_cast<int*>(base + L.sync);
   w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
+}
+
+void Engine::set_conv_split(bool on, uintptr_t conv2_stream) {
+  if (on && !conv2_stream) throw std::runtime_error("conv split needs a third stream");
+  conv_split_ = on;
+  conv2_stream_ = on ? reinterpret_cast<hipStream_t>(conv2_stream) : nullptr;
 }
 
 void Engine::set_concurrent(bool on) {
@@ -103,6 +111,7 @@ void Engine::phase_end() {
   if (!trace_) return;
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
+  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
   roctx_pop();
 }
 
@@ -144,9 +153,11 @@ void Engine::enqueue_step(int batch, bool last) {
   const bool local3 = !comm_ && !xgmi_ && overlap_fc_update_ && !concurrent_;
   const bool sched3 = ((comm_ && comm2_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3) || local3;
   if (xgmi_ && !sched3 && !comm_) throw std::runtime_error("xgmi all-reduce needs DDP schedule 3 (or an RCCL comm)");
-  if (sched3 && !side_forked_) {       // once per chunk: order the comm stream after the chunk start
+  const bool split = sched3 && xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2;
+  if (sched3 && !side_forked_) {       // once per chunk: order the side streams after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    if (split) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fc_, 0));
     side_forked_ = true;
   }
   // schedule 2/3: the previous step's fc all-reduce + fc update must be done before fc1_fwd; in
@@ -215,6 +226,36 @@ void Engine::enqueue_step(int batch, bool last) {
     launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
     phase_end();
     side_pending_ = true;
+    if (split) {
+      // conv2 part: released by dgrad's start (= wgrad done), reduced / exchanged / updated on the
+      // third stream under dgrad; counters [3] conv2 updates published, [4] dgrad starts
+      AdadeltaArgs ad2 = adc;
+      ad2.state_inc = nullptr;
+      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
+      XgmiConvPart p2;
+      p2.lo = 0;
+      p2.hi = RED_W2_PARTS;
+      xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, conv2_stream_, ad2, p2);
+      launch_stream_signal(sync_ + 3, conv2_stream_);
+      ConvBwdArgs cbd = cb;
+      cbd.signal_ctr = sync_ + 4;
+      phase_begin("bwd_conv_dgrad");
+      launch_conv_dgrad(cbd, B, compute_);
+      phase_end();
+      phase_begin("allreduce_conv+update");
+      XgmiConvPart p1;
+      p1.lo = RED_W2_PARTS;
+      p1.hi = RED_ALL_PARTS;
+      p1.wait_a = sync_ + 3;
+      p1.wait_b = sync_ + 4;
+      p1.wait_err = sync_ + 2;
+      xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
+      phase_end();
+      if (last) {
+        HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
+        HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
+      }
+    } else {
     phase_begin("bwd_conv_dgrad");
     launch_conv_dgrad(cb, B, compute_);
     phase_end();
@@ -233,6 +274,7 @@ void Engine::enqueue_step(int batch, bool last) {
       launch_adadelta(adc, ADA_CONV, compute_);
     }
     phase_end();
+    }
     if (last) {                                              // chunk end: one real join edge
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
@@ -422,19 +464,27 @@ void Engine::broadcast_params(int root) {
   refresh_shadows();
 }
 
-bool Engine::probe_stream_handoff(double timeout_s) {
+bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
   // scratch counters sync_[8..11]: [8] a, [9] b, [10] zero, [11] error
-  HIP_OK(hipMemsetAsync(sync_ + 8, 0, 4 * sizeof(int), compute_));
-  HIP_OK(hipStreamSynchronize(compute_));
-  launch_stream_wait(sync_ + 8, sync_ + 10, 1, sync_ + 11, compute_, timeout_s);   // compute waits ...
-  launch_stream_signal(sync_ + 8, comm_stream_);                                     // ... for comm
-  launch_stream_wait(sync_ + 9, sync_ + 10, 1, sync_ + 11, comm_stream_, timeout_s); // comm waits ...
-  launch_stream_signal(sync_ + 9, compute_);                                          // ... for compute
-  HIP_OK(hipStreamSynchronize(compute_));
-  HIP_OK(hipStreamSynchronize(comm_stream_));
+  HIP_OK(hipMemsetAsync(sync_ + 8, 0, 4 * sizeof(int), x));
+  HIP_OK(hipStreamSynchronize(x));
+  launch_stream_wait(sync_ + 8, sync_ + 10, 1, sync_ + 11, x, timeout_s);   // x waits ...
+  launch_stream_signal(sync_ + 8, y);                                        // ... for y
+  launch_stream_wait(sync_ + 9, sync_ + 10, 1, sync_ + 11, y, timeout_s);   // y waits ...
+  launch_stream_signal(sync_ + 9, x);                                        // ... for x
+  HIP_OK(hipStreamSynchronize(x));
+  HIP_OK(hipStreamSynchronize(y));
   int err = 0;
   HIP_OK(hipMemcpy(&err, sync_ + 11, sizeof(int), hipMemcpyDeviceToHost));
   return err == 0;
+}
+
+bool Engine::probe_stream_handoff(double timeout_s) {
+  if (!probe_stream_pair(compute_, comm_stream_, timeout_s)) return false;
+  if (conv2_stream_ && (!probe_stream_pair(compute_, conv2_stream_, timeout_s) ||
+                        !probe_stream_pair(comm_stream_, conv2_stream_, timeout_s)))
+    return false;
+  return true;
 }
 
 std::pair<int, int> Engine::errors() const {
@@ -462,6 +512,7 @@ void Engine::check_errors() const {
 void Engine::synchronize() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
+  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
   if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
   check_errors();
 }

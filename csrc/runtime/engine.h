@@ -69,7 +69,13 @@ class Engine {
   // of the RCCL all-reduces of schedule 3; while attached the gradient producers write x->in()
   // instead of buf.grad; RCCL stays attached for the parameter broadcast
   void attach_xgmi(std::shared_ptr<XgmiComm> x);
-  static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1;
+  static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1, XGMI_CH_CONV2 = 2;
+  // xGMI fused schedule, conv bucket split (needs a 3-channel communicator and a third stream that
+  // passes probe_stream_handoff): conv2.weight/bias (98 % of the conv bucket, final after
+  // conv2_wgrad) are reduced, exchanged and updated on `conv2_stream` while conv2_dgrad runs; only
+  // conv1's 320 values follow dgrad on the critical path (and that launch holds its completion until
+  // the conv2 update is published, so the next trunk_fwd reads the new conv2 weights)
+  void set_conv_split(bool on, uintptr_t conv2_stream);
   // xGMI: fold the Adadelta steps into the all-reduce kernels (fc: gather phase; conv: slab reduce
   // + one-shot + update in one launch).  Off = separate reduce / all-reduce / update launches.
   void set_xgmi_fuse_update(bool on) { xgmi_fuse_update_ = on; }
@@ -88,6 +94,7 @@ class Engine {
   // GPU_MAX_HW_QUEUES).  Each stream waits (spin kernel, `timeout_s`) for a signal enqueued on the
   // other afterwards; true if both hand-offs completed.  Eager, no graph; call before training.
   bool probe_stream_handoff(double timeout_s);
+  bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   // single GPU: fold the fc Adadelta step into fc_bwd (FcUpdate; bitwise equal either way, off by
   // default: measured 87.2 vs 85.9 us/step at B = 200)
   void set_fuse_fc_update(bool on) { fuse_fc_update_ = on; }
@@ -149,6 +156,9 @@ class Engine {
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
+  bool conv_split_ = false;
+  hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
+  hipEvent_t ev_c2_ = nullptr;
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
   void phase_begin(const char* name);
   void phase_end();

@@ -214,14 +214,14 @@ void XgmiComm::allreduce_fc_fused(int channel, hipStream_t stream, const Adadelt
 }
 
 void XgmiComm::conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hipStream_t stream,
-                                 const AdadeltaArgs& ada) {
+                                 const AdadeltaArgs& ada, const XgmiConvPart& part) {
   XgmiArgs a = args(channel, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W);
   if (PARAM_TOTAL - OFF_CONV1_W > oneshot_max_) throw std::runtime_error("xgmi: conv bucket exceeds the staging slots");
   a.fuse_ada = 1;
   a.ada_base = OFF_CONV1_W;
   a.ada = ada;
   a.max_wg = grids_.conv_fused;
-  launch_xgmi_conv_reduce_fused(a, conv, B, stream);
+  launch_xgmi_conv_reduce_fused(a, conv, B, stream, part);
 }
 
 void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t stream, const AdadeltaArgs* ada) {

@@ -49,7 +49,9 @@ class XgmiComm {
   void allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada);
   // The engine's conv bucket straight from the conv gradient slabs: slab reduce + one-shot
   // all-reduce + Adadelta + conv2 shadows in one launch (launch_xgmi_conv_reduce_fused).
-  void conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hipStream_t stream, const AdadeltaArgs& ada);
+  void conv_reduce_fused(int channel, const ConvBwdArgs& conv, int B, hipStream_t stream, const AdadeltaArgs& ada,
+                         const XgmiConvPart& part = XgmiConvPart{});
+  int channels() const { return channels_; }
   // device error code (0 = ok; else the first stage wait that timed out on this rank:
   // kernel id << 24 | stage << 16 | peer << 12 | workgroup); synchronous read
   int error() const;

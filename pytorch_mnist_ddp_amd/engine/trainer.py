@@ -126,6 +126,7 @@ class FusedTrainer:
         if allreduce not in ("rccl", "xgmi", "auto"):
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
         self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
+        self.conv_split, self.conv2_stream = False, None
         self.xgmi_validation = None
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
@@ -162,15 +163,26 @@ class FusedTrainer:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
                 self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
+                # conv bucket split (fused schedule): conv2's reduce + exchange + update on a third
+                # stream under conv2_dgrad, only conv1's 320 values after dgrad (MNIST_AMD_CONV_SPLIT=0: off)
+                if self.xgmi_fuse and os.environ.get("MNIST_AMD_CONV_SPLIT", "1") != "0":
+                    self.conv2_stream = torch.cuda.Stream(device=dev)
+                    self.engine.set_conv_split(True, int(self.conv2_stream.cuda_stream))
+                    self.conv_split = True
         # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3) or self.overlap_fc
         if uses_sched3:
-            from ..parallel.distributed import STARTUP_TIMEOUT_S
+            from ..parallel.distributed import STARTUP_TIMEOUT_S, _all_ok
             ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
             if world_size > 1:
-                from ..parallel.distributed import _all_ok
                 ok = _all_ok(ok, dev)
+            if not ok and self.conv_split:               # the third stream shares a queue: no split
+                self.conv_split = False
+                self.engine.set_conv_split(False, 0)
+                ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
+                if world_size > 1:
+                    ok = _all_ok(ok, dev)
             if not ok and self.overlap_fc:
                 self.overlap_fc = False                  # single GPU: plain serial schedule instead
                 self.engine.set_overlap_fc_update(False)

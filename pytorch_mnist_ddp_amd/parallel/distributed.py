@@ -172,7 +172,7 @@ def ranks_share_a_device(device) -> bool:
     return ranks_per_device(device) > 1
 
 
-def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 2,
+def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 3,
                      verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None):
     """Direct xGMI all-reduce communicator over ``numel`` floats (csrc/runtime/xgmi_comm.h).
 
@@ -223,13 +223,16 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
 
 def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torch.Tensor, channels: int) -> bool:
     n = grad_in.numel()
-    # channel 0: a small range (one-shot kernel), channel 1: the rest (two-shot when large)
+    # channel 0: a small range (one-shot kernel), channel 1: the rest (two-shot when large), channel 2
+    # (conv-bucket split): another small range - every channel in flight concurrently
     cut = min((n // 2) & ~3, 16384)
-    ranges = [(0, cut), (cut, n - cut)] if channels >= 2 else [(0, n)]
+    ranges = [(0, cut), (cut, n - 2 * cut), (n - cut, cut)] if channels >= 3 else \
+        [(0, cut), (cut, n - cut)] if channels >= 2 else [(0, n)]
     i = torch.arange(n, device=grad_in.device, dtype=torch.float32)
     base = torch.remainder(i, 97.0) * 0.25 - 3.0         # multiples of 1/4 in [-3, 21]: sums are exact
     s_main = torch.cuda.current_stream(grad_in.device)
     side = torch.cuda.Stream(device=grad_in.device)
+    side2 = torch.cuda.Stream(device=grad_in.device)
     x.set_timeout_seconds(STARTUP_TIMEOUT_S)
     ok = True
     try:
@@ -243,10 +246,10 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
                 grad_in.copy_(base * (scale * (rank + 1)))
                 grad_out.fill_(float("nan"))
             torch.cuda.synchronize(grad_in.device)
-            streams = [s_main, side]
+            streams = [s_main, side, side2]
             t0 = time.perf_counter()
-            for c, (off, cnt) in enumerate(ranges):       # both channels in flight concurrently
-                x.allreduce(c, off, cnt, streams[c % 2].cuda_stream)
+            for c, (off, cnt) in enumerate(ranges):       # every channel in flight concurrently
+                x.allreduce(c, off, cnt, streams[c % 3].cuda_stream)
             torch.cuda.synchronize(grad_in.device)
             dt = time.perf_counter() - t0
             expect = base * (scale * world * (world + 1) / 2)

@@ -186,8 +186,8 @@ def _engine_run(torch, dist, world, rank, dev, steps):
     assert torch.isfinite(losses).all(), "non-finite loss"
     first, last = float(losses[:5].mean()), float(losses[-5:].mean())
     assert last < first, f"loss did not decrease ({first:.4f} -> {last:.4f})"
-    return p, (f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical; "
-               f"startup validation {tr.xgmi_validation})")
+    return p, (f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical; conv split "
+               f"{tr.conv_split}; startup validation {tr.xgmi_validation})")
 
 
 def main() -> int:
