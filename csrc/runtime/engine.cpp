@@ -64,6 +64,7 @@ void Engine::alloc_workspace() {
   fcpart_ = reinterpret_cast<float*>(base + L.fcpart);
   sync_ = reinterpret_cast<int*>(base + L.sync);
   w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
+  w2d_alt_ = reinterpret_cast<uint16_t*>(base + L.w2d_alt);
 }
 
 void Engine::set_conv_split(bool on, uintptr_t conv2_stream) {
@@ -228,9 +229,16 @@ void Engine::enqueue_step(int batch, bool last) {
     side_pending_ = true;
     if (split) {
       // conv2 part: released by dgrad's start (= wgrad done), reduced / exchanged / updated on the
-      // third stream under dgrad; counters [3] conv2 updates published, [4] dgrad starts
+      // third stream under dgrad; counters [3] conv2 updates published, [4] dgrad starts.  This
+      // step's dgrad reads the conv2 weights' dgrad-layout shadow while the update runs, so the
+      // update writes the OTHER copy (w2d ping-pong, host-tracked like w1t's; a chunk that ends on
+      // the alternate copy copies it back)
+      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
+      uint16_t* w2d_next = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
       AdadeltaArgs ad2 = adc;
       ad2.state_inc = nullptr;
+      ad2.w2d = w2d_next;
+      cb.w2d = w2d_cur;
       launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
       XgmiConvPart p2;
       p2.lo = 0;
@@ -251,9 +259,15 @@ void Engine::enqueue_step(int batch, bool last) {
       p1.wait_err = sync_ + 2;
       xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
       phase_end();
+      w2d_in_alt_ = !w2d_in_alt_;
       if (last) {
         HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
         HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
+        if (w2d_in_alt_) {
+          HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                                compute_));
+          w2d_in_alt_ = false;
+        }
       }
     } else {
     phase_begin("bwd_conv_dgrad");
@@ -392,6 +406,7 @@ int Engine::capture_train(int n, int batch, int stride) {
     side_pending_ = false;
     side_forked_ = false;
     w1t_in_alt_ = false;
+    w2d_in_alt_ = false;
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
     throw;

@@ -18,7 +18,7 @@ namespace mnist {
 
 // ---------------------------------------------------------------------------- engine workspace
 struct WorkspaceLayout {
-  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w1t_alt;
+  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w1t_alt, w2d_alt;
   int64_t total;   // bytes
 };
 
@@ -51,6 +51,7 @@ inline WorkspaceLayout compute_workspace_layout(int max_batch, int max_test_batc
   L.fcpart = carve(fc_splits > 1 ? (int64_t)fc_splits * FCB_PART_STRIDE * 4 : 256);   // large-batch partials
   L.sync = carve(256);                                                                // schedule-3 counters
   L.w1t_alt = carve((int64_t)NFLAT * NH * 2);                                         // alternate w1t
+  L.w2d_alt = carve((int64_t)9 * C1 * C2 * 2);                                         // alternate w2d
   L.total = off;
   return L;
 }
