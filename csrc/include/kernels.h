@@ -196,6 +196,7 @@ struct XgmiArgs {
   int64_t ada_base;
   AdadeltaArgs ada;
   int max_wg;                        // residency cap on the launch grid (XgmiGrids; every rank the same)
+  int release;                       // system-scope release fence before each stage flag store
 };
 // Every xGMI kernel's workgroup b spins until workgroup b of every peer arrives, so the workgroups
 // that can be spinning at the same moment - on one GPU: the fc-bucket kernel on the comm stream and

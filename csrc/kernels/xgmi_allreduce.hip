@@ -58,7 +58,7 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e, int kid) 
     // (vmcnt) before they are globally ordered with a later store to another memory channel; without
     // it a peer occasionally saw the flag and read whole shards of pre-call bytes (one-GPU W=4 check
     // under load).  One wave per workgroup pays it (buffer_wbl2 + wait), once per stage.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (a.release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(a.flags[p] + (stage * XGMI_MAX_RANKS + a.rank) * XGMI_MAX_WG + b, e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const int* slot = a.flags[a.rank] + (stage * XGMI_MAX_RANKS + p) * XGMI_MAX_WG + b;

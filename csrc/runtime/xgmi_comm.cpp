@@ -1,5 +1,6 @@
 #include "xgmi_comm.h"
 
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -46,8 +47,11 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   // never returned to the allocator either (never a block of torch's caching allocator): a later
   // allocation at the same address would carry an IPC handle a peer's import cache cannot tell
   // from the old one.
-  auto alloc = [](void** p, size_t bytes, const char* what) {
-    ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
+  const char* uc = getenv("MNIST_AMD_XGMI_UNCACHED");
+  const bool uncached = uc ? atoi(uc) != 0 : kUncachedDefault;
+  auto alloc = [uncached](void** p, size_t bytes, const char* what) {
+    if (uncached) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
+    else ok(hipMalloc(p, bytes), what);
   };
   // every exported buffer ends in a 16-byte signature {magic, rank, pid, buffer id} that peers read
   // back through their mappings after connect() (a mapping that does not show it is refused)
@@ -201,6 +205,11 @@ XgmiArgs XgmiComm::args(int channel, int64_t offset, int64_t count) const {
   a.nvec = count / 4;
   a.timeout_ticks = timeout_ticks_;
   a.max_wg = XGMI_MAX_WG;
+  static const int release = [] {
+    const char* e = getenv("MNIST_AMD_XGMI_RELEASE");
+    return e ? atoi(e) : 1;
+  }();
+  a.release = release;
   return a;
 }
 

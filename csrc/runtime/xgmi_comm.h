@@ -83,6 +83,7 @@ class XgmiComm {
   std::vector<void*> opened_;   // IPC mappings to close
   XgmiArgs args(int channel, int64_t offset, int64_t count) const;
   static constexpr int kSigBytes = 16;
+  static constexpr bool kUncachedDefault = true;   // MNIST_AMD_XGMI_UNCACHED overrides
   static constexpr int32_t kSigMagic = 0x58474d49;   // "XGMI"
   char* sig_ptr(int id) const;
   char* sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const;

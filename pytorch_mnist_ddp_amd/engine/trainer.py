@@ -130,7 +130,8 @@ class FusedTrainer:
         self.xgmi_validation = None
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
-        want = allreduce == "xgmi" and (comm is not None or world_size > 1)
+        import torch.distributed as _dist
+        want = allreduce == "xgmi" and (comm is not None or world_size > 1 or _dist.is_initialized())
         probe_always = os.environ.get("MNIST_AMD_PROBE_ALWAYS", "0") == "1"   # tests: probe at world 1
         want = want or (allreduce == "auto" and comm is not None and two_buckets and (world_size > 1 or probe_always))
         # Adadelta fused into the xGMI kernels (default; MNIST_AMD_XGMI_FUSE=0: separate launches).
