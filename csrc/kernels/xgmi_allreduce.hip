@@ -54,10 +54,9 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e, int kid) 
   bool ok = true;
   const int p = threadIdx.x;
   if (p < a.world) {
-    // System-scope release before the flag: the payload's write-through stores are acknowledged
-    // (vmcnt) before they are globally ordered with a later store to another memory channel; without
-    // it a peer occasionally saw the flag and read whole shards of pre-call bytes (one-GPU W=4 check
-    // under load).  One wave per workgroup pays it (buffer_wbl2 + wait), once per stage.
+    // optional system-scope release before the flag (XgmiArgs::release, MNIST_AMD_XGMI_RELEASE=1):
+    // off by default - the payload stores are write-through (sc0 sc1) into uncached buckets and
+    // drained above; the fence's L2 write-back costs ~13 us per world-1 step
     if (a.release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(a.flags[p] + (stage * XGMI_MAX_RANKS + a.rank) * XGMI_MAX_WG + b, e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
