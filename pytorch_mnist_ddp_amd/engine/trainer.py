@@ -164,9 +164,12 @@ class FusedTrainer:
                 self.engine.set_dist_schedule(3)
                 self.engine.attach_xgmi(self.xgmi)
                 self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
-                # conv bucket split (fused schedule): conv2's reduce + exchange + update on a third
-                # stream under conv2_dgrad, only conv1's 320 values after dgrad (MNIST_AMD_CONV_SPLIT=0: off)
-                if self.xgmi_fuse and os.environ.get("MNIST_AMD_CONV_SPLIT", "1") != "0":
+                # conv bucket split (fused schedule, opt-in MNIST_AMD_CONV_SPLIT=1): conv2's reduce +
+                # exchange + update on a third stream under conv2_dgrad, only conv1's 320 values after
+                # dgrad.  Bitwise equal; at world 1 it costs 1-2 us/step (88.0-89.1 vs 87.0-87.1: two
+                # more hand-off kernels and a third graph branch) and what it saves at world > 1 (the
+                # conv2 slab reduce off the critical path) is unmeasured on one GPU, so it is off.
+                if self.xgmi_fuse and os.environ.get("MNIST_AMD_CONV_SPLIT", "0") == "1":
                     self.conv2_stream = torch.cuda.Stream(device=dev)
                     self.engine.set_conv_split(True, int(self.conv2_stream.cuda_stream))
                     self.conv_split = True

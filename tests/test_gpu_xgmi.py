@@ -72,3 +72,17 @@ def test_trainer_auto_probe_path_world1(tmp_path):
         outs[name] = json.loads(r.stdout.strip().splitlines()[-1])
     assert outs["auto"]["config"]["allreduce_probe_us"]["rccl_us"] > 0
     assert outs["auto"]["last_train_loss"] == outs["rccl"]["last_train_loss"]
+
+
+@pytest.mark.timeout(200)
+def test_conv_bucket_split_bitwise_at_two_ranks(cuda_device):
+    """Opt-in conv bucket split (MNIST_AMD_CONV_SPLIT=1): the startup validation inside the engine
+    check compares it bitwise with the separate launches, at 2 ranks on one GPU (4 HW queues per
+    process: the split's third stream needs its own queue)."""
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "xgmi_check.py"), "--world", "2", "--same-device",
+           "--iters", "10", "--engine-steps", "20", "--timeout", "170"]
+    env = dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_CONV_SPLIT="1", GPU_MAX_HW_QUEUES="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=185, env=env)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "conv split True" in r.stdout
