@@ -3,8 +3,9 @@
 usage: python tools/roofline.py --stats DIR --pmc DIR1 [DIR2 ...] --batch B [--md]
 
 Per kernel: average duration, analytic FLOPs at batch B (SURVEY §2.4 GEMM views), HBM bytes
-(FETCH_SIZE + WRITE_SIZE, KB per dispatch), achieved TFLOP/s and TB/s, MFMA-busy share of the busy
-cycles, LDS bank-conflict cycles per dispatch.  Peaks priced: 2.5 PFLOP/s dense bf16, 8 TB/s HBM3E.
+(FETCH_SIZE + WRITE_SIZE, KB per dispatch), achieved TFLOP/s and TB/s, raw MFMA-busy / SQ-busy
+cycles and LDS bank-conflict cycles per dispatch (summed over the chip's counter instances).
+Peaks priced: 2.5 PFLOP/s dense bf16, 8 TB/s HBM3E.
 """
 import argparse
 import collections
@@ -57,8 +58,8 @@ def main():
                 pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in pmc.items()}
     print(f"| kernel (B={a.batch}) | calls | us | GFLOP | TFLOP/s | % bf16 peak | HBM KB | TB/s | % HBM peak "
-          f"| MFMA busy / busy | LDS bank-conflict cyc |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
+          f"| SQ_VALU_MFMA_BUSY_CYCLES | SQ_BUSY_CYCLES | LDS bank-conflict cyc |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     tot = 0.0
     for k in sorted(dur, key=lambda k: -dur[k] * (calls[k] > 10)):
         if calls[k] < 10:
@@ -72,10 +73,10 @@ def main():
         tbs = kb * 1024 / us / 1e6
         busy = p.get("SQ_BUSY_CYCLES")
         mf = p.get("SQ_VALU_MFMA_BUSY_CYCLES")
-        mfs = f"{100 * mf / busy:.1f} %" if busy and mf is not None else "-"
         lds = p.get("SQ_LDS_BANK_CONFLICT")
+        f0 = lambda v: "-" if v is None else f"{v:.0f}"
         print(f"| {k} | {calls[k]} | {us:.2f} | {fl / 1e9:.3f} | {tf:.1f} | {100 * tf / PEAK_TF:.1f} % | {kb:.0f} | "
-              f"{tbs:.2f} | {100 * tbs / PEAK_TBS:.1f} % | {mfs} | {lds if lds is None else f'{lds:.0f}'} |")
+              f"{tbs:.2f} | {100 * tbs / PEAK_TBS:.1f} % | {f0(mf)} | {f0(busy)} | {f0(lds)} |")
     print(f"\nsum of per-step kernel time: {tot:.2f} us")
 
 
