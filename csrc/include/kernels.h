@@ -102,6 +102,7 @@ struct FcBwdArgs {
   float inv_batch;
   float* part;                // B > FC_BWD_SPLIT_ROWS: [fc_bwd_splits(B)][FCB_PART_STRIDE] partial fc grads
   FcUpdate upd;               // optional fused fc Adadelta (zero-initialised = off)
+  int* signal_ctr;            // optional: the launch's first workgroup adds 1 at its start (schedule-3 hand-off)
 };
 // Large batches split the batch (= K of the fc weight gradients) over fc_bwd_splits(B) groups of
 // workgroups writing fp32 partials that fc_grad_reduce sums in fixed order; B <= 1024 writes the
@@ -115,6 +116,9 @@ constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_P
                   FCB_PART_STRIDE = (FCB_PART_LOSS + 1 + 63) / 64 * 64;
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s);   // profiling aid
+// two-stream form (B <= FC_BWD_SPLIT_ROWS): part 0 = roles C + B (dW2 / loss and the dy records the conv
+// backward needs), part 1 = role A (dW1, only the optimizer / all-reduce needs it)
+void launch_fc_bwd_part(const FcBwdArgs& a, int B, int Bp, int part, hipStream_t s);
 
 struct ConvBwdArgs {
   const uint8_t* dyc;         // compact un-pooled gradient (written by fc_bwd role B)

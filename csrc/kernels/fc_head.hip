@@ -732,19 +732,29 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
 }
 }  // namespace
 
+__host__ __device__ inline int fc_bwd_role_b_wgs(int B) {
+  const int rows16 = (B + 15) / 16, mr = fcb_mr(B);
+  return ((rows16 + mr - 1) / mr) * ROLE_B_SBLOCKS;
+}
+
+// order 0: [C | A | B] (one launch); order 1: [C | B | A] (two launches: C + B on the compute stream,
+// A on the comm stream)
 template <bool BIG>
-__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
+__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0, int order) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
+  if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const int bid = blockIdx.x + bid0;
   const int S = fc_bwd_splits(B);
+  const int nA = S * ROLE_A_WGS, nB = fc_bwd_role_b_wgs(B);
   // role C (long-running, one per split) first so it is dispatched before the short role-B tiles
   if (bid < S) {
     fc_bwd_role_c(a, B, Bp, bid, S, smem);
-  } else if (bid < S + S * ROLE_A_WGS) {
-    const int r = bid - S;
+  } else if (order == 0 ? bid < S + nA : bid >= S + nB) {
+    const int r = bid - S - (order == 0 ? 0 : nB);
     fc_bwd_role_a(a, B, Bp, r % ROLE_A_WGS, r / ROLE_A_WGS, S, smem);
   } else {
-    fc_bwd_role_b<BIG>(a, B, Bp, bid - S - S * ROLE_A_WGS, fcb_mr(B), smem);
+    fc_bwd_role_b<BIG>(a, B, Bp, bid - S - (order == 0 ? nA : 0), fcb_mr(B), smem);
   }
 }
 
@@ -773,17 +783,14 @@ __global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B,
   }
 }
 
-static int fc_bwd_role_b_wgs(int B) {
-  const int rows16 = (B + 15) / 16, mr = fcb_mr(B);
-  return ((rows16 + mr - 1) / mr) * ROLE_B_SBLOCKS;
-}
+
 
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
   const int S = fc_bwd_splits(B);
   if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
   const int grid = S + S * ROLE_A_WGS + fc_bwd_role_b_wgs(B);
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, 0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, 0);
   if (S > 1) {
     constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;
     hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
@@ -796,8 +803,17 @@ void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t
   const int nb = fc_bwd_role_b_wgs(B);
   const int grid = role == 0 ? S : role == 1 ? S * ROLE_A_WGS : nb;
   const int bid0 = role == 0 ? 0 : role == 1 ? S : S + S * ROLE_A_WGS;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
+}
+
+void launch_fc_bwd_part(const FcBwdArgs& a, int B, int Bp, int part, hipStream_t s) {
+  if (fc_bwd_splits(B) != 1) throw std::runtime_error("fc_bwd two-stream form needs B <= FC_BWD_SPLIT_ROWS");
+  const int nb = fc_bwd_role_b_wgs(B);
+  const int grid = part == 0 ? 1 + nb : ROLE_A_WGS;
+  const int bid0 = part == 0 ? 0 : 1 + nb;
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 1);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 1);
 }
 
 }  // namespace mnist

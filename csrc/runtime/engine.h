@@ -101,6 +101,8 @@ class Engine {
   // single GPU: run the fc Adadelta step on the comm stream, overlapped with the conv backward, with
   // the schedule-3 device-counter hand-offs (needs probe_stream_handoff() to pass)
   void set_overlap_fc_update(bool on) { overlap_fc_update_ = on; }
+  // schedule 3 (incl. the single-GPU overlap): fc_bwd's role A (dW1) on the comm stream
+  void set_split_fc_bwd(bool on) { split_fc_bwd_ = on; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -156,6 +158,7 @@ class Engine {
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
+  bool split_fc_bwd_ = true;
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
   hipEvent_t ev_c2_ = nullptr;

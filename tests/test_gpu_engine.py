@@ -177,3 +177,19 @@ def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch)
     torch.cuda.synchronize()
     assert torch.equal(ms_s.param, ms_o.param) and torch.equal(ts.loss_log, to.loss_log)
     assert torch.equal(ms_s.w1t, ms_o.w1t) and torch.equal(ms_s.w2f, ms_o.w2f)
+
+
+def test_fc_bwd_role_split_bitwise_equal(cuda_device, monkeypatch):
+    """Schedule 3 puts fc_bwd's dW1 role on the comm stream (MNIST_AMD_SPLIT_FCBWD, default on):
+    the same bits as the one-launch fc_bwd."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(11))
+    monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "0")
+    _, ms_a, ta = _trainer(cuda_device, graph_steps=4)
+    monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "1")
+    _, ms_b, tb = _trainer(cuda_device, graph_steps=4)
+    assert ta.overlap_fc and tb.overlap_fc
+    ta.train_epoch(1, idx)
+    tb.train_epoch(1, idx)
+    tb.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
