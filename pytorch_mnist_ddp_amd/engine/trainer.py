@@ -106,7 +106,7 @@ class FusedTrainer:
         self.overlap_fc = (comm is None and world_size == 1 and not fuse_fc_update and not concurrent
                            and os.environ.get("MNIST_AMD_OVERLAP_FC", "1") == "1")
         self.engine.set_overlap_fc_update(self.overlap_fc)
-        # schedule 3: fc_bwd's dW1 role on the comm stream (MNIST_AMD_SPLIT_FCBWD=0: one launch)
+X
         self.engine.set_split_fc_bwd(os.environ.get("MNIST_AMD_SPLIT_FCBWD", "1") != "0")
         # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
         # device-counter stream hand-offs) when a second communicator is given, else 1

@@ -180,7 +180,7 @@ def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch)
 
 
 def test_fc_bwd_role_split_bitwise_equal(cuda_device, monkeypatch):
-    """Schedule 3 puts fc_bwd's dW1 role on the comm stream (MNIST_AMD_SPLIT_FCBWD, default on):
+    X
     the same bits as the one-launch fc_bwd."""
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(11))
     monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "0")
