@@ -180,7 +180,7 @@ def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch)
 
 
 def test_fc_bwd_role_split_bitwise_equal(cuda_device, monkeypatch):
-    X
+    """MNIST_AMD_SPLIT_FCBWD=1 (opt-in): fc_bwd's dW1 role on the comm stream under schedule 3 gives
     the same bits as the one-launch fc_bwd."""
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(11))
     monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "0")
