@@ -143,6 +143,11 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 wgrad + bias partials
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s);
+struct AdadeltaArgs;
+// single-GPU step: conv2_dgrad's 4B workgroups followed, in the same launch, by the conv2 slab reduce
+// + conv2 Adadelta update (RED_W2_PARTS workgroups filling the slots dgrad's last partial round
+// leaves idle).  u.w2d must not alias c.w2d (dgrad reads the step's shadow while the update writes)
+void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s);
 
 // ---------------- optimizer ----------------
 struct AdadeltaArgs {
@@ -163,6 +168,8 @@ void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
 // conv gradient slab reduce + the whole Adadelta update in one launch (single-GPU step tail);
 // conv_only when fc_bwd already applied the fc update (FcBwdArgs::upd)
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s);
+// conv-only form restricted to reduce parts [lo, hi) (conv_grad_reduce.h partition)
+void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s);
 // Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
 void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 

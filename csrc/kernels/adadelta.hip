@@ -16,6 +16,8 @@
 #include "../include/kernels.h"
 #include "conv_grad_reduce.h"
 
+#include <stdexcept>
+
 namespace mnist {
 
 namespace {
@@ -25,15 +27,6 @@ constexpr int64_t CONV_N = PARAM_TOTAL - OFF_CONV1_W;             // 18880
 constexpr int CONV_WGS = (int)((CONV_N / 4 + 255) / 256);         // 19
 
 // Per-element math: Ada (device_utils.h), contraction off so every launch path is bitwise equal.
-
-__device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, float v) {
-  const int rel = (int)(e - OFF_CONV2_W);
-  if (rel < 0 || rel >= C2 * C1 * 9) return;
-  const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
-  const uint16_t h = f2bf(v);
-  a.w2f[(co * 9 + t) * C1 + ci] = h;
-  a.w2d[(t * C1 + ci) * C2 + co] = h;
-}
 
 template <bool UPDATE>
 __device__ __forceinline__ void elementwise(const AdadeltaArgs& a, const Ada& ad, int64_t begin, int64_t n,
@@ -126,46 +119,32 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
 // its gradient is final (no grad round trip, no extra kernel boundary; both halves are memory-
 // bound and overlap).  Same per-element math as the two-kernel path, so results are bitwise equal.
 // conv_only: the fc parameters were already updated by fc_bwd's fused epilogue (FcBwdArgs::upd).
-__global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int conv_only) {
+// conv_only: reduce parts [bid0, bid0 + grid) only (the conv2 parts may already have run inside the
+// dgrad launch, launch_conv_dgrad_update)
+__global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int conv_only,
+                                                              int bid0) {
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   __shared__ float4 red[256];
-  const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   if (!conv_only) {
+    const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
     if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }
     bid -= FC1_TILES;
     if (bid == 0) { elementwise<true>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
     bid -= 1;
   }
-  float* gbuf = c.grad;
-  // the update's optimizer state, loaded before (and in flight with) the slab loads
-  float pp[4], ps[4], pa[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t e = conv_sink_index(bid, threadIdx.x, r);
-    if (e >= 0) {
-      pp[r] = a.param[e];
-      ps[r] = a.square_avg[e];
-      pa[r] = a.acc_delta[e];
-    }
-  }
-  int k = 0;
-  reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
-    gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
-    float p = pp[k], sq = ps[k], acc = pa[k];
-    ++k;
-    ad.step(p, g, sq, acc);
-    a.param[e] = p;
-    a.square_avg[e] = sq;
-    a.acc_delta[e] = acc;
-    conv2_shadow(a, e, p);
-  });
+  conv_reduce_update(a, c, B, bid + bid0, red);
 }
 
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s) {
   const int grid = (conv_only ? 0 : FC1_TILES + 1) + RED_WGS;
-  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(grid), dim3(256), 0, s, a, c, B, conv_only ? 1 : 0);
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(grid), dim3(256), 0, s, a, c, B, conv_only ? 1 : 0, 0);
+}
+
+void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s) {
+  if (lo < 0 || hi > RED_WGS || lo >= hi) throw std::runtime_error("adadelta_reduce: bad part range");
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(hi - lo), dim3(256), 0, s, a, c, B, 1, lo);
 }
 
 static int adadelta_grid(int region) {

@@ -85,15 +85,13 @@ int conv_wgrad_groups(int B) {
 }
 
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
+__device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int strip, int b, unsigned char* smem) {
   uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
   uint16_t* w2ds = reinterpret_cast<uint16_t*>(smem + DYS_BYTES);
   float* xs = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES);
   float* red = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES + 1024);
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int strip = blockIdx.x, b = blockIdx.y;
   // schedule-3 conv bucket split: dgrad's start = conv2_wgrad done (stream order), i.e. the conv2
   // gradient slabs are final; one lane tells the comm stream (release: wgrad's writes happen-before)
   if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
@@ -254,6 +252,27 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
     const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
     a.c1part[((int64_t)b * 4 + strip) * 320 + e] = s;
   }
+}
+
+__global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
+  dgrad_body(a, B, blockIdx.x, blockIdx.y, smem);
+}
+
+// dgrad (workgroups [0, 4B), same order as conv2_dgrad_kernel's (strip, b) grid) + the conv2 slab
+// reduce and Adadelta step (workgroups [4B, 4B + RED_W2_PARTS)).  Workgroups are dispatched in id
+// order, so the reduce parts take the slots of dgrad's last partial round (800 WGs on 512 slots at
+// B = 200) instead of a launch of their own after dgrad.  Reads only wgrad's slabs (complete at
+// launch); writes conv2 params / state / grads and the shadows u.w2f, u.w2d (!= a.w2d, which the
+// dgrad workgroups read).
+__global__ __launch_bounds__(256) void conv2_dgrad_update_kernel(ConvBwdArgs a, AdadeltaArgs u, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
+  const int bid = blockIdx.x;
+  if (bid < 4 * B) {
+    dgrad_body(a, B, bid & 3, bid >> 2, smem);
+    return;
+  }
+  conv_reduce_update(u, a, B, bid - 4 * B, reinterpret_cast<float4*>(smem));
 }
 
 // --------------------------------------------------------------------------------------------
@@ -428,6 +447,10 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, in
   __shared__ float4 red[256];
   float* grad = a.grad;
   reduce_conv_grads(a, B, blockIdx.x, red, [grad](int64_t e, float v) { grad[e] = v; });
+}
+
+void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv2_dgrad_update_kernel, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
 }
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {

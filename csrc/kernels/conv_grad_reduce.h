@@ -114,4 +114,45 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
   }
 }
 
+// bf16 shadows of one updated conv2.weight element: forward layout w2f [co][tap][ci] and dgrad
+// layout w2d [tap][ci][co]
+__device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, float v) {
+  const int rel = (int)(e - OFF_CONV2_W);
+  if (rel < 0 || rel >= C2 * C1 * 9) return;
+  const int co = rel / 288, rem = rel - co * 288, ci = rem / 9, t = rem - ci * 9;
+  const uint16_t h = f2bf(v);
+  a.w2f[(co * 9 + t) * C1 + ci] = h;
+  a.w2d[(t * C1 + ci) * C2 + co] = h;
+}
+
+// Reduce part `bid` of the conv gradients and apply the Adadelta step to each finished element
+// (grad buffer, param, optimizer state, bf16 shadows).  The optimizer state of the <= 4 elements a
+// lane sinks is loaded before (and in flight with) the slab loads.
+__device__ __forceinline__ void conv_reduce_update(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int bid,
+                                                   float4* red) {
+  const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
+  float* gbuf = c.grad;
+  float pp[4], ps[4], pa[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t e = conv_sink_index(bid, threadIdx.x, r);
+    if (e >= 0) {
+      pp[r] = a.param[e];
+      ps[r] = a.square_avg[e];
+      pa[r] = a.acc_delta[e];
+    }
+  }
+  int k = 0;
+  reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
+    gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
+    float p = pp[k], sq = ps[k], acc = pa[k];
+    ++k;
+    ad.step(p, g, sq, acc);
+    a.param[e] = p;
+    a.square_avg[e] = sq;
+    a.acc_delta[e] = acc;
+    conv2_shadow(a, e, p);
+  });
+}
+
 }  // namespace mnist

@@ -45,8 +45,9 @@ constexpr int WIN = (STRIP / 2) * HP;         // 48 pool windows per strip
 // LDS carve (bytes, 16-aligned), time-shared so NS = 1 fits three workgroups per CU (160 KiB):
 //   [0, A1S)           a1 tile (bf16 NHWC, swizzled)          -> after the MFMA loop: pool staging
 //   [W2S_OFF, +36864)  conv2 weights: the EARLY chunks of every thread are stored in phase 0, the
-//                      input rows live where the parked chunks go until conv1 has consumed them,
-//                      then the parked chunks are stored from VGPRs (phase 1b) -> later: flags
+//                      input rows + conv1 weights live where the parked chunks go until conv1 has
+//                      consumed them, then the parked chunks are stored from VGPRs (phase 1b)
+//                      -> later: flags
 template <int NS>
 struct TrunkCfg {
   static constexpr int THREADS = 256 * NS;
@@ -57,6 +58,9 @@ struct TrunkCfg {
   static constexpr int CHUNKS = W2S_BYTES / 16 / THREADS;     // 16-B weight chunks per thread: 9 | 3
   static constexpr int EARLY = NS == 1 ? 7 : 2;               // stored in phase 0, rest parked
   static constexpr int XS_OFF = W2S_OFF + EARLY * THREADS * 16, XS_BYTES = X_ROWS * IMG * 4;
+  // conv1 weights + bias (320 floats) staged once per workgroup, past the input rows (also in the
+  // parked-chunk region, consumed at the start of phase 1)
+  static constexpr int W1S_OFF = XS_OFF + XS_BYTES, W1S_BYTES = (C1 * 9 + C1) * 4;
   static constexpr int WIN_LD = WIN * NS + 4;                 // [channel][window] row: 52 | 148 =
                                                               // 20 mod 32 words -> conflict-free rows
   static constexpr int POOL_OFF = 0, POOL_BYTES = C2 * WIN_LD * 4;
@@ -66,6 +70,7 @@ struct TrunkCfg {
   static constexpr int C1_ITERS = (A1_ROWS * H1 + C1_PIX - 1) / C1_PIX;   // 5 | 4
   static_assert(CHUNKS * THREADS * 16 == W2S_BYTES, "weight chunking");
   static_assert(XS_OFF + XS_BYTES <= LDS, "input rows alias the parked weight chunks");
+  static_assert(W1S_OFF % 16 == 0 && W1S_OFF + W1S_BYTES <= LDS, "conv1 weights alias the parked chunks");
   static_assert(POOL_BYTES <= A1S_BYTES && FLAG_OFF + FLAG_BYTES <= LDS, "epilogue staging aliasing");
   static_assert(NS != 1 || 3 * LDS <= 160 * 1024, "three strip workgroups per CU");
 };
@@ -84,6 +89,7 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
   using K = TrunkCfg<NS>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[K::LDS];
   float* xs = reinterpret_cast<float*>(smem + K::XS_OFF);
+  float* w1s = reinterpret_cast<float*>(smem + K::W1S_OFF);
   uint16_t* a1s = reinterpret_cast<uint16_t*>(smem);
   uint16_t* w2s = reinterpret_cast<uint16_t*>(smem + K::W2S_OFF);
   float* pool_s = reinterpret_cast<float*>(smem + K::POOL_OFF);
@@ -98,7 +104,7 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
   // ---- phase 0: issue every global load first (input rows, conv2 weights, conv1 weights, conv2
   // bias), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
   const int c = tid & 3;                         // conv1: fixed 8-channel chunk per thread
-  float w[8][9], bias[8], bias2[4];
+  float bias2[4];
   constexpr int PARKED = K::CHUNKS - K::EARLY;
   static_assert(PARKED == 1 || PARKED == 2, "parked chunk count");
   uint4 wp0, wp1 = {0u, 0u, 0u, 0u};            // conv2-weight chunks held in VGPRs until phase 1b
@@ -110,18 +116,11 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
     for (int i = 0; i < K::EARLY; ++i) wv[i] = src[tid + K::THREADS * i];
     wp0 = src[tid + K::THREADS * K::EARLY];
     if constexpr (PARKED == 2) wp1 = src[tid + K::THREADS * (K::EARLY + 1)];
-    const float4* w1v = reinterpret_cast<const float4*>(a.w1c + c * 72);
-#pragma unroll
-    for (int k = 0; k < 18; ++k) {
-      const float4 f = w1v[k];
-      const float fv[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[(4 * k + e) / 9][(4 * k + e) % 9] = fv[e];
-    }
-    const float4* b1v = reinterpret_cast<const float4*>(a.b1c + c * 8);
-    const float4 b0 = b1v[0], b1 = b1v[1];
-    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
-    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+    // conv1 weights [32][9] (72 float4) + bias (8 float4): 80 threads fetch them once per workgroup
+    // (per-thread copies were 18 float4 loads x 768 threads of L1 traffic)
+    float4 w1v = {0.f, 0.f, 0.f, 0.f};
+    if (tid < 72) w1v = reinterpret_cast<const float4*>(a.w1c)[tid];
+    else if (tid < 80) w1v = reinterpret_cast<const float4*>(a.b1c)[tid - 72];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) bias2[nt] = a.b2c[nt * 16 + (tid & 15)];
 #pragma unroll
@@ -129,6 +128,15 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
       const int ch = tid + K::THREADS * i;
       const int row = ch >> 2, kc = ch & 3;      // row = n*9 + tap
       *reinterpret_cast<uint4*>(w2s + row * 32 + ((kc ^ swz_w2(row / 9)) * 8)) = wv[i];
+    }
+    if (tid < 80) {                              // pair-interleaved: [chunk c][pair jp][tap t | bias][2]
+      const float fv[4] = {w1v.x, w1v.y, w1v.z, w1v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int f = 4 * tid + e;                 // w1c[ch][t] (f < 288) or b1c[ch]
+        const int ch = f < C1 * 9 ? f / 9 : f - C1 * 9, t = f < C1 * 9 ? f - 9 * (f / 9) : 9;
+        w1s[(((ch >> 3) * 4 + ((ch & 7) >> 1)) * 10 + t) * 2 + (ch & 1)] = fv[e];
+      }
     }
     uint4 xv = {0u, 0u, 0u, 0u};
     float4 xf = {0.f, 0.f, 0.f, 0.f};
@@ -160,16 +168,37 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
   __syncthreads();
   PHASE_MARK(1);
 
-  // ---- phase 1: conv1 + bias + ReLU (fp32 VALU) -> a1 tile (bf16 NHWC, swizzled) [+ HBM copy]
+  // ---- phase 1: conv1 + bias + ReLU (fp32 VALU) -> a1 tile (bf16 NHWC, swizzled) [+ HBM copy].
+  // Channel pairs on v_pk_fma_f32 (the input pixel broadcast to both halves): per channel the same
+  // fma chain as conv1_preact (bias, then taps in row-major order), so bitwise the scalar result.
+  float2v wp[4][9], bp[4];
+  {
+    const float2v* wl = reinterpret_cast<const float2v*>(w1s) + c * 40;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wp[jp][t] = wl[jp * 10 + t];
+      bp[jp] = wl[jp * 10 + 9];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < K::C1_ITERS; ++i) {
     const int pidx = (tid >> 2) + K::C1_PIX * i;
     if (pidx < K::A1_ROWS * H1) {
       const int r = pidx / H1, col = pidx - r * H1;
       const float* xp = xs + r * IMG + col;
+      float xv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) xv[t] = xp[(t / 3) * IMG + t % 3];
       float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaxf(conv1_preact(xp, IMG, w[j], bias[j]), 0.0f);
+      for (int jp = 0; jp < 4; ++jp) {
+        float2v acc = bp[jp];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc = __builtin_elementwise_fma(float2v{xv[t], xv[t]}, wp[jp][t], acc);
+        o[2 * jp] = fmaxf(acc.x, 0.0f);
+        o[2 * jp + 1] = fmaxf(acc.y, 0.0f);
+      }
       uint4 v;
       v.x = pack2bf(o[0], o[1]); v.y = pack2bf(o[2], o[3]);
       v.z = pack2bf(o[4], o[5]); v.w = pack2bf(o[6], o[7]);

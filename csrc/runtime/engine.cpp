@@ -283,6 +283,26 @@ void Engine::enqueue_step(int batch, bool last) {
           w2d_in_alt_ = false;
         }
       }
+    } else if (local3 && dgrad_update_) {
+      // single GPU: conv2's reduce + update inside the dgrad launch (it reads this step's w2d while
+      // the update writes the other copy: ping-pong as in the split path), conv1's after it
+      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
+      AdadeltaArgs u = adc;
+      u.state_inc = nullptr;
+      u.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
+      cb.w2d = w2d_cur;
+      phase_begin("bwd_conv_dgrad+conv2_update");
+      launch_conv_dgrad_update(cb, u, B, compute_);
+      phase_end();
+      phase_begin("conv1_update");
+      launch_adadelta_reduce_parts(adc, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+      phase_end();
+      w2d_in_alt_ = !w2d_in_alt_;
+      if (last && w2d_in_alt_) {
+        HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                              compute_));
+        w2d_in_alt_ = false;
+      }
     } else {
     phase_begin("bwd_conv_dgrad");
     launch_conv_dgrad(cb, B, compute_);

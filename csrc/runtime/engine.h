@@ -103,6 +103,9 @@ class Engine {
   void set_overlap_fc_update(bool on) { overlap_fc_update_ = on; }
   // schedule 3 (incl. the single-GPU overlap): fc_bwd's role A (dW1) on the comm stream
   void set_split_fc_bwd(bool on) { split_fc_bwd_ = on; }
+  // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
+  // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
+  void set_dgrad_update(bool on) { dgrad_update_ = on; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -159,6 +162,7 @@ class Engine {
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
   bool split_fc_bwd_ = true;
+  bool dgrad_update_ = true;
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
   hipEvent_t ev_c2_ = nullptr;
@@ -167,7 +171,7 @@ class Engine {
   void phase_end();
   uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (fused fc update ping-pong)
   bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
-  uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv bucket split ping-pong)
+  uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv split / dgrad_update ping-pong)
   bool w2d_in_alt_ = false;
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;
   hipStream_t wgrad_stream_ = nullptr;

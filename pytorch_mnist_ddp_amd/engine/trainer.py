@@ -109,6 +109,9 @@ class FusedTrainer:
         # schedule 3: fc_bwd's dW1 role on the comm stream (opt-in MNIST_AMD_SPLIT_FCBWD=1; bitwise
         # equal, measured 82.7 -> 82.9-83.1 us/step: role A then competes with role B / conv2_wgrad)
         self.engine.set_split_fc_bwd(os.environ.get("MNIST_AMD_SPLIT_FCBWD", "0") == "1")
+        # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
+        # (MNIST_AMD_DGRAD_UPDATE=0 for the separate step-tail launch; bitwise equal)
+        self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "1") != "0")
         # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
         # device-counter stream hand-offs) when a second communicator is given, else 1
         # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)

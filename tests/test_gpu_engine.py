@@ -193,3 +193,20 @@ def test_fc_bwd_role_split_bitwise_equal(cuda_device, monkeypatch):
     tb.synchronize()
     torch.cuda.synchronize()
     assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
+
+
+def test_dgrad_update_bitwise_equal(cuda_device, monkeypatch):
+    """MNIST_AMD_DGRAD_UPDATE (default): the conv2 slab reduce + update as extra workgroups of the
+    dgrad launch (w2d ping-pong across steps, odd graph chunks end on the alternate copy) gives the
+    bits of the separate step-tail launch; the eval after training sees the current shadows."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(13))
+    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "0")
+    _, ms_a, ta = _trainer(cuda_device, graph_steps=3)
+    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "1")
+    _, ms_b, tb = _trainer(cuda_device, graph_steps=3)
+    ta.train_epoch(1, idx)
+    tb.train_epoch(1, idx)
+    tb.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
+    assert torch.equal(ms_a.w2f, ms_b.w2f) and torch.equal(ms_a.w2d, ms_b.w2d)
