@@ -137,7 +137,13 @@ struct ConvBwdArgs {
   int wgrad_groups;           // G
   const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
   int* signal_ctr;            // optional: conv2_wgrad / conv2_dgrad add 1 at kernel start (schedule-3 hand-offs)
+  // optional [C1_PRE_SLABS][320]: when set, launch_conv_dgrad(_update) pre-reduces the 4B conv1
+  // partials into C1_PRE_SLABS fixed-order group sums and the conv reduce reads those (large B:
+  // 20 reduce workgroups walking 4B slabs is a dependent-load chain, 81 us at B = 8192)
+  float* c1red;
 };
+constexpr int C1_PRE_SLABS = 256;
+constexpr int C1_PRE_MIN_SLABS = 1024;    // engine: pre-reduce when 4B exceeds this
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials

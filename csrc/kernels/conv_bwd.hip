@@ -449,12 +449,53 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, in
   reduce_conv_grads(a, B, blockIdx.x, red, [grad](int64_t e, float v) { grad[e] = v; });
 }
 
+static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
+
 void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_dgrad_update_kernel, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
+  launch_c1_prereduce(c, B, s);
+}
+
+// c1red[j] = sum of the conv1 partial rows [j*R, (j+1)*R) (R = ceil(4B / C1_PRE_SLABS)) in fixed
+// order: thread (column, slice) sums rows slice, slice+3, ... in batches of 16 independent loads,
+// then the 3 slices are added in order.
+__global__ __launch_bounds__(256) void c1_prereduce_kernel(const float* __restrict__ c1part, int nslab,
+                                                           float* __restrict__ c1red) {
+  __shared__ float4 sh[240];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int R = (nslab + C1_PRE_SLABS - 1) / C1_PRE_SLABS;
+  const int r0 = j * R, r1 = min(r0 + R, nslab);
+  const int col = tid % 80, sl = tid / 80;       // 80 float4 columns x 3 slices (240 threads)
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sl < 3) {
+    const float4* src = reinterpret_cast<const float4*>(c1part) + col;
+    for (int k0 = r0 + sl; k0 < r1; k0 += 3 * 16) {
+      float4 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int r = k0 + 3 * k;
+        v[k] = (r < r1) ? src[(int64_t)r * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+    }
+    sh[tid] = t;
+  }
+  __syncthreads();
+  if (tid < 80) {
+    const float4 a = sh[tid], b = sh[tid + 80], c = sh[tid + 160];
+    reinterpret_cast<float4*>(c1red)[(int64_t)j * 80 + tid] =
+        make_float4((a.x + b.x) + c.x, (a.y + b.y) + c.y, (a.z + b.z) + c.z, (a.w + b.w) + c.w);
+  }
+}
+
+static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
+  if (a.c1red) hipLaunchKernelGGL(c1_prereduce_kernel, dim3(C1_PRE_SLABS), dim3(256), 0, s, a.c1part, 4 * B, a.c1red);
 }
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
+  launch_c1_prereduce(a, B, s);
 }
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);

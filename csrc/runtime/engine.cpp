@@ -65,6 +65,7 @@ void Engine::alloc_workspace() {
   sync_ = reinterpret_cast<int*>(base + L.sync);
   w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
   w2d_alt_ = reinterpret_cast<uint16_t*>(base + L.w2d_alt);
+  c1red_ = reinterpret_cast<float*>(base + L.c1red);
 }
 
 void Engine::set_conv_split(bool on, uintptr_t conv2_stream) {
@@ -215,6 +216,7 @@ void Engine::enqueue_step(int batch, bool last) {
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
+  if (4 * B > C1_PRE_MIN_SLABS) cb.c1red = c1red_;          // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
   if (sched3) {

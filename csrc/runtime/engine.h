@@ -171,6 +171,7 @@ class Engine {
   void phase_end();
   uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (fused fc update ping-pong)
   bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
+  float* c1red_ = nullptr;          // conv1 partial group sums (large batches)
   uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv split / dgrad_update ping-pong)
   bool w2d_in_alt_ = false;
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;

@@ -18,7 +18,7 @@ namespace mnist {
 
 // ---------------------------------------------------------------------------- engine workspace
 struct WorkspaceLayout {
-  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w1t_alt, w2d_alt;
+  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w1t_alt, w2d_alt, c1red;
   int64_t total;   // bytes
 };
 
@@ -52,6 +52,7 @@ inline WorkspaceLayout compute_workspace_layout(int max_batch, int max_test_batc
   L.sync = carve(256);                                                                // schedule-3 counters
   L.w1t_alt = carve((int64_t)NFLAT * NH * 2);                                         // alternate w1t
   L.w2d_alt = carve((int64_t)9 * C1 * C2 * 2);                                         // alternate w2d
+  L.c1red = carve((int64_t)C1_PRE_SLABS * 320 * 4);                                    // conv1 group sums
   L.total = off;
   return L;
 }

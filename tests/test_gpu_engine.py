@@ -210,3 +210,36 @@ def test_dgrad_update_bitwise_equal(cuda_device, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
     assert torch.equal(ms_a.w2f, ms_b.w2f) and torch.equal(ms_a.w2d, ms_b.w2d)
+
+
+def test_large_batch_conv1_prereduce_matches_functional(cuda_device):
+    """B = 512 (4B > C1_PRE_MIN_SLABS): the engine pre-reduces the 4B conv1 partial rows in 256
+    fixed-order groups before the conv reduce; its gradients equal the functional path's (one pass
+    over the 4B rows) up to fp32 summation order, and a repeated run gives the same bits."""
+    from pytorch_mnist_ddp_amd.engine.state import FLAG_NO_DROPOUT
+    from pytorch_mnist_ddp_amd.ops import functional as Fk
+    B = 512
+    torch.manual_seed(1)
+    net = Net()
+    tr = load_mnist(synthetic_data=True, train=True, synthetic_size=B, verbose=False)
+    idx = torch.arange(B)
+    grads = []
+    for _ in range(2):
+        ms = ModelState(net, cuda_device, lr=1.0)
+        t = FusedTrainer(ms, tr, None, B, 1, num_samples=B, seed=1, graph_steps=0, dropout=False)
+        t.train_epoch(1, idx)
+        t.synchronize()
+        torch.cuda.synchronize()
+        grads.append(ms.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    ms2 = ModelState(net, cuda_device, lr=1.0)
+    u8 = tr.images.reshape(B, -1).contiguous().to(cuda_device)
+    lab = tr.targets.to(torch.int32).to(cuda_device)
+    buf = Fk.StepBuffers.allocate(B, cuda_device)
+    ms2.set_state(0, seed=1, rng_base=0, flags=FLAG_NO_DROPOUT)
+    Fk.train_step(ms2, u8, lab, torch.arange(B, dtype=torch.int32, device=cuda_device), buf, update=False)
+    torch.cuda.synchronize()
+    g_eng, g_fn = ms.views(grads[0]), ms2.views(ms2.grad)
+    for name in g_fn:
+        err = ((g_eng[name] - g_fn[name]).norm() / g_fn[name].norm().clamp_min(1e-30)).item()
+        assert err < 1e-4, (name, err)
