@@ -189,6 +189,7 @@ PYBIND11_MODULE(_C, m) {
                   P<const float>(w1c), P<const float>(b1c), P<const uint8_t>(data_u8), P<const int32_t>(idx),
                   idx_stride, P<const StepState>(state), P<float>(c1part), P<float>(w2part), P<float>(grad),
                   grad_scale, conv_wgrad_groups(B), P<const float>(xin)};
+    a.c1_rows = conv_dgrad_c1_rows(B);
     launch_conv_bwd(a, B, S(stream));
     launch_conv_grad_reduce(a, B, S(stream));
     check_launch();
@@ -309,7 +310,6 @@ PYBIND11_MODULE(_C, m) {
       .def("set_fuse_fc_update", &Engine::set_fuse_fc_update)
       .def("set_overlap_fc_update", &Engine::set_overlap_fc_update)
       .def("set_conv_split", &Engine::set_conv_split)
-      .def("set_split_fc_bwd", &Engine::set_split_fc_bwd)
       .def("set_dgrad_update", &Engine::set_dgrad_update)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())

@@ -141,9 +141,13 @@ struct ConvBwdArgs {
   // partials into C1_PRE_SLABS fixed-order group sums and the conv reduce reads those (large B:
   // 20 reduce workgroups walking 4B slabs is a dependent-load chain, 81 us at B = 8192)
   float* c1red;
+  int c1_rows;                // conv1 partial rows the dgrad launch writes: conv_dgrad_c1_rows(B)
 };
+// 4B (4 strips of 7 rows per image, 2 workgroups per CU) or 3B (3 strips of 9/9/8 rows, conv2
+// weights read from L2 instead of LDS: 3 workgroups per CU, one round at B <= 256); MNIST_AMD_DGRAD3
+int conv_dgrad_c1_rows(int B);
 constexpr int C1_PRE_SLABS = 256;
-constexpr int C1_PRE_MIN_SLABS = 1024;    // engine: pre-reduce when 4B exceeds this
+constexpr int C1_PRE_MIN_SLABS = 1024;    // engine: pre-reduce when c1_rows exceeds this
 int conv_wgrad_groups(int B);
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(+conv1 wgrad) and wgrad
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials

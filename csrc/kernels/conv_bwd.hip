@@ -19,6 +19,9 @@
 #include "../include/kernels.h"
 #include "conv_grad_reduce.h"
 
+#include <stdexcept>
+#include <stdlib.h>
+
 namespace mnist {
 
 namespace {
@@ -259,6 +262,190 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
   dgrad_body(a, B, blockIdx.x, blockIdx.y, smem);
 }
 
+// --------------------------------------------------------------------------------------------
+// conv2_dgrad, 3-strip form: WG = image x strip of 9/9/8 conv1 rows.  The conv2 weights' B fragments
+// come straight from L2 (w2d is 36.9 KB, L2-resident; each wave streams it once per strip with a
+// 4-k-step register prefetch) instead of an LDS copy, so a workgroup needs only the dy tile (11 x 28
+// pixels x 64 ch) + input rows + the reduction scratch: 45.8 KB -> 3 workgroups per CU, and the 3B
+// workgroups of B <= 256 run in one round (the 4-strip form: 4B workgroups, 2 per CU, 1.56 rounds
+// at B = 200).  Same math per pixel as conv2_dgrad_kernel (K order, masks, conv1-gradient MFMA);
+// the conv1 partials are per (image, strip of 3).
+namespace {
+constexpr int D3_ROWS = 9;
+constexpr int D3_TROWS = D3_ROWS + 2;                        // 11 dy rows incl. halo, 11 input rows
+constexpr int D3_DYS = D3_TROWS * DG_TCOLS * C2 * 2;         // 39424
+constexpr int D3_XS = 1280;                                  // 11 * 28 floats (1232 B)
+constexpr int D3_RED = 4 * 32 * 10 * 4;                      // 5120
+constexpr int D3_LDS = D3_DYS + D3_XS + D3_RED;              // 45824
+constexpr int D3_MT = 4;                                     // M-tiles per wave (<= 15 per strip)
+constexpr int D3_PF = 4;                                     // B-fragment prefetch depth (k-steps)
+static_assert(3 * D3_LDS <= 160 * 1024, "three dgrad workgroups per CU");
+static_assert(D3_TROWS * IMG <= 2 * 256, "input rows: two per thread");
+}  // namespace
+
+__global__ __launch_bounds__(256, 3) void conv2_dgrad3_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[D3_LDS];
+  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
+  float* xs = reinterpret_cast<float*>(smem + D3_DYS);
+  float* red = reinterpret_cast<float*>(smem + D3_DYS + D3_XS);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int strip = blockIdx.x, b = blockIdx.y;
+  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const int r0 = strip * D3_ROWS;
+  const int npix = ((strip == 2) ? (H1 - 2 * D3_ROWS) : D3_ROWS) * H1;   // 9, 9, 8 rows
+  const int step = a.state ? a.state->step : 0;
+
+  // ---- stage the padded dy tile (rows r0-2..r0+8, cols -2..25) and the input rows
+  {
+    constexpr int NCH = D3_TROWS * DG_TCOLS * 8;   // 2464 16-B chunks
+    constexpr int KV = (NCH + 255) / 256;          // 10
+    uint4 v[KV];
+    uint2 rt[KV];
+    uint32_t okm = 0;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int c = tid + 256 * k;
+      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
+      const int y = r0 - 2 + ly, x = col - 2;
+      const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
+      okm |= (ok ? 1u : 0u) << k;
+      const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
+      v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
+      rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
+    }
+    float xv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = tid + 256 * j;
+      const bool okx = e < D3_TROWS * IMG && r0 + e / IMG < IMG;
+      const int off = r0 * IMG + (okx ? e : 0);
+      if (a.xin) {
+        xv[j] = a.xin[(int64_t)b * (IMG * IMG) + off];
+      } else {
+        const int64_t row = (int64_t)step * a.idx_step_stride + b;
+        const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
+        xv[j] = normalize_u8(a.data_u8[img * (IMG * IMG) + off]);
+      }
+      if (!okx) xv[j] = 0.0f;
+    }
+    const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int c = tid + 256 * k;
+      if (c < NCH) {
+        const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
+        const int y = r0 - 2 + ly, x = col - 2;
+        const int row = c >> 3, c8 = c & 7;
+        const uint4 d = ((okm >> k) & 1u) ? dyc_expand(v[k], rt[k], ((y & 1) << 1) | (x & 1)) : z;
+        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (tid + 256 * j < D3_TROWS * IMG) xs[tid + 256 * j] = xv[j];
+  }
+  __syncthreads();
+
+  // ---- transposed conv on MFMA: wave w owns M-tiles w, w+4, w+8, w+12 (16 pixels each)
+  const int m = lane & 15, kg = lane >> 4;
+  int qbase[D3_MT];
+#pragma unroll
+  for (int i = 0; i < D3_MT; ++i) {
+    int q = 16 * (wave + 4 * i) + m;
+    if (q >= npix) q = 0;
+    const int qy = q / H1, qx = q - qy * H1;
+    qbase[i] = (qy + 2) * DG_TCOLS + qx + 2;
+  }
+  floatx4 acc[D3_MT][2];
+#pragma unroll
+  for (int i = 0; i < D3_MT; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // conv1 ReLU mask (a1 > 0), two bf16 per VGPR, loaded before the B stream (vmcnt is in order)
+  uint32_t a1v[D3_MT][4];
+#pragma unroll
+  for (int i = 0; i < D3_MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int q = 16 * (wave + 4 * i) + 4 * kg + r;
+      q = q < npix ? q : npix - 1;
+      const uint16_t* src = a.a1 + ((int64_t)b * H1 * H1 + r0 * H1 + q) * C1 + m;
+      a1v[i][r] = (uint32_t)src[0] | ((uint32_t)src[16] << 16);
+    }
+  // B fragment (tap t, ci tile nt, co chunk) of w2d [9][32][64]: 16 contiguous bytes per lane
+  const uint16_t* wb = a.w2d + (int64_t)m * C2 + 8 * kg;
+  bf16x8 Bq[18][2];
+#pragma unroll
+  for (int ks = 0; ks < D3_PF; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) Bq[ks][nt] = ld16(wb + ((ks >> 1) * C1 + nt * 16) * C2 + 32 * (ks & 1));
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) {
+    if (ks + D3_PF < 18) {
+      const int kn = ks + D3_PF;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) Bq[kn][nt] = ld16(wb + ((kn >> 1) * C1 + nt * 16) * C2 + 32 * (kn & 1));
+    }
+    const int t = ks >> 1, co0 = 32 * (ks & 1);
+    const int toff = (t / 3) * DG_TCOLS + (t % 3);
+    const int ch = (co0 >> 3) + kg;
+    bf16x8 A[D3_MT];
+#pragma unroll
+    for (int i = 0; i < D3_MT; ++i) {
+      const int row = qbase[i] - toff;
+      A[i] = ld16(dys + row * C2 + ((ch ^ swz8(row)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < D3_MT; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bq[ks][nt], acc[i][nt]);
+  }
+
+  // ---- conv1 ReLU mask + conv1 weight/bias gradient MFMA (as conv2_dgrad_kernel)
+  floatx4 dw[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  {
+    const int tap = lane & 15, ty = tap / 3, tx = tap - 3 * ty;
+#pragma unroll
+    for (int i = 0; i < D3_MT; ++i) {
+      short4_t ax, bd[2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 16 * (wave + 4 * i) + 4 * kg + j;
+        const int qc = q < npix ? q : npix - 1;
+        const int py = qc / H1, px = qc - py * H1;
+        const float xv = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
+        ax[j] = (short)f2bf(xv);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const uint16_t av = (uint16_t)(a1v[i][j] >> (16 * nt));
+          const float d = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
+          bd[nt][j] = (short)f2bf(d);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) dw[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ax, bd[nt], dw[nt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = 4 * kg + r;
+      if (t < 10) red[(wave * 32 + nt * 16 + m) * 10 + t] = dw[nt][r];
+    }
+  __syncthreads();
+  for (int e = tid; e < 320; e += 256) {
+    const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
+    a.c1part[((int64_t)b * 3 + strip) * 320 + e] = s;
+  }
+}
+
+// read per call (host, at enqueue / capture time) so a process can compare both forms
+static int dgrad_strips() {
+  const char* e = getenv("MNIST_AMD_DGRAD3");
+  return (e && e[0] == '0') ? 4 : 3;
+}
+int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
+
 // dgrad (workgroups [0, 4B), same order as conv2_dgrad_kernel's (strip, b) grid) + the conv2 slab
 // reduce and Adadelta step (workgroups [4B, 4B + RED_W2_PARTS)).  Workgroups are dispatched in id
 // order, so the reduce parts take the slots of dgrad's last partial round (800 WGs on 512 slots at
@@ -452,6 +639,7 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, in
 static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
 
 void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s) {
+  if (c.c1_rows != 4 * B) throw std::runtime_error("conv_dgrad_update: needs the 4-strip dgrad (c1_rows = 4B)");
   hipLaunchKernelGGL(conv2_dgrad_update_kernel, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
   launch_c1_prereduce(c, B, s);
 }
@@ -490,11 +678,16 @@ __global__ __launch_bounds__(256) void c1_prereduce_kernel(const float* __restri
 }
 
 static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
-  if (a.c1red) hipLaunchKernelGGL(c1_prereduce_kernel, dim3(C1_PRE_SLABS), dim3(256), 0, s, a.c1part, 4 * B, a.c1red);
+  if (a.c1red) hipLaunchKernelGGL(c1_prereduce_kernel, dim3(C1_PRE_SLABS), dim3(256), 0, s, a.c1part, a.c1_rows, a.c1red);
 }
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
+  if (a.c1_rows == 3 * B)
+    hipLaunchKernelGGL(conv2_dgrad3_kernel, dim3(3, B), dim3(256), 0, s, a, B);
+  else if (a.c1_rows == 4 * B)
+    hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
+  else
+    throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
   launch_c1_prereduce(a, B, s);
 }
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {

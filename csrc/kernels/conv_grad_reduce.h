@@ -4,7 +4,7 @@
 // thread issues all of its float4 loads before the first add:
 //   [0, 289): conv2 weight+bias slab columns, 16 float4 columns x 16 slab slices per WG
 //             (<= 16 loads in flight per thread for G <= 256), fixed-order LDS tree over slices
-//   [289, 309): conv1 weight+bias, 4 float4 columns x 64 slices of the 4*B dgrad partials (or of
+//   [289, 309): conv1 weight+bias, 4 float4 columns x 64 slices of the c1_rows dgrad partials (or of
 //               their C1_PRE_SLABS group sums, ConvBwdArgs::c1red)
 // Each final (scaled) value is handed to sink(flat_element_index, value).
 #pragma once
@@ -83,7 +83,7 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
     }
   } else {
     const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
-    const int nslab = a.c1red ? C1_PRE_SLABS : 4 * B;
+    const int nslab = a.c1red ? C1_PRE_SLABS : a.c1_rows;
     const float4* src = reinterpret_cast<const float4*>(a.c1red ? a.c1red : a.c1part) + col;
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {

@@ -197,18 +197,8 @@ void Engine::enqueue_step(int batch, bool last) {
                       w1t_in_alt_ ? buf_.w1t : w1t_alt_};
     w1t_in_alt_ = !w1t_in_alt_;
   }
-  // schedule 3: only roles C + B of fc_bwd (dW2 / loss, and the dy records the conv backward
-  // needs) stay on the critical path; role A (dW1, needed only by the fc all-reduce / update) runs on
-  // the comm stream, released by this launch's start (counter [5])
-  const bool split_fcbwd = sched3 && split_fc_bwd_ && !fuse_fc && fc_bwd_splits(B) == 1;
   phase_begin("bwd_fc");
-  if (split_fcbwd) {
-    FcBwdArgs f0 = fb;
-    f0.signal_ctr = sync_ + 5;
-    launch_fc_bwd_part(f0, B, Bp, 0, compute_);
-  } else {
-    launch_fc_bwd(fb, B, Bp, compute_);
-  }
+  launch_fc_bwd(fb, B, Bp, compute_);
   phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
@@ -216,7 +206,8 @@ void Engine::enqueue_step(int batch, bool last) {
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
-  if (4 * B > C1_PRE_MIN_SLABS) cb.c1red = c1red_;          // large batch: conv1 partials pre-reduced
+  cb.c1_rows = (local3 && dgrad_update_) ? 4 * B : conv_dgrad_c1_rows(B);   // dgrad_update: 4-strip dgrad
+  if (cb.c1_rows > C1_PRE_MIN_SLABS) cb.c1red = c1red_;     // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
   if (sched3) {
@@ -228,10 +219,6 @@ void Engine::enqueue_step(int batch, bool last) {
     launch_conv_wgrad(cbs, B, compute_);
     phase_end();
     phase_begin("allreduce_fc+update");
-    if (split_fcbwd) {
-      launch_stream_wait(sync_ + 5, sync_ + 1, 1, sync_ + 2, comm_stream_);   // this step's fc_bwd started
-      launch_fc_bwd_part(fb, B, Bp, 1, comm_stream_);                          // role A: dW1, db1
-    }
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
     if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);

@@ -101,8 +101,6 @@ class Engine {
   // single GPU: run the fc Adadelta step on the comm stream, overlapped with the conv backward, with
   // the schedule-3 device-counter hand-offs (needs probe_stream_handoff() to pass)
   void set_overlap_fc_update(bool on) { overlap_fc_update_ = on; }
-  // schedule 3 (incl. the single-GPU overlap): fc_bwd's role A (dW1) on the comm stream
-  void set_split_fc_bwd(bool on) { split_fc_bwd_ = on; }
   // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
   // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
   void set_dgrad_update(bool on) { dgrad_update_ = on; }
@@ -161,7 +159,6 @@ class Engine {
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
-  bool split_fc_bwd_ = true;
   bool dgrad_update_ = true;
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)

@@ -106,9 +106,6 @@ class FusedTrainer:
         self.overlap_fc = (comm is None and world_size == 1 and not fuse_fc_update and not concurrent
                            and os.environ.get("MNIST_AMD_OVERLAP_FC", "1") == "1")
         self.engine.set_overlap_fc_update(self.overlap_fc)
-        # schedule 3: fc_bwd's dW1 role on the comm stream (opt-in MNIST_AMD_SPLIT_FCBWD=1; bitwise
-        # equal, measured 82.7 -> 82.9-83.1 us/step: role A then competes with role B / conv2_wgrad)
-        self.engine.set_split_fc_bwd(os.environ.get("MNIST_AMD_SPLIT_FCBWD", "0") == "1")
         # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
         # (opt-in MNIST_AMD_DGRAD_UPDATE=1, bitwise equal; measured 81.6-82.2 vs 80.9-81.8 us/step)
         self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "0") == "1")
@@ -400,7 +397,7 @@ class FusedTrainer:
         dev_s = None
         if sync:
             self.compute.synchronize()
-            if self.xgmi is not None or self.comm is not None:
+            if self.xgmi is not None or self.comm is not None or self.overlap_fc:
                 self.check_errors()        # fail at the first bad epoch, not after the last one
             dev_s = ev0.elapsed_time(ev1) / 1000.0
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged, dev_s)

@@ -237,3 +237,26 @@ def test_ranks_per_device_detection_gloo():
         p.join(60)
     expect = [(False, 1), (True, 3), (False, 1), (True, 3), (True, 2)]
     assert [r[1] for r in res] == [expect] * world
+
+
+def test_trainer_check_errors_raises_through_engine():
+    """The per-epoch device error check (hand-off / xGMI stage timeouts) surfaces the engine's
+    error as an exception on the host (fake engine: no GPU needed)."""
+    from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+
+    class _Engine:
+        def __init__(self, err):
+            self.err, self.calls = err, 0
+
+        def check_errors(self):
+            self.calls += 1
+            if self.err:
+                raise RuntimeError(self.err)
+
+    t = object.__new__(FusedTrainer)
+    t.engine = _Engine(None)
+    t.check_errors()
+    assert t.engine.calls == 1
+    t.engine = _Engine("xgmi stage timeout: kernel fc_fused stage 1 peer 3 wg 17")
+    with pytest.raises(RuntimeError, match="stage timeout"):
+        t.check_errors()

@@ -179,27 +179,12 @@ def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch)
     assert torch.equal(ms_s.w1t, ms_o.w1t) and torch.equal(ms_s.w2f, ms_o.w2f)
 
 
-def test_fc_bwd_role_split_bitwise_equal(cuda_device, monkeypatch):
-    """MNIST_AMD_SPLIT_FCBWD=1 (opt-in): fc_bwd's dW1 role on the comm stream under schedule 3 gives
-    the same bits as the one-launch fc_bwd."""
-    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(11))
-    monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "0")
-    _, ms_a, ta = _trainer(cuda_device, graph_steps=4)
-    monkeypatch.setenv("MNIST_AMD_SPLIT_FCBWD", "1")
-    _, ms_b, tb = _trainer(cuda_device, graph_steps=4)
-    assert ta.overlap_fc and tb.overlap_fc
-    ta.train_epoch(1, idx)
-    tb.train_epoch(1, idx)
-    tb.synchronize()
-    torch.cuda.synchronize()
-    assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
-
-
 def test_dgrad_update_bitwise_equal(cuda_device, monkeypatch):
     """MNIST_AMD_DGRAD_UPDATE (default): the conv2 slab reduce + update as extra workgroups of the
     dgrad launch (w2d ping-pong across steps, odd graph chunks end on the alternate copy) gives the
     bits of the separate step-tail launch; the eval after training sees the current shadows."""
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(13))
+    monkeypatch.setenv("MNIST_AMD_DGRAD3", "0")          # the dgrad-launch update rides the 4-strip dgrad
     monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "0")
     _, ms_a, ta = _trainer(cuda_device, graph_steps=3)
     monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "1")
@@ -219,20 +204,23 @@ def test_large_batch_conv1_prereduce_matches_functional(cuda_device):
     from pytorch_mnist_ddp_amd.engine.state import FLAG_NO_DROPOUT
     from pytorch_mnist_ddp_amd.ops import functional as Fk
     B = 512
-    torch.manual_seed(1)
-    net = Net()
+
+    def fresh_net():
+        torch.manual_seed(1)
+        return Net()
+
     tr = load_mnist(synthetic_data=True, train=True, synthetic_size=B, verbose=False)
     idx = torch.arange(B)
     grads = []
     for _ in range(2):
-        ms = ModelState(net, cuda_device, lr=1.0)
+        ms = ModelState(fresh_net(), cuda_device, lr=1.0)
         t = FusedTrainer(ms, tr, None, B, 1, num_samples=B, seed=1, graph_steps=0, dropout=False)
         t.train_epoch(1, idx)
         t.synchronize()
         torch.cuda.synchronize()
         grads.append(ms.grad.clone())
     assert torch.equal(grads[0], grads[1])
-    ms2 = ModelState(net, cuda_device, lr=1.0)
+    ms2 = ModelState(fresh_net(), cuda_device, lr=1.0)
     u8 = tr.images.reshape(B, -1).contiguous().to(cuda_device)
     lab = tr.targets.to(torch.int32).to(cuda_device)
     buf = Fk.StepBuffers.allocate(B, cuda_device)
@@ -243,3 +231,25 @@ def test_large_batch_conv1_prereduce_matches_functional(cuda_device):
     for name in g_fn:
         err = ((g_eng[name] - g_fn[name]).norm() / g_fn[name].norm().clamp_min(1e-30)).item()
         assert err < 1e-4, (name, err)
+
+
+@pytest.mark.parametrize("B", [200, 512])
+def test_dgrad_strip_forms_agree(cuda_device, monkeypatch, B):
+    """conv2_dgrad in 3 strips (9/9/8 rows, conv2 weights from L2) and in 4 strips (7 rows, weights in
+    LDS): identical per-pixel math; only the conv1 gradient partials are grouped differently, so the
+    trained parameters agree to fp32 summation-order level."""
+    idx = torch.randperm(B * 4, generator=torch.Generator().manual_seed(17))
+    out = {}
+    for form in ("0", "1"):
+        monkeypatch.setenv("MNIST_AMD_DGRAD3", form)
+        _, ms, t = _trainer(cuda_device, graph_steps=2, n_train=B * 4, B=B, dropout=False)
+        t.train_epoch(1, idx)
+        t.synchronize()
+        torch.cuda.synchronize()
+        out[form] = (ms.param.clone(), t.loss_log.clone())
+    p4, l4 = out["0"]
+    p3, l3 = out["1"]
+    assert torch.isfinite(p3).all()
+    rel = ((p3 - p4).norm() / p4.norm()).item()
+    assert rel < 1e-5, rel
+    assert (l3 - l4).abs().max().item() < 1e-3
