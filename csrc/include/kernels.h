@@ -144,7 +144,8 @@ struct ConvBwdArgs {
   int c1_rows;                // conv1 partial rows the dgrad launch writes: conv_dgrad_c1_rows(B)
 };
 // 4B (4 strips of 7 rows per image, 2 workgroups per CU) or 3B (3 strips of 9/9/8 rows, conv2
-// weights read from L2 instead of LDS: 3 workgroups per CU, one round at B <= 256); MNIST_AMD_DGRAD3
+// weights read from L2 instead of LDS: 3 workgroups per CU, one round at B <= 256; opt-in
+// MNIST_AMD_DGRAD3=1, slower: see docs/PERF_NOTES.md)
 int conv_dgrad_c1_rows(int B);
 constexpr int C1_PRE_SLABS = 256;
 constexpr int C1_PRE_MIN_SLABS = 1024;    // engine: pre-reduce when c1_rows exceeds this

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) 
 }
 
 // --------------------------------------------------------------------------------------------
-// conv2_dgrad, 3-strip form: WG = image x strip of 9/9/8 conv1 rows.  The conv2 weights' B fragments
+// conv2_dgrad, 3-strip form (opt-in MNIST_AMD_DGRAD3=1): WG = image x strip of 9/9/8 conv1 rows.  The conv2 weights' B fragments
 // come straight from L2 (w2d is 36.9 KB, L2-resident; each wave streams it once per strip with a
 // 4-k-step register prefetch) instead of an LDS copy, so a workgroup needs only the dy tile (11 x 28
 // pixels x 64 ch) + input rows + the reduction scratch: 45.8 KB -> 3 workgroups per CU, and the 3B
@@ -439,10 +439,12 @@ __global__ __launch_bounds__(256, 3) void conv2_dgrad3_kernel(ConvBwdArgs a, int
   }
 }
 
-// read per call (host, at enqueue / capture time) so a process can compare both forms
+// read per call (host, at enqueue / capture time) so a process can compare both forms.  Default: the
+// 4-strip LDS form (measured B = 200: 81.2-81.5 vs 84.6-84.8 us/step, B = 8192: 1326 vs 1377 us):
+// streaming w2d through L1 (32 KB, smaller than w2d) costs more than the occupancy it buys.
 static int dgrad_strips() {
   const char* e = getenv("MNIST_AMD_DGRAD3");
-  return (e && e[0] == '0') ? 4 : 3;
+  return (e && e[0] == '1') ? 3 : 4;
 }
 int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
 
