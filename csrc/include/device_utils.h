@@ -5,6 +5,11 @@
 
 namespace mnist {
 
+// Zero StepState for kernels launched without one (module API): `st = a.state ? a.state : &g_zero_state`
+// keeps the state load unconditional.  A load under a branch ends in vmcnt(0) at the join, which
+// serialises every load issued before it.
+static __device__ StepState g_zero_state;
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((ext_vector_type(4))) float floatx4;
@@ -102,6 +107,12 @@ struct NormLut {
 };
 __constant__ constexpr NormLut kNormLut{};
 __device__ __forceinline__ float normalize_u8(uint8_t v) { return kNormLut.v[v]; }
+// The same value from IEEE fp32 arithmetic (correctly rounded division, contraction off: bitwise the
+// table entry): for a pixel whose load should not grow a dependent table load in a latency chain.
+__device__ __forceinline__ float normalize_u8_alu(uint32_t v) {
+#pragma clang fp contract(off)
+  return ((float)v / 255.0f - MNIST_MEAN) / MNIST_STD;
+}
 
 // One Adadelta element update (torch/optim/adadelta.py, foreach order: mul_, addcmul_, add+sqrt,
 // add+sqrt, div_, mul_, mul_, addcmul_, add_), every operation individually rounded (FMA

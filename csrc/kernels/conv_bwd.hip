@@ -88,6 +88,10 @@ int conv_wgrad_groups(int B) {
 }
 
 // --------------------------------------------------------------------------------------------
+// input-row source of the conv1 gradient: pre-gathered epoch rows, rows by index, or fp32 module input
+enum DgX { DGX_PRE = 0, DGX_IDX = 1, DGX_XIN = 2 };
+
+template <int XM>
 __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int strip, int b, unsigned char* smem) {
   uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
   uint16_t* w2ds = reinterpret_cast<uint16_t*>(smem + DYS_BYTES);
@@ -102,61 +106,63 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
   const int r0 = strip * DG_ROWS;
   const int nrows = (strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS;   // 7,7,7,5
   const int npix = nrows * H1;
-  const int step = a.state ? a.state->step : 0;
+  const StepState* st = a.state ? a.state : &g_zero_state;
+  const int step = st->step;                      // oldest load: the input-row chain hangs off it
 
-  // ---- phase 0: stage the padded dy tile (rows r0-2..r0+6, cols -2..25), w2d and the input rows.
-  // All global loads are independent 16-B loads issued before any LDS store.
+  // ---- phase 0: stage the padded dy tile (rows r0-2..r0+6, cols -2..25) and w2d: every load is
+  // unconditional (clamped address, validity applied at the LDS store) so all of them are in flight
+  // at once.  The input row (state -> [index] -> pixel, a dependent chain) is loaded last and only
+  // stored to LDS after the MFMA loop - the conv1 gradient epilogue is its first reader.
+  float xv;                                       // fp32 module input, or the raw pixel byte
   {
     constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
+    uint4 w[9];
+    const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
     uint4 v[8];
     uint2 rt[8];
-    int qv[8];
-    const uint4 z = {0u, 0u, 0u, 0u};
+    uint32_t okm = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int c = tid + 256 * k;
       const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
       const int y = r0 - 2 + ly, x = col - 2;
-      v[k] = z;
-      rt[k] = uint2{0xFFFFFFFFu, 0xFFFFFFFFu};                    // no channel matches -> zero chunk
-      qv[k] = ((y & 1) << 1) | (x & 1);
-      if (c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2) {
-        const uint8_t* rec = dyc_record(a.dyc, b, y, x);
-        v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
-        rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
-      }
-    }
-    uint4 w[9];
-    const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
-    if (a.xin) {
-      const float* srcf = a.xin + (int64_t)b * (IMG * IMG);
-      for (int e = tid; e < DG_TROWS * IMG; e += 256) {
-        const int row = r0 + e / IMG;
-        xs[e] = (row < IMG) ? srcf[r0 * IMG + e] : 0.0f;
-      }
-    } else {
-      const int64_t row = (int64_t)step * a.idx_step_stride + b;   // idx == nullptr: pre-gathered epoch rows
-      const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
-      const uint8_t* src8 = a.data_u8 + (int64_t)img * (IMG * IMG);
-      for (int e = tid; e < DG_TROWS * IMG; e += 256) {
-        const int row = r0 + e / IMG;
-        xs[e] = (row < IMG) ? normalize_u8(src8[r0 * IMG + e]) : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = tid + 256 * k;
-      if (c < NCH) {
-        const int row = c >> 3, c8 = c & 7;
-        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = dyc_expand(v[k], rt[k], qv[k]);
-      }
+      const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
+      okm |= (ok ? 1u : 0u) << k;
+      const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
+      v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
+      rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int c = tid + 256 * i, row = c >> 3, c8 = c & 7;
       reinterpret_cast<uint4*>(w2ds)[row * 8 + (c8 ^ swz8(row))] = w[i];
+    }
+    {
+      const int e = tid < DG_TROWS * IMG ? tid : 0;   // DG_TROWS * IMG = 252 <= 256
+      const bool okx = tid < DG_TROWS * IMG && r0 + e / IMG < IMG;
+      const int off = r0 * IMG + (okx ? e : 0);
+      if constexpr (XM == DGX_XIN) {
+        xv = a.xin[(int64_t)b * (IMG * IMG) + off];
+      } else {
+        const int64_t row = (int64_t)step * a.idx_step_stride + b;
+        const int64_t img = (XM == DGX_IDX) ? (int64_t)a.idx[row] : row;
+        xv = __builtin_bit_cast(float, (uint32_t)a.data_u8[img * (IMG * IMG) + off]);
+      }
+      if (!okx) xv = (XM == DGX_XIN) ? 0.0f : __builtin_bit_cast(float, 0x100u);   // 0x100: "outside"
+    }
+    const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = tid + 256 * k;
+      if (c < NCH) {
+        const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
+        const int y = r0 - 2 + ly, x = col - 2;
+        const int row = c >> 3, c8 = c & 7;
+        const uint4 d = ((okm >> k) & 1u) ? dyc_expand(v[k], rt[k], ((y & 1) << 1) | (x & 1)) : z;
+        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
+      }
     }
   }
   __syncthreads();
@@ -213,6 +219,16 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
       for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bf[nt], acc[i][nt]);
   }
 
+  if (tid < DG_TROWS * IMG) {                     // input rows: first read by the epilogue below
+    float x = xv;
+    if (XM != DGX_XIN) {
+      const uint32_t u = __builtin_bit_cast(uint32_t, xv);
+      x = u > 0xFFu ? 0.0f : normalize_u8_alu(u);
+    }
+    xs[tid] = x;
+  }
+  __syncthreads();
+
   // ---- phase 3: conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
   // second, tiny MFMA: D[tap][ci] = sum_px X[px][tap] * d[px][ci] on v_mfma_f32_16x16x16_bf16
   // (row 9 of X = ones -> the bias gradient).  That instruction's B-operand layout (lane l holds
@@ -257,9 +273,10 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
   }
 }
 
+template <int XM>
 __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
-  dgrad_body(a, B, blockIdx.x, blockIdx.y, smem);
+  dgrad_body<XM>(a, B, blockIdx.x, blockIdx.y, smem);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -454,11 +471,12 @@ int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
 // B = 200) instead of a launch of their own after dgrad.  Reads only wgrad's slabs (complete at
 // launch); writes conv2 params / state / grads and the shadows u.w2f, u.w2d (!= a.w2d, which the
 // dgrad workgroups read).
+template <int XM>
 __global__ __launch_bounds__(256) void conv2_dgrad_update_kernel(ConvBwdArgs a, AdadeltaArgs u, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
   const int bid = blockIdx.x;
   if (bid < 4 * B) {
-    dgrad_body(a, B, bid & 3, bid >> 2, smem);
+    dgrad_body<XM>(a, B, bid & 3, bid >> 2, smem);
     return;
   }
   conv_reduce_update(u, a, B, bid - 4 * B, reinterpret_cast<float4*>(smem));
@@ -472,33 +490,36 @@ __device__ __forceinline__ int a1_row_of(int R) { return R + 2 * (R / H2); }
 struct WgradChunk {
   uint4 vd[WDY_V], va[WA1_V];
   uint2 rt[WDY_V];
+  uint32_t okd, oka;          // validity bits, applied at the LDS store (not on the loaded values)
 };
 
 // Issue the global loads of chunk [c0, c1) into registers (zeros past the valid rows, so every LDS
-// byte of the buffer is rewritten and finite).
+// byte of the buffer is rewritten and finite).  The loads are unconditional (clamped to the chunk's
+// first element, the value masked after): loads under a branch make the waitcnt pass fall back to
+// vmcnt(0), which pulled the wait for this prefetch up into the middle of the MFMA loop.
 __device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1, int tid, WgradChunk& k) {
   const int ndy = (c1 - c0) * H2 * 8;                               // valid 16-B chunks of dy
   const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
   const int na1 = (A1 - A0) * H1 * 4;                               // valid 16-B chunks of a1
   const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
-  const uint4 z = {0u, 0u, 0u, 0u};
+  k.okd = k.oka = 0;
 #pragma unroll
   for (int i = 0; i < WDY_V; ++i) {
-    const int c = tid + WG_THREADS * i;
-    k.vd[i] = z;
-    k.rt[i] = uint2{0xFFFFFFFFu, 0xFFFFFFFFu};
-    if (c < ndy) {                                  // dense chunk (pixel c>>3, channels 8(c&7)..)
-      const int pix = c >> 3, R = c0 + pix / H2, x = pix - (pix / H2) * H2;
-      const int bimg = R / H2, y = R - bimg * H2;
-      const uint8_t* rec = dyc_record(a.dyc, bimg, y, x);
-      k.vd[i] = *reinterpret_cast<const uint4*>(rec + (c & 7) * 16);
-      k.rt[i] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + (c & 7) * 8);
-    }
+    const int c0i = tid + WG_THREADS * i;
+    const bool ok = c0i < ndy;
+    k.okd |= (ok ? 1u : 0u) << i;
+    const int c = ok ? c0i : 0;                     // dense chunk (pixel c>>3, channels 8(c&7)..)
+    const int pix = c >> 3, R = c0 + pix / H2, x = pix - (pix / H2) * H2;
+    const int bimg = R / H2, y = R - bimg * H2;
+    const uint8_t* rec = dyc_record(a.dyc, bimg, y, x);
+    k.vd[i] = *reinterpret_cast<const uint4*>(rec + (c & 7) * 16);
+    k.rt[i] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + (c & 7) * 8);
   }
 #pragma unroll
   for (int i = 0; i < WA1_V; ++i) {
     const int c = tid + WG_THREADS * i;
-    k.va[i] = (c < na1) ? asrc[c] : z;
+    k.oka |= (c < na1 ? 1u : 0u) << i;
+    k.va[i] = asrc[c < na1 ? c : 0];
   }
 }
 
@@ -509,7 +530,8 @@ __device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0,
   for (int i = 0; i < WDY_V; ++i) {
     const int c = tid + WG_THREADS * i, pix = c >> 3;
     const int R = c0 + pix / H2, x = pix - (pix / H2) * H2;
-    const uint4 d = dyc_expand(k.vd[i], k.rt[i], ((R & 1) << 1) | (x & 1));   // H2 even: y&1 == R&1
+    const uint4 d = ((k.okd >> i) & 1u) ? dyc_expand(k.vd[i], k.rt[i], ((R & 1) << 1) | (x & 1))   // H2 even: y&1 == R&1
+                                        : uint4{0u, 0u, 0u, 0u};
     dys[pix * 8 + ((c & 7) ^ swz_dy(pix))] = d;
     const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
@@ -521,7 +543,7 @@ __device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0,
 #pragma unroll
   for (int i = 0; i < WA1_V; ++i) {
     const int c = tid + WG_THREADS * i;
-    if (c < WA1_BYTES / 16) a1s[c] = k.va[i];
+    if (c < WA1_BYTES / 16) a1s[c] = ((k.oka >> i) & 1u) ? k.va[i] : uint4{0u, 0u, 0u, 0u};
   }
 }
 }  // namespace
@@ -642,7 +664,10 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
 
 void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s) {
   if (c.c1_rows != 4 * B) throw std::runtime_error("conv_dgrad_update: needs the 4-strip dgrad (c1_rows = 4B)");
-  hipLaunchKernelGGL(conv2_dgrad_update_kernel, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
+  if (c.idx)
+    hipLaunchKernelGGL(conv2_dgrad_update_kernel<DGX_IDX>, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
+  else
+    hipLaunchKernelGGL(conv2_dgrad_update_kernel<DGX_PRE>, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
   launch_c1_prereduce(c, B, s);
 }
 
@@ -686,8 +711,12 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   if (a.c1_rows == 3 * B)
     hipLaunchKernelGGL(conv2_dgrad3_kernel, dim3(3, B), dim3(256), 0, s, a, B);
+  else if (a.c1_rows == 4 * B && a.xin)
+    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_XIN>, dim3(4, B), dim3(256), 0, s, a, B);
+  else if (a.c1_rows == 4 * B && a.idx)
+    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_IDX>, dim3(4, B), dim3(256), 0, s, a, B);
   else if (a.c1_rows == 4 * B)
-    hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(4, B), dim3(256), 0, s, a, B);
+    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_PRE>, dim3(4, B), dim3(256), 0, s, a, B);
   else
     throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
   launch_c1_prereduce(a, B, s);

@@ -238,6 +238,12 @@ __device__ __forceinline__ void log_softmax10(const float* x, float* lp) {
 }
 }  // namespace
 
+// Training head.  Every load of the row is issued up front - the KS split-K partial sums, fc1 bias,
+// fc2 weights and bias, the label - with no load under a branch (IDX / KS are template parameters):
+// a branch-guarded load ends in vmcnt(0), which used to finish the label + bias round trip before
+// the partial-sum loads even went out.  Arithmetic (order and expression forms) is that of
+// head_forward_row / the module head, so the results are bitwise unchanged.
+template <int KS, bool IDX>
 __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -253,12 +259,47 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   const uint64_t seed = a.state->seed;
   const uint64_t off = a.state->rng_base + 2ull * (uint64_t)step + 1ull;
   const bool no_drop = (a.state->flags & STEP_FLAG_NO_DROPOUT) != 0;
-  // the label is two dependent loads (index -> label): issue them before the row's 64 partial-sum
-  // loads so their latency overlaps instead of trailing the softmax
-  const int64_t lrow = (int64_t)step * a.idx_step_stride + b;     // idx == nullptr: pre-gathered labels
-  const int y = a.dlogp ? 0 : a.labels[a.idx ? (int64_t)a.idx[lrow] : lrow];
+  const int64_t lrow = (int64_t)step * a.idx_step_stride + b;     // !IDX: pre-gathered labels
+  const int32_t* lab = a.labels ? a.labels : &g_zero_state.step;   // module API (dlogp): no labels
+  int64_t li = lrow;
+  if constexpr (IDX) li = a.idx[lrow];
+  const int y_raw = lab[a.labels ? li : 0];
+  float part[KS][2], bf1[2], w2v[NCLS][2];
+#pragma unroll
+  for (int c = 0; c < KS; ++c)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) part[c][j] = a.z1part[((int64_t)c * B + b) * NH + lane + 64 * j];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bf1[j] = a.b_fc1[lane + 64 * j];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2v[c][j] = a.w_fc2[c * NH + lane + 64 * j];
   HeadRow r;
-  head_forward_row(a, B, b, lane, true, no_drop, seed, off, r);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = lane + 64 * j;
+    float z = bf1[j];
+    float s = 0.f;                                   // partial sums in fixed chunk order
+#pragma unroll
+    for (int c = 0; c < KS; ++c) s += part[c][j];
+    z += s;
+    r.z[j] = z;
+    float h = fmaxf(z, 0.0f);
+    bool keep = true;
+    if (!no_drop) {
+      const u32x4 w = dropout_block(seed, off, ((uint64_t)b * NH + o) >> 4);
+      keep = dropout_byte(w, o & 15) < KEEP2_THR8;
+    }
+    h = keep ? (no_drop ? h : h * (1.0f / KEEP2)) : 0.0f;
+    r.keep[j] = keep;
+    r.h[j] = h;
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float v = r.h[0] * w2v[c][0] + r.h[1] * w2v[c][1];
+    r.logit[c] = wave_sum(v) + a.b_fc2[c];
+  }
   float lp[NCLS];
   log_softmax10(r.logit, lp);
   float dl[NCLS];
@@ -270,6 +311,7 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) dl[c] = go[c] - expf(lp[c]) * sg;
   } else {
+    const int y = y_raw;
     if (lane == 0) a.loss_rows[b] = -lp[y];
     // nll(mean) backward: go[c] = -[c==y]/B; log_softmax backward: go - exp(lp) * sum(go)
 #pragma unroll
@@ -283,7 +325,7 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
     const int o = lane + 64 * j;
     float dh = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) dh = __builtin_fmaf(dl[c], a.w_fc2[c * NH + o], dh);
+    for (int c = 0; c < NCLS; ++c) dh = __builtin_fmaf(dl[c], w2v[c][j], dh);
     const float dz = (r.keep[j] && r.z[j] > 0.0f) ? (no_drop ? dh : dh * (1.0f / KEEP2)) : 0.0f;
     a.dz1[(int64_t)b * NH + o] = f2bf(dz);
     a.h_bf[(int64_t)b * NH + o] = f2bf(r.h[j]);
@@ -358,7 +400,14 @@ static int head_waves() {
 
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {
   const int w = Bp >= 2048 ? 4 : head_waves();   // (Bp is a multiple of 32)
-  hipLaunchKernelGGL(head_train_kernel, dim3(Bp / w), dim3(64 * w), 0, s, a, B);
+  const dim3 g(Bp / w), t(64 * w);
+  if (fc1_ksplit(B) == FC1_KSPLIT) {
+    if (a.idx) hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, true>), g, t, 0, s, a, B);
+    else hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, false>), g, t, 0, s, a, B);
+  } else {
+    if (a.idx) hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT_BIG, true>), g, t, 0, s, a, B);
+    else hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT_BIG, false>), g, t, 0, s, a, B);
+  }
 }
 void launch_head_eval(const HeadArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(head_eval_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B);
@@ -576,7 +625,8 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
   const int m = lane & 15, kg = lane >> 4;
   const int bb = rb / ROLE_B_SBLOCKS, sb = rb - bb * ROLE_B_SBLOCKS;
   const int s0 = sb * 4;                               // 4 consecutive pooled positions (row-major 12x12)
-  const float dscale = (a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT)) ? 1.0f : (1.0f / KEEP1);
+  const StepState* st = a.state ? a.state : &g_zero_state;   // unconditional load (no vmcnt(0) join)
+  const float dscale = (st->flags & STEP_FLAG_NO_DROPOUT) ? 1.0f : (1.0f / KEEP1);
   // large batches (CACHE_W): this wave's w1 slice (pooled position s0 + wave, 64 channels, K = 128)
   // stays in VGPRs for all MR row tiles of the workgroup; small batches (MR = 1) stream it, which
   // keeps the kernel at 3 workgroups per CU
@@ -591,26 +641,41 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
   for (int t = 0; t < MR; ++t) {
     const int b0 = (bb * MR + t) * 16;
     if (b0 >= B) break;                                // workgroup-uniform
-    // pmask tile (4 consecutive pooled positions per (b, c) = one u32)
+    // Every load of the tile is issued before the first wait: the pmask words unconditionally
+    // (clamped row, value masked after) - loads under a branch each end in vmcnt(0), which turned
+    // the tile's staging into four dependent round trips.
+    uint32_t pmv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
-      uint32_t v = 0;
-      if (b0 + bl < B) v = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)(b0 + bl) * NFLAT + c * NPOOL + s0);
-      reinterpret_cast<uint32_t*>(pms)[idx] = v;
+      const int row = b0 + bl < B ? b0 + bl : B - 1;
+      pmv[k] = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)row * NFLAT + c * NPOOL + s0);
+    }
+    const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;   // rows < Bp: zero padding rows
+    bf16x8 Af[NH / 32], Bs[CACHE_W ? 1 : NH / 32][4];
+#pragma unroll
+    for (int ks = 0; ks < NH / 32; ++ks) {
+      Af[ks] = ld16(arow + ks * 32);
+      if (!CACHE_W) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          Bs[CACHE_W ? 0 : ks][nt] = ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = tid + 256 * k, bl = idx >> 6;
+      reinterpret_cast<uint32_t*>(pms)[idx] = b0 + bl < B ? pmv[k] : 0u;
     }
     floatx4 acc[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;
 #pragma unroll
     for (int ks = 0; ks < NH / 32; ++ks) {
-      const bf16x8 A = ld16(arow + ks * 32);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const bf16x8 Bf = CACHE_W ? Bw[CACHE_W ? ks : 0][nt]
-                                  : ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
-        acc[nt] = mfma16x16x32(A, Bf, acc[nt]);
+        const bf16x8 Bf = CACHE_W ? Bw[CACHE_W ? ks : 0][nt] : Bs[CACHE_W ? 0 : ks][nt];
+        acc[nt] = mfma16x16x32(Af[ks], Bf, acc[nt]);
       }
     }
     __syncthreads();

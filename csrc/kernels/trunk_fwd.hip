@@ -84,7 +84,11 @@ __device__ __forceinline__ int swz_a1(int col) { return col & 3; }
 __device__ __forceinline__ int swz_w2(int n) { return (4 - ((n >> 2) & 3)) & 3; }
 }  // namespace
 
-template <bool TRAIN, int NS>
+// input-row source: pre-gathered epoch rows, rows by index, or fp32 module input (a template
+// parameter so phase 0 has no load under a branch: such a load ends in vmcnt(0) at the join)
+enum TrunkX { TX_PRE = 0, TX_IDX = 1, TX_XIN = 2 };
+
+template <bool TRAIN, int NS, int XM>
 __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(TrunkFwdArgs a) {
   using K = TrunkCfg<NS>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[K::LDS];
@@ -98,11 +102,17 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
   const int tid = threadIdx.x;
   const int strip0 = blockIdx.x * NS;   // first strip of this workgroup
   const int b = blockIdx.y;             // row in batch
-  const int step = a.state ? a.state->step : 0;
+  // the whole step state read once at entry (phase 4's dropout key would otherwise be re-loaded
+  // after the phase-1 global stores, two dependent round trips at the tail)
+  const StepState* st = a.state ? a.state : &g_zero_state;   // unconditional state loads
+  const int step = st->step, st_flags = st->flags;
+  const uint64_t st_seed = st->seed, st_rng_base = st->rng_base;
   PHASE_MARK(0);
 
   // ---- phase 0: issue every global load first (input rows, conv2 weights, conv1 weights, conv2
-  // bias), then fill LDS: conv2 weights swizzled, input rows normalised to fp32.
+  // bias) - all unconditional, so the waits count exactly - then fill LDS: conv2 weights swizzled,
+  // input rows normalised to fp32 by IEEE arithmetic (bitwise the table; a table lookup would be a
+  // dependent load per pixel).
   const int c = tid & 3;                         // conv1: fixed 8-channel chunk per thread
   float bias2[4];
   constexpr int PARKED = K::CHUNKS - K::EARLY;
@@ -118,11 +128,31 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
     if constexpr (PARKED == 2) wp1 = src[tid + K::THREADS * (K::EARLY + 1)];
     // conv1 weights [32][9] (72 float4) + bias (8 float4): 80 threads fetch them once per workgroup
     // (per-thread copies were 18 float4 loads x 768 threads of L1 traffic)
-    float4 w1v = {0.f, 0.f, 0.f, 0.f};
-    if (tid < 72) w1v = reinterpret_cast<const float4*>(a.w1c)[tid];
-    else if (tid < 80) w1v = reinterpret_cast<const float4*>(a.b1c)[tid - 72];
+    const float4 w1v = tid < 72 ? reinterpret_cast<const float4*>(a.w1c)[tid]
+                                : reinterpret_cast<const float4*>(a.b1c)[tid < 80 ? tid - 72 : 0];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) bias2[nt] = a.b2c[nt * 16 + (tid & 15)];
+    // input rows: pixel e = tid + THREADS*j, one coalesced byte (or float) load each
+    constexpr int NX = K::X_ROWS * IMG;
+    constexpr int XJ = (NX + K::THREADS - 1) / K::THREADS;   // 2
+    const int64_t xoff = (int64_t)strip0 * STRIP * IMG;
+    float xv[XJ];
+    if constexpr (XM == TX_XIN) {
+#pragma unroll
+      for (int j = 0; j < XJ; ++j) {
+        const int e = tid + K::THREADS * j;
+        xv[j] = a.xin[(int64_t)b * (IMG * IMG) + xoff + (e < NX ? e : 0)];
+      }
+    } else {
+      const int64_t row = (int64_t)step * a.idx_step_stride + b;
+      const int64_t img = (XM == TX_IDX) ? (int64_t)a.idx[row] : row;
+      const uint8_t* src8 = a.data_u8 + img * (IMG * IMG) + xoff;
+#pragma unroll
+      for (int j = 0; j < XJ; ++j) {
+        const int e = tid + K::THREADS * j;
+        xv[j] = __builtin_bit_cast(float, (uint32_t)src8[e < NX ? e : 0]);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < K::EARLY; ++i) {         // swizzle only permutes chunks inside a 64-B row
       const int ch = tid + K::THREADS * i;
@@ -138,31 +168,10 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
         w1s[(((ch >> 3) * 4 + ((ch & 7) >> 1)) * 10 + t) * 2 + (ch & 1)] = fv[e];
       }
     }
-    uint4 xv = {0u, 0u, 0u, 0u};
-    float4 xf = {0.f, 0.f, 0.f, 0.f};
-    constexpr int XCH = K::X_ROWS * IMG / 16;    // 16-byte chunks of the input rows (rows are 16-B aligned)
-    const int64_t xoff = (int64_t)strip0 * STRIP * IMG;
-    if (a.xin) {                                 // module API: fp32 input rows
-      if (tid < K::X_ROWS * IMG / 4)
-        xf = *reinterpret_cast<const float4*>(a.xin + (int64_t)b * (IMG * IMG) + xoff + tid * 4);
-    } else {
-      const int64_t row = (int64_t)step * a.idx_step_stride + b;   // idx == nullptr: pre-gathered epoch rows
-      const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
-      if (tid < XCH) xv = *reinterpret_cast<const uint4*>(a.data_u8 + img * (IMG * IMG) + xoff + tid * 16);
-    }
-    if (a.xin) {
-      if (tid < K::X_ROWS * IMG / 4) *reinterpret_cast<float4*>(xs + tid * 4) = xf;
-    } else if (tid < XCH) {
-      const uint32_t words[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float4 f;
-        f.x = normalize_u8((uint8_t)(words[k] & 0xFF));
-        f.y = normalize_u8((uint8_t)((words[k] >> 8) & 0xFF));
-        f.z = normalize_u8((uint8_t)((words[k] >> 16) & 0xFF));
-        f.w = normalize_u8((uint8_t)(words[k] >> 24));
-        *reinterpret_cast<float4*>(xs + tid * 16 + 4 * k) = f;
-      }
+    for (int j = 0; j < XJ; ++j) {
+      const int e = tid + K::THREADS * j;
+      if (e < NX) xs[e] = (XM == TX_XIN) ? xv[j] : normalize_u8_alu(__builtin_bit_cast(uint32_t, xv[j]));
     }
   }
   __syncthreads();
@@ -287,9 +296,9 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
 
   // ---- phase 4: dropout + coalesced stores.  One thread = 16 contiguous flat elements of one
   // channel = exactly one Philox block (3 per channel-strip).
-  const uint64_t seed = a.state ? a.state->seed : 0;
-  const uint64_t off = a.state ? a.state->rng_base + 2ull * (uint64_t)step : 0;
-  const bool drop = TRAIN && !(a.state && (a.state->flags & STEP_FLAG_NO_DROPOUT));
+  const uint64_t seed = st_seed;
+  const uint64_t off = st_rng_base + 2ull * (uint64_t)step;
+  const bool drop = TRAIN && !(st_flags & STEP_FLAG_NO_DROPOUT);
   if (tid < C2 * 3 * NS) {
     const int n = tid / (3 * NS), j16 = (tid - n * 3 * NS) * 16;
     const int flat = n * NPOOL + strip0 * WIN + j16;
@@ -333,17 +342,23 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
 
 int trunk_strips_per_wg(int B) { return B <= TRUNK_IMG_MAX_B ? 3 : 1; }
 
+template <bool TRAIN, int NS>
+static void launch_trunk(const TrunkFwdArgs& a, dim3 grid, hipStream_t s) {
+  if (a.xin)
+    hipLaunchKernelGGL((trunk_fwd_kernel<TRAIN, NS, TX_XIN>), grid, dim3(256 * NS), 0, s, a);
+  else if (a.idx)
+    hipLaunchKernelGGL((trunk_fwd_kernel<TRAIN, NS, TX_IDX>), grid, dim3(256 * NS), 0, s, a);
+  else
+    hipLaunchKernelGGL((trunk_fwd_kernel<TRAIN, NS, TX_PRE>), grid, dim3(256 * NS), 0, s, a);
+}
+
 void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s) {
   if (trunk_strips_per_wg(B) == 3) {
-    if (train)
-      hipLaunchKernelGGL((trunk_fwd_kernel<true, 3>), dim3(1, B), dim3(768), 0, s, a);
-    else
-      hipLaunchKernelGGL((trunk_fwd_kernel<false, 3>), dim3(1, B), dim3(768), 0, s, a);
+    if (train) launch_trunk<true, 3>(a, dim3(1, B), s);
+    else launch_trunk<false, 3>(a, dim3(1, B), s);
   } else {
-    if (train)
-      hipLaunchKernelGGL((trunk_fwd_kernel<true, 1>), dim3(3, B), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((trunk_fwd_kernel<false, 1>), dim3(3, B), dim3(256), 0, s, a);
+    if (train) launch_trunk<true, 1>(a, dim3(3, B), s);
+    else launch_trunk<false, 1>(a, dim3(3, B), s);
   }
 }
 

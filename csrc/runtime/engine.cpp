@@ -140,7 +140,11 @@ void Engine::enqueue_step(int batch, bool last) {
   const int B = batch, Bp = round_up(B, 32);
   const int stride = idx_stride_;
   float* P = buf_.param;
-  const float gscale = 1.0f / (float)world_;
+  // DDP averaging: each rank's head scales the loss gradient by 1/(world*B) and the all-reduce sums,
+  // so every row's bf16 gradient operands (dz1, dl) are bitwise those of the world-1 run on the
+  // world*B batch (scaling by 1/B and then by 1/world rounds the fp32 constant differently and flips
+  // bf16 ties: a systematic ~7e-6 gradient offset, tools/ddp_equivalence.py)
+  const float gscale = 1.0f;
 
   // pre-gathered epoch rows when available (one load level less on every step's critical path)
   const bool pre = buf_.epoch_u8 != nullptr;
@@ -180,7 +184,7 @@ void Engine::enqueue_step(int batch, bool last) {
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
   ha.labels = labels; ha.idx = idxp; ha.idx_step_stride = stride;
-  ha.state = buf_.state; ha.inv_batch = 1.0f / (float)B;
+  ha.state = buf_.state; ha.inv_batch = 1.0f / (float)(B * world_);
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
   launch_head_train(ha, B, Bp, compute_);
   phase_end();
@@ -207,7 +211,7 @@ void Engine::enqueue_step(int batch, bool last) {
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
   cb.c1_rows = (local3 && dgrad_update_) ? 4 * B : conv_dgrad_c1_rows(B);   // dgrad_update: 4-strip dgrad
-  if (cb.c1_rows > C1_PRE_MIN_SLABS) cb.c1red = c1red_;     // large batch: conv1 partials pre-reduced
+  if (cb.c1_rows > C1_PRE_MIN_SLABS && c1_prereduce_) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
   if (sched3) {

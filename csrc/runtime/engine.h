@@ -15,6 +15,7 @@
 // The fc-bucket all-reduce + its Adadelta update (98.4 % of parameters) overlap the whole conv
 // backward; conv2 wgrad overlaps conv2 dgrad.  With world_size == 1 the all-reduces are skipped.
 #pragma once
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <map>
@@ -169,6 +170,8 @@ class Engine {
   uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (fused fc update ping-pong)
   bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
   float* c1red_ = nullptr;          // conv1 partial group sums (large batches)
+  // MNIST_AMD_C1_PREREDUCE=0 turns the large-batch conv1 pre-reduce off (A/B, numerics checks)
+  bool c1_prereduce_ = [] { const char* e = getenv("MNIST_AMD_C1_PREREDUCE"); return !(e && e[0] == '0'); }();
   uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv split / dgrad_update ping-pong)
   bool w2d_in_alt_ = false;
   hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;

@@ -12,7 +12,12 @@ order flips.  Two checks: (a) the step-1 all-reduced gradient (separate-launch s
 materialised) against the world-1 gradient of the W*B batch, ||g_W - g_1|| / ||g_1|| <= max(1e-3,
 2 x noise) - Adadelta normalises its step, so gradient scale errors only show here; (b) parameters
 after S fused steps, ||p_W - p_1|| / ||p_1|| <= max(1e-3, 3 x noise).  The noise floors are the same
-world-1 runs with the rows of every batch permuted (shards in reverse order).
+world-1 runs perturbed only in fp32 summation order, the max over: the rows of every batch permuted
+(shards in reverse order; a full random permutation of each step's W*B rows) and a different
+decomposition of the same sums (the large-batch conv1 pre-reduce toggled).  W ranks at B rows and
+one rank at W*B rows run different kernel decompositions (fc1 split-K, fc_bwd K blocking, per-rank
+then cross-rank sums), so row permutations alone - which keep the decomposition - under-sample the
+order sensitivity of the first, nearly sign-like Adadelta steps.
 Also checked: every rank holds bitwise identical parameters, and the loss log matches per step.
 Exit code 0 = pass.  (Reference semantics: mnist_ddp.py:161-173 - DistributedSampler shards +
 DistributedDataParallel averaging.)
@@ -101,14 +106,27 @@ def worker(rank, world, port, args, q):
             p1, l1 = p1.cpu(), l1.cpu()
             # noise floor: the same world-1 batches with the shards in reverse order (a permutation of
             # the rows of every batch changes nothing but fp32 summation order / bf16 tie rounding)
-            p1r, l1r, _ = _train(torch, dev, 1, 0, W * B, S, stream.flip(1).reshape(-1), "rccl")
-            p1r, l1r = p1r.cpu(), l1r.cpu()
+            noise = lnoise = 0.0
+            gp = torch.Generator().manual_seed(7)
+            shuffled = torch.stack([st.reshape(-1)[torch.randperm(W * B, generator=gp)] for st in stream])
+            prev = os.environ.get("MNIST_AMD_C1_PREREDUCE")
+            for perm, pre in ((stream.flip(1), prev), (shuffled, prev), (stream, "0" if prev != "0" else "1")):
+                if pre is None:
+                    os.environ.pop("MNIST_AMD_C1_PREREDUCE", None)
+                else:
+                    os.environ["MNIST_AMD_C1_PREREDUCE"] = pre
+                p1r, l1r, _ = _train(torch, dev, 1, 0, W * B, S, perm.reshape(-1), "rccl")
+                p1r, l1r = p1r.cpu(), l1r.cpu()
+                noise = max(noise, float((p1r - p1).norm() / p1.norm()))
+                lnoise = max(lnoise, float(((l1r - l1).abs() / l1.abs()).max()))
+            if prev is None:
+                os.environ.pop("MNIST_AMD_C1_PREREDUCE", None)
+            else:
+                os.environ["MNIST_AMD_C1_PREREDUCE"] = prev
             rel = float((allp[0] - p1).norm() / p1.norm())
-            noise = float((p1r - p1).norm() / p1.norm())
             mx = float((allp[0] - p1).abs().max())
             lw = torch.stack(alll).mean(0)                     # per-step mean of the shard losses
             lrel = float(((lw - l1).abs() / l1.abs()).max())
-            lnoise = float(((l1r - l1).abs() / l1.abs()).max())
             tol = max(args.tol, 3.0 * noise)
             ok = same and grel <= gtol and rel <= tol and lrel <= max(1e-3, 2.0 * lnoise)
             msg = (f"{'PASS' if ok else 'FAIL'}: W={W} B={B} steps={S}: ranks identical={same}, "
