@@ -43,10 +43,16 @@ __device__ __forceinline__ int64_t conv_sink_index(int bid, int tid, int r) {
   return kk < 9 ? (int64_t)OFF_CONV1_W + ci * 9 + kk : (int64_t)OFF_CONV1_B + ci;
 }
 
-template <class Sink>
-__device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Sink&& sink) {
+// All slab loads are unconditional (clamped row; the out-of-range values are replaced by 0 in the
+// sum, as before) and issued before `pre()` - the caller's own loads (e.g. the optimizer state the
+// sink updates) - so the sums wait for the slabs alone: a branch-guarded load would end in vmcnt(0)
+// and split the kernel into dependent round trips.
+template <class Pre, class Sink>
+__device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Pre&& pre,
+                                                  Sink&& sink) {
   const int tid = threadIdx.x;
   const float sc = a.grad_scale;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (bid < RED_W2_WGS) {
     const int G = a.wgrad_groups;
     const int col = bid * 16 + (tid & 15), sl = tid >> 4;          // float4 column, slab slice
@@ -56,8 +62,12 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int g = sl + 16 * k;
-      v[k] = (g < G) ? src[(int64_t)g * S4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k] = src[(int64_t)(g < G ? g : 0) * S4];
     }
+    pre();
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (sl + 16 * k >= G) v[k] = z4;
     float4 t = v[0];
 #pragma unroll
     for (int k = 1; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
@@ -85,17 +95,24 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
     const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
     const int nslab = a.c1red ? C1_PRE_SLABS : a.c1_rows;
     const float4* src = reinterpret_cast<const float4*>(a.c1red ? a.c1red : a.c1part) + col;
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 t = z4;
+    bool first = true;
     for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {
       float4 v[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int r = k0 + 64 * k;
-        v[k] = (r < nslab) ? src[(int64_t)r * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = src[(int64_t)(r < nslab ? r : 0) * 80];
       }
+      if (first) pre();
+      first = false;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k0 + 64 * k >= nslab) v[k] = z4;
 #pragma unroll
       for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
     }
+    if (first) pre();
     red[tid] = t;
     __syncthreads();
 #pragma unroll
@@ -115,6 +132,11 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
   }
 }
 
+template <class Sink>
+__device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Sink&& sink) {
+  reduce_conv_grads(a, B, bid, red, [] {}, sink);
+}
+
 // bf16 shadows of one updated conv2.weight element: forward layout w2f [co][tap][ci] and dgrad
 // layout w2d [tap][ci][co]
 __device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, float v) {
@@ -131,20 +153,22 @@ __device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, f
 // lane sinks is loaded before (and in flight with) the slab loads.
 __device__ __forceinline__ void conv_reduce_update(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int bid,
                                                    float4* red) {
-  const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
   float* gbuf = c.grad;
-  float pp[4], ps[4], pa[4];
+  float pp[4], ps[4], pa[4], lr = 0.f;
+  auto pre = [&] {                      // issued right after the slab loads, unconditionally
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t e = conv_sink_index(bid, threadIdx.x, r);
-    if (e >= 0) {
+    for (int r = 0; r < 4; ++r) {
+      int64_t e = conv_sink_index(bid, threadIdx.x, r);
+      e = e >= 0 ? e : OFF_CONV1_W;
       pp[r] = a.param[e];
       ps[r] = a.square_avg[e];
       pa[r] = a.acc_delta[e];
     }
-  }
+    lr = *a.lr;
+  };
   int k = 0;
-  reduce_conv_grads(c, B, bid, red, [&](int64_t e, float g) {
+  reduce_conv_grads(c, B, bid, red, pre, [&](int64_t e, float g) {
+    const Ada ad{a.rho, a.eps, a.weight_decay, lr};
     gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
     float p = pp[k], sq = ps[k], acc = pa[k];
     ++k;
