@@ -19,3 +19,15 @@ def cuda_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+def init_world1_pg(backend, device=None):
+    """world_size=1 process group over a TCPStore bound to an OS-chosen port (port 0): no
+    pick-a-free-port-then-bind race with other jobs on the box (EADDRINUSE)."""
+    import datetime
+
+    import torch.distributed as dist
+    store = dist.TCPStore("127.0.0.1", 0, 1, True, timeout=datetime.timedelta(seconds=60))
+    kw = {"device_id": device} if device is not None else {}
+    dist.init_process_group(backend, store=store, world_size=1, rank=0, **kw)
+    return store

@@ -89,19 +89,14 @@ def test_module_path_with_stock_torch_optimizer(cuda_device):
 
 def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
     """world_size=1 process group: DDP wrapper hooks (nccl) + engine's RCCL-overlapped schedule."""
-    import socket
     import torch.distributed as dist
     from pytorch_mnist_ddp_amd.data.datasets import load_mnist
     from pytorch_mnist_ddp_amd.engine.state import ModelState
     from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
     from pytorch_mnist_ddp_amd.ops import native
     from pytorch_mnist_ddp_amd.parallel.ddp import DistributedDataParallel
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
-                            device_id=cuda_device)
+    from conftest import init_world1_pg
+    init_world1_pg("nccl", cuda_device)
     try:
         torch.manual_seed(3)
         net = Net().to(cuda_device)
@@ -183,15 +178,10 @@ def test_scripts_on_gpu(tmp_path):
 def test_torchrun_ddp_paths_on_one_gpu(tmp_path):
     """torchrun world_size=1: env rendezvous, c10d-store RCCL unique-id exchange, engine broadcast,
     comm-attached graphs (fused engine) and hook-driven buckets (module engine)."""
-    import socket
     env = dict(os.environ, PYTHONPATH=ROOT)
     for engine in ("fused", "module"):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "mnist_ddp.py"),
+               "--standalone", "--local-addr=127.0.0.1", os.path.join(ROOT, "mnist_ddp.py"),
                "--epochs", "1", "--batch-size", "200", "--synthetic", "--synthetic-train-size", "2000",
                "--synthetic-test-size", "1000", "--save-model", "--engine", engine]
         r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)

@@ -28,17 +28,11 @@ def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps, f
 def test_allreduce_auto_choice_plumbing_world1(cuda_device):
     """choose_allreduce at world 1 (RCCL comms + the xGMI communicator's copy path): both launch
     sequences run, the timings come back and the buffers are left zeroed."""
-    import socket
-
     import torch
     import torch.distributed as dist
+    from conftest import init_world1_pg
     from pytorch_mnist_ddp_amd.parallel.distributed import choose_allreduce, create_rccl_comms, create_xgmi_comm
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
-                            device_id=cuda_device)
+    init_world1_pg("nccl", cuda_device)
     try:
         c0, c1 = create_rccl_comms(1, 0, 0)
         n, split = 1200000, 1181120
@@ -62,8 +56,8 @@ def test_trainer_auto_probe_path_world1(tmp_path):
     state, forced at world 1) runs and leaves training bit-identical to a plain RCCL run."""
     outs = {}
     for name, env in (("auto", {"MNIST_AMD_PROBE_ALWAYS": "1"}), ("rccl", {"MNIST_AMD_ALLREDUCE": "rccl"})):
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr",
-               "127.0.0.1", "--master-port", str(29600 + len(outs)), os.path.join(ROOT, "bench.py"),
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--standalone",
+               "--local-addr", "127.0.0.1", os.path.join(ROOT, "bench.py"),
                "--force-comm", "--no-full-run", "--steps", "40", "--warmup", "10"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
                            env=dict(os.environ, PYTHONPATH=ROOT, **env))
