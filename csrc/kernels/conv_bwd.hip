@@ -28,11 +28,19 @@ namespace {
 constexpr int DG_ROWS = 7;                              // conv1-output rows per dgrad WG (4 strips)
 constexpr int DG_TROWS = DG_ROWS + 2;                   // dy rows incl. halo (top 2)
 constexpr int DG_TCOLS = H2 + 4;                        // 28 (2 zero columns each side)
-constexpr int DYS_BYTES = DG_TROWS * DG_TCOLS * C2 * 2; // 32256
+// LDS row pitch of the dy tile (pixels).  A pitch of 34 makes a 16-pixel M-tile that wraps from
+// column 25 of one strip row to column 0 of the next advance the LDS row by 9 = 1 mod 8, so the
+// row&7 swizzle continues as on a contiguous run (A-fragment reads 6.2 -> 4.3 modelled LDS cycles,
+// ideal 4) - and measured slower (B = 8192 dgrad 407 -> 420 us): the kernel is not bound by these
+// reads' bank conflicts.  28 = the tile's width.
+constexpr int DG_PITCH = 28;
+constexpr int DYS_BYTES = DG_TROWS * DG_PITCH * C2 * 2; // 32256
 constexpr int W2DS_BYTES = 9 * C1 * C2 * 2;             // 36864
 constexpr int XS2_BYTES = DG_TROWS * IMG * 4;           // 1008 -> pad 1024
 constexpr int RED_BYTES = 4 * 32 * 10 * 4;              // 5120
-constexpr int DG_LDS = DYS_BYTES + W2DS_BYTES + 1024 + RED_BYTES;
+constexpr int DG_LDS = DYS_BYTES + W2DS_BYTES + 1024;   // 70144: two per CU; the conv1-gradient
+                                                        // reduction scratch aliases the dy tile
+static_assert(RED_BYTES <= DYS_BYTES && 2 * DG_LDS <= 160 * 1024, "dgrad LDS carve");
 
 // wgrad: every workgroup owns a contiguous range of dy rows of the whole batch (rows of
 // consecutive images are contiguous in both dy [B*24 rows] and a1 [B*26 rows]), processed in
@@ -91,83 +99,96 @@ int conv_wgrad_groups(int B) {
 // input-row source of the conv1 gradient: pre-gathered epoch rows, rows by index, or fp32 module input
 enum DgX { DGX_PRE = 0, DGX_IDX = 1, DGX_XIN = 2 };
 
+// Global loads of one (image, strip) item of the 4-strip dgrad: the padded dy tile's 16-B chunks
+// (rows r0-2..r0+6, cols -2..25, compact records + argmax routes) and this thread's input pixel.
+// Every load is unconditional (clamped address, validity applied at the LDS store) so all of them
+// are in flight at once; the input row (state -> [index] -> pixel, a dependent chain) is issued last.
+struct DgLoad {
+  uint4 v[8];
+  uint2 rt[8];
+  uint32_t okm;
+  float xv;                                       // fp32 module input, or the raw pixel byte
+};
+
 template <int XM>
-__device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int strip, int b, unsigned char* smem) {
+__device__ __forceinline__ void dgrad_fetch(const ConvBwdArgs& a, int strip, int b, int step, int tid, DgLoad& L) {
+  constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
+  const int r0 = strip * DG_ROWS;
+  L.okm = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = tid + 256 * k;
+    const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
+    const int y = r0 - 2 + ly, x = col - 2;
+    const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
+    L.okm |= (ok ? 1u : 0u) << k;
+    const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
+    L.v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
+    L.rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
+  }
+  const int e = tid < DG_TROWS * IMG ? tid : 0;   // DG_TROWS * IMG = 252 <= 256
+  const bool okx = tid < DG_TROWS * IMG && r0 + e / IMG < IMG;
+  const int off = r0 * IMG + (okx ? e : 0);
+  if constexpr (XM == DGX_XIN) {
+    L.xv = a.xin[(int64_t)b * (IMG * IMG) + off];
+  } else {
+    const int64_t row = (int64_t)step * a.idx_step_stride + b;
+    const int64_t img = (XM == DGX_IDX) ? (int64_t)a.idx[row] : row;
+    L.xv = __builtin_bit_cast(float, (uint32_t)a.data_u8[img * (IMG * IMG) + off]);
+  }
+  if (!okx) L.xv = (XM == DGX_XIN) ? 0.0f : __builtin_bit_cast(float, 0x100u);   // 0x100: "outside"
+}
+
+__device__ __forceinline__ void dgrad_w2d_load(const ConvBwdArgs& a, int tid, uint4 (&w)[9]) {
+  const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
+}
+__device__ __forceinline__ void dgrad_w2d_store(unsigned char* smem, int tid, const uint4 (&w)[9]) {
+  uint16_t* w2ds = reinterpret_cast<uint16_t*>(smem + DYS_BYTES);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int c = tid + 256 * i, row = c >> 3, c8 = c & 7;
+    reinterpret_cast<uint4*>(w2ds)[row * 8 + (c8 ^ swz8(row))] = w[i];
+  }
+}
+__device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, int tid, const DgLoad& L) {
+  constexpr int NCH = DG_TROWS * DG_TCOLS * 8;
+  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
+  const int r0 = strip * DG_ROWS;
+  const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = tid + 256 * k;
+    if (c < NCH) {
+      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
+      const int y = r0 - 2 + ly, x = col - 2;
+      const int row = ly * DG_PITCH + col, c8 = c & 7;
+      const uint4 d = ((L.okm >> k) & 1u) ? dyc_expand(L.v[k], L.rt[k], ((y & 1) << 1) | (x & 1)) : z;
+      reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
+    }
+  }
+}
+
+// MFMA loop + conv1 gradient epilogue of one item whose dy tile and the conv2 weights are in LDS
+// (after a barrier).  Ends with the item's c1part row written; the LDS reads of the dy tile are all
+// done once every wave has passed this function's first barrier.  ``prefetch()`` runs right after
+// the a1 mask loads are issued (the persistent kernel issues the next item's loads there, so the
+// epilogue's wait for the mask does not also wait for them).
+template <int XM, class Prefetch>
+__device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, int b, unsigned char* smem, float xv,
+                                              Prefetch prefetch) {
   uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
   uint16_t* w2ds = reinterpret_cast<uint16_t*>(smem + DYS_BYTES);
   float* xs = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES);
-  float* red = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES + 1024);
-
+  float* red = reinterpret_cast<float*>(smem);   // aliases the dy tile: written after the barrier
+                                                  // that ends every wave's MFMA loop
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // schedule-3 conv bucket split: dgrad's start = conv2_wgrad done (stream order), i.e. the conv2
-  // gradient slabs are final; one lane tells the comm stream (release: wgrad's writes happen-before)
-  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const int r0 = strip * DG_ROWS;
   const int nrows = (strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS;   // 7,7,7,5
   const int npix = nrows * H1;
-  const StepState* st = a.state ? a.state : &g_zero_state;
-  const int step = st->step;                      // oldest load: the input-row chain hangs off it
 
-  // ---- phase 0: stage the padded dy tile (rows r0-2..r0+6, cols -2..25) and w2d: every load is
-  // unconditional (clamped address, validity applied at the LDS store) so all of them are in flight
-  // at once.  The input row (state -> [index] -> pixel, a dependent chain) is loaded last and only
-  // stored to LDS after the MFMA loop - the conv1 gradient epilogue is its first reader.
-  float xv;                                       // fp32 module input, or the raw pixel byte
-  {
-    constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
-    uint4 w[9];
-    const uint4* src = reinterpret_cast<const uint4*>(a.w2d);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = src[tid + 256 * i];
-    uint4 v[8];
-    uint2 rt[8];
-    uint32_t okm = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = tid + 256 * k;
-      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
-      const int y = r0 - 2 + ly, x = col - 2;
-      const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
-      okm |= (ok ? 1u : 0u) << k;
-      const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
-      v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
-      rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, c8 = c & 7;
-      reinterpret_cast<uint4*>(w2ds)[row * 8 + (c8 ^ swz8(row))] = w[i];
-    }
-    {
-      const int e = tid < DG_TROWS * IMG ? tid : 0;   // DG_TROWS * IMG = 252 <= 256
-      const bool okx = tid < DG_TROWS * IMG && r0 + e / IMG < IMG;
-      const int off = r0 * IMG + (okx ? e : 0);
-      if constexpr (XM == DGX_XIN) {
-        xv = a.xin[(int64_t)b * (IMG * IMG) + off];
-      } else {
-        const int64_t row = (int64_t)step * a.idx_step_stride + b;
-        const int64_t img = (XM == DGX_IDX) ? (int64_t)a.idx[row] : row;
-        xv = __builtin_bit_cast(float, (uint32_t)a.data_u8[img * (IMG * IMG) + off]);
-      }
-      if (!okx) xv = (XM == DGX_XIN) ? 0.0f : __builtin_bit_cast(float, 0x100u);   // 0x100: "outside"
-    }
-    const uint4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = tid + 256 * k;
-      if (c < NCH) {
-        const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
-        const int y = r0 - 2 + ly, x = col - 2;
-        const int row = c >> 3, c8 = c & 7;
-        const uint4 d = ((okm >> k) & 1u) ? dyc_expand(v[k], rt[k], ((y & 1) << 1) | (x & 1)) : z;
-        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: transposed conv on MFMA: M-tiles 3w..3w+2 (16 pixels of the 26-wide strip),
+  // ---- transposed conv on MFMA: M-tiles 3w..3w+2 (16 pixels of the 26-wide strip),
   // N = 2 tiles of 16 ci, K = 9 taps x 64 co.  (Enumerating M over the 28-wide padded grid is
   // bank-conflict free but needs 13 tiles per strip - an unbalanced, branchy split that measured
   // slower; this balanced split keeps the row&7 swizzle at ~1.6x the ideal read cost.)
@@ -179,7 +200,7 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
     int q = 16 * (3 * wave + i) + m;
     if (q >= npix) q = 0;
     const int qy = q / H1, qx = q - qy * H1;
-    qbase[i] = (qy + 2) * DG_TCOLS + qx + 2;     // LDS row of the un-shifted pixel
+    qbase[i] = (qy + 2) * DG_PITCH + qx + 2;     // LDS row of the un-shifted pixel
   }
   floatx4 acc[MT][2];
 #pragma unroll
@@ -197,10 +218,11 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
       a1v[i][r][0] = src[0];
       a1v[i][r][1] = src[16];
     }
+  prefetch();
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) {
     const int t = ks >> 1, co0 = 32 * (ks & 1);
-    const int toff = (t / 3) * DG_TCOLS + (t % 3);
+    const int toff = (t / 3) * DG_PITCH + (t % 3);
     const int ch = (co0 >> 3) + kg;
     bf16x8 A[MT], Bf[2];
 #pragma unroll
@@ -229,7 +251,7 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
   }
   __syncthreads();
 
-  // ---- phase 3: conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
+  // ---- conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
   // second, tiny MFMA: D[tap][ci] = sum_px X[px][tap] * d[px][ci] on v_mfma_f32_16x16x16_bf16
   // (row 9 of X = ones -> the bias gradient).  That instruction's B-operand layout (lane l holds
   // k = 4(l>>4)+j, n = l&15) is exactly the C layout of the dgrad accumulators, so the masked
@@ -274,9 +296,62 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
 }
 
 template <int XM>
+__device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int strip, int b, unsigned char* smem) {
+  const int tid = threadIdx.x;
+  // schedule-3 conv bucket split: dgrad's start = conv2_wgrad done (stream order), i.e. the conv2
+  // gradient slabs are final; one lane tells the comm stream (release: wgrad's writes happen-before)
+  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const StepState* st = a.state ? a.state : &g_zero_state;
+  const int step = st->step;                      // oldest load: the input-row chain hangs off it
+  uint4 w[9];
+  dgrad_w2d_load(a, tid, w);
+  DgLoad L;
+  dgrad_fetch<XM>(a, strip, b, step, tid, L);
+  dgrad_w2d_store(smem, tid, w);
+  dgrad_dy_store(smem, strip, tid, L);
+  __syncthreads();
+  dgrad_compute<XM>(a, strip, b, smem, L.xv, [] {});
+}
+
+template <int XM>
 __global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
   dgrad_body<XM>(a, B, blockIdx.x, blockIdx.y, smem);
+}
+
+// Persistent form (default): G <= 2 x CUs workgroups (two fit a CU by LDS), each staging the
+// conv2 weights (36.9 KB) into LDS ONCE and then walking items it = blockIdx.x, +G, ... of the 4B
+// (image, strip) items (strip = it & 3, image = it >> 2: the dgrad_update grid's order).  The next
+// item's dy / input loads are issued right after the current tile's barrier, so they are in flight
+// under the MFMA loop; the co-resident workgroup of the CU overlaps the LDS stores.  Per item the
+// math (K order, masks, conv1-gradient MFMA, c1part row) is the per-item kernel's, bit for bit.
+template <int XM, bool PF>
+__global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
+  const int tid = threadIdx.x, n = 4 * B, G = gridDim.x;
+  int it = blockIdx.x;
+  if (a.signal_ctr && it == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const StepState* st = a.state ? a.state : &g_zero_state;
+  const int step = st->step;
+  uint4 w[9];
+  dgrad_w2d_load(a, tid, w);
+  DgLoad L;
+  dgrad_fetch<XM>(a, it & 3, it >> 2, step, tid, L);
+  dgrad_w2d_store(smem, tid, w);
+  for (; it < n; it += G) {
+    if (!PF && it != (int)blockIdx.x) dgrad_fetch<XM>(a, it & 3, it >> 2, step, tid, L);
+    dgrad_dy_store(smem, it & 3, tid, L);
+    const float xv = L.xv;
+    __syncthreads();
+    const int nx = (it + G < n) ? it + G : it;   // clamped: the last item's prefetch is a re-read
+    if constexpr (PF)
+      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
+    else
+      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, [] {});
+    __syncthreads();                              // the next dy store must not overtake the red reads
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -464,6 +539,29 @@ static int dgrad_strips() {
   return (e && e[0] == '1') ? 3 : 4;
 }
 int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
+
+// Grid of the persistent 4-strip dgrad: MNIST_AMD_DGRAD_PERSIST = 0 -> per-item kernel (returns 0),
+// unset / 1 -> 2 x CUs workgroups when that covers the 4B items in at most two rounds (B <= 256 on
+// 256 CUs; measured B = 200: 80.4 vs 82.6 us/step), else the per-item kernel (B = 8192: 1.44 vs
+// 1.35 ms/step - at large B independent per-item workgroups overlap one's staging with the other's
+// MFMAs better than the item loop does); N > 1 -> min(4B, N) workgroups.  Read per call (host).
+static int dgrad_persist_grid(int B) {
+  const char* e = getenv("MNIST_AMD_DGRAD_PERSIST");
+  const int v = e ? atoi(e) : 1;
+  if (v == 0) return 0;
+  int g = v;
+  if (v == 1) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    g = 2 * cus;
+    if (4 * B > 2 * g) return 0;
+  }
+  return g < 4 * B ? g : 4 * B;
+}
 
 // dgrad (workgroups [0, 4B), same order as conv2_dgrad_kernel's (strip, b) grid) + the conv2 slab
 // reduce and Adadelta step (workgroups [4B, 4B + RED_W2_PARTS)).  Workgroups are dispatched in id
@@ -711,7 +809,21 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   if (a.c1_rows == 3 * B)
     hipLaunchKernelGGL(conv2_dgrad3_kernel, dim3(3, B), dim3(256), 0, s, a, B);
-  else if (a.c1_rows == 4 * B && a.xin)
+  else if (a.c1_rows == 4 * B && dgrad_persist_grid(B) > 0) {
+    const dim3 g(dgrad_persist_grid(B));
+    const char* pe = getenv("MNIST_AMD_DGRAD_PF");
+    const bool pf = !(pe && pe[0] == '0');
+    if (a.xin)
+      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_XIN, true>), g, dim3(256), 0, s, a, B);
+    else if (a.idx && pf)
+      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_IDX, true>), g, dim3(256), 0, s, a, B);
+    else if (a.idx)
+      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_IDX, false>), g, dim3(256), 0, s, a, B);
+    else if (pf)
+      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_PRE, true>), g, dim3(256), 0, s, a, B);
+    else
+      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_PRE, false>), g, dim3(256), 0, s, a, B);
+  } else if (a.c1_rows == 4 * B && a.xin)
     hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_XIN>, dim3(4, B), dim3(256), 0, s, a, B);
   else if (a.c1_rows == 4 * B && a.idx)
     hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_IDX>, dim3(4, B), dim3(256), 0, s, a, B);

@@ -253,3 +253,23 @@ def test_dgrad_strip_forms_agree(cuda_device, monkeypatch, B):
     rel = ((p3 - p4).norm() / p4.norm()).item()
     assert rel < 1e-5, rel
     assert (l3 - l4).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("B,grid", [(200, "1"), (200, "37"), (512, "512")])
+def test_dgrad_persistent_bitwise_equal(cuda_device, monkeypatch, B, grid):
+    """Persistent conv2_dgrad (conv2 weights staged once per workgroup, items it, it+G, ... with the
+    next item's loads in flight under the MFMA loop; default) gives the bits of the per-item grid,
+    including a small odd grid (37 workgroups: ~22 items each, ragged last round)."""
+    idx = torch.randperm(B * 4, generator=torch.Generator().manual_seed(23))
+    out = {}
+    monkeypatch.setenv("MNIST_AMD_DGRAD3", "0")
+    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "0")
+    for form in ("0", grid):
+        monkeypatch.setenv("MNIST_AMD_DGRAD_PERSIST", form)
+        _, ms, t = _trainer(cuda_device, graph_steps=2, n_train=B * 4, B=B)
+        t.train_epoch(1, idx)
+        t.synchronize()
+        torch.cuda.synchronize()
+        out[form] = (ms.param.clone(), t.loss_log.clone(), ms.grad.clone())
+    a, b = out["0"], out[grid]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
