@@ -9,7 +9,7 @@ for rep in 1 2; do
   for n in $NAMES; do
     cp tools/so/$n.so $SO
     timeout -k 10 240 python bench.py --no-full-run "$@" > gpurun_out/abs_${T}_${n}_$rep.log 2>&1 || { echo "bench $n failed"; tail -5 gpurun_out/abs_${T}_${n}_$rep.log; cp /tmp/_C_keep.so $SO; exit 1; }
-    echo "$T $n $(tail -1 gpurun_out/abs_${T}_${n}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"]*1000, "us/step")')"
+    echo "$T $n $(tail -1 gpurun_out/abs_${T}_${n}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"]*1000, "us/step loss", d.get("last_train_loss"))')"
   done
 done
 cp /tmp/_C_keep.so $SO
