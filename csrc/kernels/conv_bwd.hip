@@ -154,7 +154,7 @@ __device__ __forceinline__ void dgrad_w2d_store(unsigned char* smem, int tid, co
 }
 __device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, int tid, const DgLoad& L) {
   constexpr int NCH = DG_TROWS * DG_TCOLS * 8;
-  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);   // the dy tile is at the start of smem
   const int r0 = strip * DG_ROWS;
   const uint4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -175,15 +175,32 @@ __device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, i
 // done once every wave has passed this function's first barrier.  ``prefetch()`` runs right after
 // the a1 mask loads are issued (the persistent kernel issues the next item's loads there, so the
 // epilogue's wait for the mask does not also wait for them).
-template <int XM, class Prefetch>
-__device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, int b, unsigned char* smem, float xv,
-                                              Prefetch prefetch) {
-  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* w2ds = reinterpret_cast<uint16_t*>(smem + DYS_BYTES);
-  float* xs = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES);
-  float* red = reinterpret_cast<float*>(smem);   // aliases the dy tile: written after the barrier
-                                                  // that ends every wave's MFMA loop
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+// Input-row value staged for the conv1-gradient epilogue (raw pixel byte -> normalised fp32).
+template <int XM>
+__device__ __forceinline__ float dgrad_xs_value(float xv) {
+  if (XM == DGX_XIN) return xv;
+  const uint32_t u = __builtin_bit_cast(uint32_t, xv);
+  return u > 0xFFu ? 0.0f : normalize_u8_alu(u);
+}
+
+// Fixed-order sum of the 4 waves' conv1-gradient partials -> the item's c1part row (256 threads).
+__device__ __forceinline__ void dgrad_red_reduce(const ConvBwdArgs& a, int strip, int b, const float* red, int ltid) {
+  for (int e = ltid; e < 320; e += 256) {
+    const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
+    a.c1part[((int64_t)b * 4 + strip) * 320 + e] = s;
+  }
+}
+
+// STAG = false: the whole item on one 4-wave workgroup (xs store, barriers, reduce inside).
+// STAG = true: xs is already staged and no barriers are taken; the item ends with the waves'
+// partials in red (the caller reduces them later).  The staggered-halves dgrad that used this
+// (one 8-wave workgroup per CU, halves alternating MFMA and staging phases) measured slower than
+// two independent per-item workgroups per CU (B = 8192: 1.56 vs 1.24 ms/step) and was removed.
+template <int XM, bool STAG, class Prefetch>
+__device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip, int b, uint16_t* dys,
+                                                const uint16_t* w2ds, float* xs, float* red, int wave,
+                                                int ltid, float xv, Prefetch prefetch) {
+  const int lane = threadIdx.x & 63, tid = ltid;
   const int r0 = strip * DG_ROWS;
   const int nrows = (strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS;   // 7,7,7,5
   const int npix = nrows * H1;
@@ -194,14 +211,29 @@ __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, i
   // slower; this balanced split keeps the row&7 swizzle at ~1.6x the ideal read cost.)
   const int m = lane & 15, kg = lane >> 4;
   constexpr int MT = 3;
-  int qbase[MT];
+  // A-fragment addresses without per-read VALU: for tap t = 3d + c the LDS row is R_c - 28d with
+  // R_c = qbase - c, and (R_c - 28d) & 7 = (R_c & 7) ^ 4(d & 1), so the swizzled chunk of co-half h is
+  // ((kg ^ (R_c & 7)) ^ 4(h ^ (d & 1))): per (M-tile, c) two base addresses (chunk bit 2 clear / set)
+  // at row R_c - 56, and every read of the loop is base + an immediate (1792 elements per d step).
+  static_assert(DG_PITCH % 8 == 4, "row step of one tap row = 4 mod 8");
+  const uint16_t* abase[MT][3][2];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     int q = 16 * (3 * wave + i) + m;
     if (q >= npix) q = 0;
     const int qy = q / H1, qx = q - qy * H1;
-    qbase[i] = (qy + 2) * DG_PITCH + qx + 2;     // LDS row of the un-shifted pixel
+    const int qbase = (qy + 2) * DG_PITCH + qx + 2;     // LDS row of the un-shifted pixel
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int rc = qbase - c;
+      const int e = (rc - 2 * DG_PITCH) * C2 + ((kg ^ (rc & 7)) << 3);
+      abase[i][c][0] = dys + e;
+      abase[i][c][1] = dys + (e ^ 32);
+    }
   }
+  // B fragments: row t*32 + 16nt + m has swizzle key m & 7 for every t, nt
+  const int be = m * C2 + ((kg ^ (m & 7)) << 3);
+  const uint16_t* bbase[2] = {w2ds + be, w2ds + (be ^ 32)};
   floatx4 acc[MT][2];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -221,35 +253,22 @@ __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, i
   prefetch();
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) {
-    const int t = ks >> 1, co0 = 32 * (ks & 1);
-    const int toff = (t / 3) * DG_PITCH + (t % 3);
-    const int ch = (co0 >> 3) + kg;
+    const int t = ks >> 1, h = ks & 1, d = t / 3, c = t % 3;
     bf16x8 A[MT], Bf[2];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int row = qbase[i] - toff;
-      A[i] = ld16(dys + row * C2 + ((ch ^ swz8(row)) << 3));
-    }
+    for (int i = 0; i < MT; ++i) A[i] = ld16(abase[i][c][h ^ (d & 1)] + (2 - d) * DG_PITCH * C2);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int row = t * C1 + nt * 16 + m;
-      Bf[nt] = ld16(w2ds + row * C2 + ((ch ^ swz8(row)) << 3));
-    }
+    for (int nt = 0; nt < 2; ++nt) Bf[nt] = ld16(bbase[h] + (t * C1 + nt * 16) * C2);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bf[nt], acc[i][nt]);
   }
 
-  if (tid < DG_TROWS * IMG) {                     // input rows: first read by the epilogue below
-    float x = xv;
-    if (XM != DGX_XIN) {
-      const uint32_t u = __builtin_bit_cast(uint32_t, xv);
-      x = u > 0xFFu ? 0.0f : normalize_u8_alu(u);
-    }
-    xs[tid] = x;
+  if constexpr (!STAG) {
+    if (tid < DG_TROWS * IMG) xs[tid] = dgrad_xs_value<XM>(xv);   // input rows: first read below
+    __syncthreads();
   }
-  __syncthreads();
 
   // ---- conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
   // second, tiny MFMA: D[tap][ci] = sum_px X[px][tap] * d[px][ci] on v_mfma_f32_16x16x16_bf16
@@ -288,11 +307,21 @@ __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, i
       const int t = 4 * kg + r;
       if (t < 10) red[(wave * 32 + nt * 16 + m) * 10 + t] = dw[nt][r];
     }
-  __syncthreads();
-  for (int e = tid; e < 320; e += 256) {
-    const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
-    a.c1part[((int64_t)b * 4 + strip) * 320 + e] = s;
+  if constexpr (!STAG) {
+    __syncthreads();
+    dgrad_red_reduce(a, strip, b, red, tid);
   }
+}
+
+template <int XM, class Prefetch>
+__device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, int b, unsigned char* smem, float xv,
+                                              Prefetch prefetch) {
+  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
+  const uint16_t* w2ds = reinterpret_cast<const uint16_t*>(smem + DYS_BYTES);
+  float* xs = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES);
+  float* red = reinterpret_cast<float*>(smem);   // aliases the dy tile: written after the barrier
+                                                  // that ends every wave's MFMA loop
+  dgrad_compute_p<XM, false>(a, strip, b, dys, w2ds, xs, red, threadIdx.x >> 6, threadIdx.x, xv, prefetch);
 }
 
 template <int XM>
@@ -585,25 +614,31 @@ namespace {
 // first a1 row (global, [B*26]) under dy row R (global, [B*24])
 __device__ __forceinline__ int a1_row_of(int R) { return R + 2 * (R / H2); }
 
-struct WgradChunk {
-  uint4 vd[WDY_V], va[WA1_V];
-  uint2 rt[WDY_V];
+template <int NTH>
+struct WgradChunkT {
+  static constexpr int VD = WDY_BYTES / 16 / NTH, VA = (WA1_BYTES / 16 + NTH - 1) / NTH;
+  uint4 vd[VD], va[VA];
+  uint2 rt[VD];
   uint32_t okd, oka;          // validity bits, applied at the LDS store (not on the loaded values)
 };
+using WgradChunk = WgradChunkT<WG_THREADS>;
+static_assert(WDY_BYTES % (16 * 256) == 0, "dy chunk staging by 256 threads");
 
 // Issue the global loads of chunk [c0, c1) into registers (zeros past the valid rows, so every LDS
 // byte of the buffer is rewritten and finite).  The loads are unconditional (clamped to the chunk's
 // first element, the value masked after): loads under a branch make the waitcnt pass fall back to
 // vmcnt(0), which pulled the wait for this prefetch up into the middle of the MFMA loop.
-__device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1, int tid, WgradChunk& k) {
+template <int NTH>
+__device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1, int tid, WgradChunkT<NTH>& k) {
+  constexpr int VD = WgradChunkT<NTH>::VD, VA = WgradChunkT<NTH>::VA;
   const int ndy = (c1 - c0) * H2 * 8;                               // valid 16-B chunks of dy
   const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
   const int na1 = (A1 - A0) * H1 * 4;                               // valid 16-B chunks of a1
   const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
   k.okd = k.oka = 0;
 #pragma unroll
-  for (int i = 0; i < WDY_V; ++i) {
-    const int c0i = tid + WG_THREADS * i;
+  for (int i = 0; i < VD; ++i) {
+    const int c0i = tid + NTH * i;
     const bool ok = c0i < ndy;
     k.okd |= (ok ? 1u : 0u) << i;
     const int c = ok ? c0i : 0;                     // dense chunk (pixel c>>3, channels 8(c&7)..)
@@ -614,19 +649,21 @@ __device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1
     k.rt[i] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + (c & 7) * 8);
   }
 #pragma unroll
-  for (int i = 0; i < WA1_V; ++i) {
-    const int c = tid + WG_THREADS * i;
+  for (int i = 0; i < VA; ++i) {
+    const int c = tid + NTH * i;
     k.oka |= (c < na1 ? 1u : 0u) << i;
     k.va[i] = asrc[c < na1 ? c : 0];
   }
 }
 
-__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0, const WgradChunk& k, float* bsum) {
+template <int NTH>
+__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0, const WgradChunkT<NTH>& k, float* bsum) {
+  constexpr int VD = WgradChunkT<NTH>::VD, VA = WgradChunkT<NTH>::VA;
   uint4* dys = reinterpret_cast<uint4*>(buf);
   uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
 #pragma unroll
-  for (int i = 0; i < WDY_V; ++i) {
-    const int c = tid + WG_THREADS * i, pix = c >> 3;
+  for (int i = 0; i < VD; ++i) {
+    const int c = tid + NTH * i, pix = c >> 3;
     const int R = c0 + pix / H2, x = pix - (pix / H2) * H2;
     const uint4 d = ((k.okd >> i) & 1u) ? dyc_expand(k.vd[i], k.rt[i], ((R & 1) << 1) | (x & 1))   // H2 even: y&1 == R&1
                                         : uint4{0u, 0u, 0u, 0u};
@@ -639,8 +676,8 @@ __device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0,
     }
   }
 #pragma unroll
-  for (int i = 0; i < WA1_V; ++i) {
-    const int c = tid + WG_THREADS * i;
+  for (int i = 0; i < VA; ++i) {
+    const int c = tid + NTH * i;
     if (c < WA1_BYTES / 16) a1s[c] = ((k.oka >> i) & 1u) ? k.va[i] : uint4{0u, 0u, 0u, 0u};
   }
 }
@@ -751,6 +788,135 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
 }
 
 // --------------------------------------------------------------------------------------------
+// conv2_wgrad, staggered halves (large batches, see wgrad_staggered).  The
+// 8 waves form two independent halves of 4 (waves 0-3 / 4-7: one wave of each half per SIMD), each
+// owning one of the two LDS chunk buffers and the alternate chunks of the workgroup's row range
+// (half h: chunks h, h+2, ...).  In phase p half (p & 1) runs the MFMAs of chunk p while the other
+// half stores its prefetched chunk p+1 into its buffer and issues the global loads of chunk p+3 - so
+// every SIMD pairs one MFMA wave with one staging wave instead of all 8 waves alternating between
+// an MFMA phase and a VALU/LDS-store phase in lockstep (cdna4 "stagger": matrix beside memory).
+// Each wave of a half covers 2 co-tiles x 9 (tap, ci-half) n-tiles; at the end half 1 hands its
+// accumulators to half 0 through LDS (fixed order: half 0 + half 1) and the workgroup writes one
+// slab, so the reduce sees the same G slabs.  The conv2 bias sum is per thread as before.
+__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_stag_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int half = wave >> 2, hw = wave & 3, htid = tid & 255;
+  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int mt0 = 2 * (hw & 1), nt0 = 9 * (hw >> 1);
+  const int G = gridDim.x, g = blockIdx.x;
+  if (a.signal_ctr && g == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const int rows = H2 * B;
+  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
+  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
+
+  floatx4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  const int clo = 8 * gq + q, chi = clo + 4;
+  int aoff_lo[2], aoff_hi[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cb = 16 * (mt0 + i) + 4 * pp;
+    aoff_lo[i] = clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7));
+    aoff_hi[i] = chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7));
+  }
+  int toffs[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int nt = nt0 + j, t = nt >> 1, ci0 = 16 * (nt & 1);
+    toffs[j] = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
+  }
+  auto chunk_lo = [&](int ch) { return r0 + ch * WG_CH; };
+  auto chunk_hi = [&](int ch) { return min(r0 + (ch + 1) * WG_CH, r1); };
+  unsigned char* mybuf = smem + half * WBUF_BYTES;
+
+  // prologue: half 0 stages chunk 0 and prefetches chunk 2; half 1 prefetches chunk 1
+  WgradChunkT<256> k;
+  if (half == 0) {
+    if (nchunks > 0) {
+      wgrad_fetch<256>(a, chunk_lo(0), chunk_hi(0), htid, k);
+      wgrad_store<256>(mybuf, htid, chunk_lo(0), k, bsum);
+    }
+    if (nchunks > 2) wgrad_fetch<256>(a, chunk_lo(2), chunk_hi(2), htid, k);
+  } else if (nchunks > 1) {
+    wgrad_fetch<256>(a, chunk_lo(1), chunk_hi(1), htid, k);
+  }
+  __syncthreads();
+  for (int ph = 0; ph < nchunks; ++ph) {
+    if ((ph & 1) == half) {                             // MFMAs of chunk ph (half-uniform)
+      const int c0 = chunk_lo(ph), c1 = chunk_hi(ph);
+      const uint16_t* dys = reinterpret_cast<const uint16_t*>(mybuf);
+      const uint16_t* a1s = reinterpret_cast<const uint16_t*>(mybuf + WDY_BYTES);
+      const int A0 = a1_row_of(c0);
+      const int nks = ((c1 - c0) * H2 + 31) / 32;
+#pragma unroll 1
+      for (int ks = 0; ks < nks; ++ks) {
+        bf16x8 A[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) A[i] = tr_frag(dys + ks * 32 * C2 + aoff_lo[i], dys + ks * 32 * C2 + aoff_hi[i]);
+        const int plo = 32 * ks + clo, phi = plo + 4;
+        const int rlo = plo / H2, rhi = phi / H2;
+        const int blo_px = (a1_row_of(c0 + rlo) - A0) * H1 + (plo - rlo * H2);
+        const int bhi_px = (a1_row_of(c0 + rhi) - A0) * H1 + (phi - rhi * H2);
+        const uint16_t* blo = a1s + blo_px * C1 + 4 * pp;
+        const uint16_t* bhi = a1s + bhi_px * C1 + 4 * pp;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          const bf16x8 Bf = tr_frag(blo + toffs[j], bhi + toffs[j]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
+        }
+      }
+    } else if (ph + 1 < nchunks) {                      // stage chunk ph+1, prefetch chunk ph+3
+      wgrad_store<256>(mybuf, htid, chunk_lo(ph + 1), k, bsum);
+      if (ph + 3 < nchunks) wgrad_fetch<256>(a, chunk_lo(ph + 3), chunk_hi(ph + 3), htid, k);
+    }
+    __syncthreads();
+  }
+  // half 1 -> half 0 through LDS ([hw][i][j][lane] float4, 73.7 KB), half 0 adds in fixed order
+  floatx4* xch = reinterpret_cast<floatx4*>(smem);
+  static_assert(4 * 18 * 64 * 16 <= WG_LDS, "accumulator exchange fits the chunk buffers");
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) xch[((hw * 2 + i) * 9 + j) * 64 + lane] = acc[i][j];
+  }
+  __syncthreads();
+  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
+  if (half == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const floatx4 o = xch[((hw * 2 + i) * 9 + j) * 64 + lane];
+        const floatx4 v = {acc[i][j][0] + o[0], acc[i][j][1] + o[1], acc[i][j][2] + o[2], acc[i][j][3] + o[3]};
+        const int tile = (mt0 + i) * 18 + nt0 + j;
+        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = v;
+      }
+  }
+  __syncthreads();
+  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 64 such threads via LDS
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[j * WG_THREADS + tid] = bsum[j];
+  __syncthreads();
+  if (tid < 64) {
+    const int c8 = tid >> 3, j = tid & 7;     // channel = 8*c8 + j
+    float sm = 0.f;
+    for (int kk = 0; kk < WG_THREADS / 8; ++kk) sm += red[j * WG_THREADS + kk * 8 + c8];
+    out[18432 + 8 * c8 + j] = sm;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
   __shared__ float4 red[256];
@@ -833,8 +999,20 @@ void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
     throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
   launch_c1_prereduce(a, B, s);
 }
+// Staggered halves pay once every half has >= 2 chunks of its own (rows per workgroup >= 32, i.e.
+// B >= 342 at 256 groups): measured B = 8192 1263-1266 -> 1214-1216 us/step, B = 2048 367-370 ->
+// 355-363; at B = 200 (2-3 chunks per workgroup) the plain kernel stays (78.5-78.9 vs 80.3-80.8).
+// MNIST_AMD_WGRAD_STAG=0 / 1 forces either form (read per call, host).
+static bool wgrad_staggered(const ConvBwdArgs& a, int B) {
+  const char* e = getenv("MNIST_AMD_WGRAD_STAG");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return (int64_t)H2 * B >= (int64_t)4 * WG_CH * a.wgrad_groups;
+}
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
+  if (!wgrad_staggered(a, B))
+    hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
+  else
+    hipLaunchKernelGGL(conv2_wgrad_stag_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
 }
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
   launch_conv_dgrad(a, B, s);

@@ -273,3 +273,25 @@ def test_dgrad_persistent_bitwise_equal(cuda_device, monkeypatch, B, grid):
         out[form] = (ms.param.clone(), t.loss_log.clone(), ms.grad.clone())
     a, b = out["0"], out[grid]
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("B", [200, 512])
+def test_wgrad_staggered_halves_agree(cuda_device, monkeypatch, B):
+    """conv2_wgrad with two staggered 4-wave halves (alternate chunks, accumulators summed half 0 +
+    half 1; the large-batch default) vs the 8-wave lockstep kernel: the same conv gradients up to
+    fp32 summation order, and each form repeats bit for bit."""
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(29))
+    grads = {}
+    for form in ("0", "1", "1"):
+        monkeypatch.setenv("MNIST_AMD_WGRAD_STAG", form)
+        _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=B, B=B, dropout=False)
+        t.train_epoch(1, idx)
+        t.synchronize()
+        torch.cuda.synchronize()
+        g = ms.grad.clone()
+        if form in grads:
+            assert torch.equal(grads[form], g)
+        grads[form] = g
+    g0, g1 = grads["0"], grads["1"]
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 1e-5, rel

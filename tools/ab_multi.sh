@@ -11,6 +11,6 @@ for rep in 1 2; do
   for c in "${cfgs[@]}"; do
     i=$((i+1))
     env $c timeout -k 10 200 python bench.py --no-full-run "$@" > gpurun_out/abm_${T}_${i}_$rep.log 2>&1 || { tail -20 gpurun_out/abm_${T}_${i}_$rep.log; exit 1; }
-    echo "$T [$c] $(tail -1 gpurun_out/abm_${T}_${i}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+    echo "$T [$c] $(tail -1 gpurun_out/abm_${T}_${i}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("last_train_loss"))')"
   done
 done

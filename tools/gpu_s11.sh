@@ -1,0 +1,5 @@
+set -o pipefail
+timeout -k 10 500 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_numerics.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/s11_t.log 2>&1 || { tail -30 gpurun_out/s11_t.log; exit 1; }
+tail -2 gpurun_out/s11_t.log
+C="persist cur:MNIST_AMD_WGRAD_STAG=0 cur:MNIST_AMD_WGRAD_STAG=1"
+bash tools/ab_so_env.sh big "$C" --batch-size 8192 --steps 60 --warmup 10 && bash tools/ab_so_env.sh b200 "$C" --steps 1000 && bash tools/ab_so_env.sh b2048 "$C" --batch-size 2048 --steps 200

@@ -1,0 +1,6 @@
+set -o pipefail
+timeout -k 10 500 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_numerics.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/s13_t.log 2>&1 || { tail -30 gpurun_out/s13_t.log; exit 1; }
+tail -2 gpurun_out/s13_t.log
+bash tools/ab_multi.sh big "MNIST_AMD_DGRAD_STAG=0" "MNIST_AMD_DGRAD_STAG=auto" -- --batch-size 8192 --steps 60 --warmup 10 && \
+bash tools/ab_multi.sh b512 "MNIST_AMD_DGRAD_STAG=0" "MNIST_AMD_DGRAD_STAG=auto" -- --batch-size 512 --steps 400 && \
+bash tools/ab_multi.sh b200 "MNIST_AMD_DGRAD_STAG=auto" "MNIST_AMD_DGRAD_STAG=1" -- --steps 1000
