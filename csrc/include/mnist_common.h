@@ -7,7 +7,9 @@
 // Layout conventions (all chosen for 64-wide wavefronts and MFMA fragment shapes):
 //   a1      bf16 [B][26][26][32]   NHWC conv1 output (8 contiguous channels = one 16-B MFMA fragment)
 //   p       bf16 [B][9216]         pooled+dropout output in torch flatten order (c*144 + y*12 + x)
-//   pmask   u8   [B][9216]         bits 0-1 argmax in the 2x2 window, bit 2 dropout keep, bit 3 pooled>0
+//   pmask   u8   [B][36][64][4]    (pooled position / 4, channel, position % 4) bits 0-1 argmax in the
+//                                   2x2 window, bit 2 dropout keep, bit 3 pooled>0 (functional.pmask_flat
+//                                   gives the channel-major [B][9216] view)
 //   w2f     bf16 [64][9][32]       conv2 weight, forward B operand  (co, tap, ci)
 //   w2d     bf16 [9][32][64]       conv2 weight, dgrad B operand    (tap, ci, co)
 //   w1      bf16 [128][9216]       fc1 weight (torch layout) - forward B operand

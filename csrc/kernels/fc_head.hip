@@ -649,7 +649,7 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
     for (int k = 0; k < 4; ++k) {
       const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
       const int row = b0 + bl < B ? b0 + bl : B - 1;
-      pmv[k] = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)row * NFLAT + c * NPOOL + s0);
+      pmv[k] = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)row * NFLAT + ((s0 >> 2) * C2 + c) * 4);
     }
     const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;   // rows < Bp: zero padding rows
     bf16x8 Af[NH / 32], Bs[CACHE_W ? 1 : NH / 32][4];

@@ -320,7 +320,12 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
         o[k] = keep ? (drop ? o[k] * (1.0f / KEEP1) : o[k]) : 0.0f;
         if (keep) mk[k >> 2] |= 4u << (8 * (k & 3));
       }
-      *reinterpret_cast<uint4*>(a.pmask_out + (int64_t)b * NFLAT + flat) = uint4{mk[0], mk[1], mk[2], mk[3]};
+      // pmask layout [b][pooled position / 4][channel][4] (mnist_common.h): fc_bwd role B reads one
+      // contiguous 256-B run per row and 4-position group instead of 4 bytes per 144-B stride
+      const int w0 = strip0 * WIN + j16;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        *reinterpret_cast<uint32_t*>(a.pmask_out + (int64_t)b * NFLAT + (((w0 >> 2) + q4) * C2 + n) * 4) = mk[q4];
     }
     uint4 s0, s1;
     s0.x = pack2bf(o[0], o[1]);   s0.y = pack2bf(o[2], o[3]);

@@ -73,6 +73,13 @@ class StepBuffers:
         )
 
 
+def pmask_flat(pmask: torch.Tensor) -> torch.Tensor:
+    """The trunk's pool/dropout flags in torch flatten order [B, 9216] (channel-major) from the device
+    layout [B][36][64][4] (pooled position / 4, channel, position % 4; mnist_common.h)."""
+    B = pmask.shape[0]
+    return pmask.view(B, 36, 64, 4).permute(0, 2, 1, 3).reshape(B, 9216)
+
+
 def trunk_fwd(ms, data_u8: torch.Tensor, idx: torch.Tensor, buf: StepBuffers, train: bool,
               idx_stride: int = 0, state: torch.Tensor | None = None) -> None:
     p, o = native.ptr, ms.offsets

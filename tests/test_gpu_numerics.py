@@ -72,7 +72,7 @@ def test_train_step_dropout_masks_consistent(cuda_device):
     ms.set_state(3, seed=seed, rng_base=base)
     Fk.train_step(ms, u8, lab, idx, buf, update=False)
     torch.cuda.synchronize()
-    pm = buf.pmask.cpu()
+    pm = Fk.pmask_flat(buf.pmask).cpu()
     keep1 = ((pm >> 2) & 1).bool()
     rate = keep1.float().mean().item()
     assert abs(rate - 0.75) < 0.01, rate
@@ -144,7 +144,7 @@ def test_backward_kernels_stagewise_exact(cuda_device, B):
     grads = {n: v.detach().cpu().double() for n, v in ms.views(ms.grad).items()}
     q = lambda t: t.float().to(torch.bfloat16).double()
     p = buf.p[:B].cpu().double()
-    pm = buf.pmask.cpu().long()
+    pm = Fk.pmask_flat(buf.pmask).cpu().long()
     dz1 = buf.dz1[:B].cpu().double()
     # fc1 weight/bias grads from the kernel's dz1 / p
     assert rel_err(grads["fc1.weight"], dz1.t() @ p) < 1e-5
