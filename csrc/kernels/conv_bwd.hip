@@ -103,26 +103,34 @@ enum DgX { DGX_PRE = 0, DGX_IDX = 1, DGX_XIN = 2 };
 // (rows r0-2..r0+6, cols -2..25, compact records + argmax routes) and this thread's input pixel.
 // Every load is unconditional (clamped address, validity applied at the LDS store) so all of them
 // are in flight at once; the input row (state -> [index] -> pixel, a dependent chain) is issued last.
+// Staging by pooled record: the tile's dy rows r0-2..r0+6 lie under 5 pooled rows (py0..py0+4,
+// py0 = floor((r0-2)/2)) x 12 pooled columns; job = (pooled row, pooled column, 16-B channel chunk):
+// 480 jobs, 2 per thread.  Each job loads its record chunk + argmax routes ONCE and expands them into
+// the (up to) 4 pixels of its 2x2 window (the per-pixel form loaded every record 4 times and paid the
+// pixel addressing 8 times per thread); pooled rows outside [0, 12) stage zeros (the padding rows),
+// and the 4 padding columns are zero-filled separately (288 chunks).  Same LDS bytes as before.
+constexpr int DG_JOBS = 5 * HP * 8;                // 480
 struct DgLoad {
-  uint4 v[8];
-  uint2 rt[8];
-  uint32_t okm;
+  uint4 v[2];
+  uint2 rt[2];
+  uint32_t okm;                                   // bit j: job j's pooled row is inside the image
   float xv;                                       // fp32 module input, or the raw pixel byte
 };
 
 template <int XM>
 __device__ __forceinline__ void dgrad_fetch(const ConvBwdArgs& a, int strip, int b, int step, int tid, DgLoad& L) {
-  constexpr int NCH = DG_TROWS * DG_TCOLS * 8;   // 2016 16-B chunks
   const int r0 = strip * DG_ROWS;
+  const int py0 = (r0 - 2) >> 1;                  // arithmetic shift: floor
   L.okm = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = tid + 256 * k;
-    const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
-    const int y = r0 - 2 + ly, x = col - 2;
-    const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
+  for (int k = 0; k < 2; ++k) {
+    const int jb = tid + 256 * k;
+    const int j = jb < DG_JOBS ? jb : 0;
+    const int c8 = j & 7, pc = (j >> 3) % HP, pr = (j >> 3) / HP;
+    const int py = py0 + pr;
+    const bool ok = jb < DG_JOBS && py >= 0 && py < HP;
     L.okm |= (ok ? 1u : 0u) << k;
-    const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
+    const uint8_t* rec = a.dyc + (int64_t)b * DYC_BYTES_PER_IMAGE + ((ok ? py : 0) * HP + pc) * DYC_REC;
     L.v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
     L.rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
   }
@@ -153,19 +161,35 @@ __device__ __forceinline__ void dgrad_w2d_store(unsigned char* smem, int tid, co
   }
 }
 __device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, int tid, const DgLoad& L) {
-  constexpr int NCH = DG_TROWS * DG_TCOLS * 8;
-  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);   // the dy tile is at the start of smem
+  uint4* dys = reinterpret_cast<uint4*>(smem);    // the dy tile is at the start of smem
   const int r0 = strip * DG_ROWS;
+  const int py0 = (r0 - 2) >> 1;
   const uint4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = tid + 256 * k;
-    if (c < NCH) {
-      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
-      const int y = r0 - 2 + ly, x = col - 2;
-      const int row = ly * DG_PITCH + col, c8 = c & 7;
-      const uint4 d = ((L.okm >> k) & 1u) ? dyc_expand(L.v[k], L.rt[k], ((y & 1) << 1) | (x & 1)) : z;
-      reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
+  for (int k = 0; k < 2; ++k) {
+    const int jb = tid + 256 * k;
+    if (jb < DG_JOBS) {
+      const int c8 = jb & 7, pc = (jb >> 3) % HP, pr = (jb >> 3) / HP;
+      const int ly0 = 2 * (py0 + pr) - (r0 - 2);  // tile row of the window's top pixel row (-1..9)
+      const bool ok = (L.okm >> k) & 1u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ly = ly0 + (q >> 1);
+        if (ly >= 0 && ly < DG_TROWS) {
+          const int row = ly * DG_PITCH + 2 * pc + (q & 1) + 2;
+          dys[row * 8 + (c8 ^ swz8(row))] = ok ? dyc_expand(L.v[k], L.rt[k], q) : z;
+        }
+      }
+    }
+  }
+  // padding columns 0, 1, 26, 27 of every tile row: 9 x 4 x 8 = 288 zero chunks
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int jz = tid + 256 * k;
+    if (jz < DG_TROWS * 4 * 8) {
+      const int c8 = jz & 7, pcol = (jz >> 3) & 3, ly = jz >> 5;
+      const int row = ly * DG_PITCH + (pcol < 2 ? pcol : pcol + 24);
+      dys[row * 8 + (c8 ^ swz8(row))] = z;
     }
   }
 }
