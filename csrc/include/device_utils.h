@@ -21,8 +21,13 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
   return __builtin_bit_cast(uint16_t, b);
 }
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, the same bits as two f2bf calls;
+// the scalar form compiled to one conversion per value plus the packing)
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const b2_t b = __builtin_convertvector((f2_t){lo, hi}, b2_t);
+  return __builtin_bit_cast(uint32_t, b);
 }
 
 __device__ __forceinline__ floatx4 mfma16x16x32(const bf16x8& a, const bf16x8& b, floatx4 c) {
