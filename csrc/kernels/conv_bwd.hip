@@ -304,23 +304,26 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
     const int tap = lane & 15, ty = tap / 3, tx = tap - 3 * ty;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      short4_t ax, bd[2];
+      float xf[4], df[2][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = 16 * (3 * wave + i) + 4 * kg + j;
         const int qc = q < npix ? q : npix - 1;
         const int py = qc / H1, px = qc - py * H1;
-        const float xv = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
-        ax[j] = (short)f2bf(xv);
+        xf[j] = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const uint16_t av = a1v[i][j][nt];
-          const float d = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
-          bd[nt][j] = (short)f2bf(d);
+          df[nt][j] = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
         }
       }
+      // bf16 operands two at a time (one v_cvt_pk_bf16_f32 per pair)
+      const short4_t ax = __builtin_bit_cast(short4_t, uint2{pack2bf(xf[0], xf[1]), pack2bf(xf[2], xf[3])});
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) dw[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ax, bd[nt], dw[nt], 0, 0, 0);
+      for (int nt = 0; nt < 2; ++nt) {
+        const short4_t bd = __builtin_bit_cast(short4_t, uint2{pack2bf(df[nt][0], df[nt][1]), pack2bf(df[nt][2], df[nt][3])});
+        dw[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ax, bd, dw[nt], 0, 0, 0);
+      }
     }
   }
   // dw[nt]: lane l holds D[tap = 4(l>>4) + r][ci = 16nt + (l&15)]
@@ -607,7 +610,7 @@ static int dgrad_persist_grid(int B) {
     static int cus = 0;
     if (!cus) {
       int dev = 0;
-      hipGetDevice(&dev);
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
     g = 2 * cus;
