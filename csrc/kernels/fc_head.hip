@@ -18,6 +18,9 @@ namespace mnist {
 // distinct 18 KB slice of w1 (L2/MALL resident) and the grid is ceil(B/16) x 32 WGs.  All 27
 // fragment loads of a wave are independent and issued before the MFMAs.
 // ============================================================================================
+// MR = 16-row M-tiles per workgroup: MR = 2 (default) halves the w1 fragment traffic per output
+// (each wave's B fragments feed two M-tiles) at half the workgroups; bitwise the MR = 1 result.
+template <int MR>
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
                                                       const uint16_t* __restrict__ w1,
                                                       float* __restrict__ z1part, int B) {
@@ -34,31 +37,39 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
   const int xcd = lin & 7, j = lin >> 3;
   const int chunk = 4 * xcd + j / R;
   const int tile = j - (j / R) * R;
-  const int row = tile * 16 + m;
-  const bool valid = row < B;
-  const uint16_t* pa = p + (int64_t)(valid ? row : 0) * NFLAT + chunk * KC + 8 * kg;
   const uint16_t* pb = w1 + (int64_t)(32 * wave + m) * NFLAT + chunk * KC + 8 * kg;
-  bf16x8 A[KS], B0[KS], B1[KS];
+  bf16x8 A[MR][KS], B0[KS], B1[KS];
+  bool valid[MR];
+#pragma unroll
+  for (int t = 0; t < MR; ++t) {
+    const int row = (tile * MR + t) * 16 + m;
+    valid[t] = row < B;
+    const uint16_t* pa = p + (int64_t)(valid[t] ? row : 0) * NFLAT + chunk * KC + 8 * kg;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) A[t][ks] = ld16(pa + ks * 32);
+  }
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    A[ks] = ld16(pa + ks * 32);
     B0[ks] = ld16(pb + ks * 32);
     B1[ks] = ld16(pb + 16 * NFLAT + ks * 32);
   }
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const bf16x8 a = valid ? A[ks] : zero_frag();
-    acc0 = mfma16x16x32(a, B0[ks], acc0);
-    acc1 = mfma16x16x32(a, B1[ks], acc1);
-  }
+  for (int t = 0; t < MR; ++t) {
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int b = tile * 16 + 4 * kg + r;
-    if (b < B) {
-      float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
-      dst[0] = acc0[r];
-      dst[16] = acc1[r];
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 a = valid[t] ? A[t][ks] : zero_frag();
+      acc0 = mfma16x16x32(a, B0[ks], acc0);
+      acc1 = mfma16x16x32(a, B1[ks], acc1);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = (tile * MR + t) * 16 + 4 * kg + r;
+      if (b < B) {
+        float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
+        dst[0] = acc0[r];
+        dst[16] = acc1[r];
+      }
     }
   }
 }
@@ -174,8 +185,17 @@ void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B,
                        p, w1, z1part, B);
     return;
   }
-  dim3 grid((B + 15) / 16, FC1_KSPLIT);
-  hipLaunchKernelGGL(fc1_fwd_kernel, grid, dim3(256), 0, s, p, w1, z1part, B);
+  // 16-row tiles per workgroup (MNIST_AMD_FC1_MR = 1 / 2 / 4, read per call; default 2: measured
+  // B = 200 75.6-77.0 -> 73.8-74.7 us/step with 2, B = 300 97.0-97.2 -> 95.6-96.3)
+  const char* e = getenv("MNIST_AMD_FC1_MR");
+  const int mr = e ? atoi(e) : 2;
+  if (mr == 4) {
+    hipLaunchKernelGGL(fc1_fwd_kernel<4>, dim3((B + 63) / 64, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
+  } else if (mr == 1) {
+    hipLaunchKernelGGL(fc1_fwd_kernel<1>, dim3((B + 15) / 16, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
+  } else {
+    hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3((B + 31) / 32, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
+  }
 }
 
 // ============================================================================================
