@@ -56,7 +56,8 @@ from pytorch_mnist_ddp_amd.engine.state import ModelState  # noqa: E402
 from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer  # noqa: E402
 from pytorch_mnist_ddp_amd.models.net import Net  # noqa: E402
 from pytorch_mnist_ddp_amd.parallel.distributed import (_max_over_ranks, broadcast_,  # noqa: E402
-                                                        create_rccl_comms)
+                                                        create_rccl_comms, params_fingerprint_equal)
+from pytorch_mnist_ddp_amd.utils.profiling import PhaseTimes  # noqa: E402
 
 METRIC = "images/sec + 20-epoch wallclock, MNIST CNN DDP at 1/2/4/8 MI355X"
 CPU_ANCHOR_IMG_S = 3518.0      # torch fp32 CPU train step, B=64, 8 vCPU dev box
@@ -64,12 +65,18 @@ _LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RA
                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
 
 
-def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 900.0, extra=()) -> dict:
+def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 900.0, extra=(),
+                         with_setup: bool = True) -> dict:
     """The reference's README command at this N (mnist_ddp.py, README.md:41-51) as a child job;
-    returns the max over ranks of its ``Total cost time`` print, the child's wall time and the last
-    printed test accuracy."""
+    returns the max over ranks of its ``Total cost time`` print, the child's wall time, the last
+    printed test accuracy and (``with_setup``: ``--json-log``) the per-phase startup seconds inside
+    that timer (max over ranks per phase) plus the summed per-epoch train/eval time."""
+    import tempfile
     script = os.path.join(ROOT, "mnist_ddp.py")
+    jlog = tempfile.NamedTemporaryFile(prefix="mnist_amd_child_", suffix=".jsonl", delete=False).name
     sargs = ["--batch-size", str(batch), "--epochs", str(epochs), "--synthetic", *extra]
+    if with_setup:
+        sargs += ["--json-log", jlog]
     env = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC")}
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     if world == 1:
@@ -89,6 +96,24 @@ def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 9
            "test_acc": round(int(accs[-1][0]) / int(accs[-1][1]), 4) if accs else None}
     if r.returncode != 0 or len(times) != world:
         out["stderr_tail"] = r.stderr[-1500:]
+    if with_setup:
+        try:
+            recs = [json.loads(ln) for ln in open(jlog) if ln.strip()]
+            setups = [rc["setup_s"] for rc in recs if "setup_s" in rc]
+            if setups:
+                keys = list(dict.fromkeys(k for st in setups for k in st))
+                out["setup_phases_s"] = {k: round(max(st.get(k, 0.0) for st in setups), 3) for k in keys}
+                out["setup_total_s"] = round(max(sum(st.values()) for st in setups), 3)
+            ep = [rc for rc in recs if "epoch" in rc]
+            if ep:
+                out["epochs_train_s_rank_sum"] = round(sum(rc.get("train_s", 0.0) for rc in ep), 3)
+        except (OSError, ValueError):
+            pass
+        finally:
+            try:
+                os.unlink(jlog)
+            except OSError:
+                pass
     return out
 
 
@@ -170,6 +195,8 @@ def main() -> int:
     ap.add_argument("--cpu", action="store_true", help="reference CPU config (mnist.py --no-cuda, batch 64)")
     ap.add_argument("--no-script-run", dest="script_run", action="store_false",
                     help="skip the mnist_ddp.py child job (total_cost_time_s)")
+    ap.add_argument("--no-warm-replay", dest="warm_replay", action="store_false",
+                    help="do not replay the timed region's graphs once (state restored) before the warmup")
     args = ap.parse_args()
     if args.cpu:
         return cpu_bench(200 if args.steps is None else args.steps, 10 if args.warmup is None else args.warmup)
@@ -186,32 +213,42 @@ def main() -> int:
             return 2
     if os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
         local = 0                      # one-GPU multi-rank rehearsal (gloo + xgmi only)
+    phases = PhaseTimes()              # host seconds per setup phase (JSON "setup_phases_s")
+    t_setup = time.perf_counter()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
     if use_pg:
         kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
-        dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank, **kw)
-    t_setup = time.perf_counter()
+        with phases.phase("pg_init"):
+            dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank, **kw)
 
     B = args.batch_size
-    torch.manual_seed(args.seed)
-    net = Net()
-    train = load_mnist(train=True, synthetic_data=True, verbose=False)
-    test = load_mnist(train=False, synthetic_data=True, verbose=False) if rank == 0 else None
-    sampler = DistributedIndexStream(len(train), world, rank, shuffle=True, seed=0)
-    total = args.warmup + args.steps
-    steps_per_epoch = math.ceil(len(sampler) / B)
-    num_samples = max(total * B, steps_per_epoch * B)
-    ms = ModelState(net, dev, lr=1.0)
-    # RCCL communicators for the gradient all-reduce / its probe (none when the xGMI kernels are forced)
+    with phases.phase("data_model"):
+        torch.manual_seed(args.seed)
+        net = Net()
+        train = load_mnist(train=True, synthetic_data=True, verbose=False)
+        test = load_mnist(train=False, synthetic_data=True, verbose=False) if rank == 0 else None
+        sampler = DistributedIndexStream(len(train), world, rank, shuffle=True, seed=0)
+        total = args.warmup + args.steps
+        steps_per_epoch = math.ceil(len(sampler) / B)
+        num_samples = max(total * B, steps_per_epoch * B)
+        ms = ModelState(net, dev, lr=1.0)
+    # the RCCL communicator for the gradient all-reduce / its probe (none when the xGMI kernels are
+    # forced); a second one only on opt-in (MNIST_AMD_RCCL_COMMS=2)
     rccl = use_pg and args.allreduce != "xgmi"
-    comm, comm2 = create_rccl_comms(world, rank, local) if rccl else (None, None)
+    comm, comm2 = (None, None)
+    if rccl:
+        with phases.phase("rccl_comms"):
+            comm, comm2 = create_rccl_comms(world, rank, local)
+    t_tr = time.perf_counter()
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
                       two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
+    phases.add("trainer", time.perf_counter() - t_tr)
     if use_pg:                        # DDP construction semantics: rank-0 weights everywhere
-        _broadcast_params(tr, comm)
+        with phases.phase("broadcast"):
+            _broadcast_params(tr, comm)
 
     # flat index stream = consecutive DistributedSampler epochs, full batches only
     parts, ep = [], 1
@@ -222,8 +259,18 @@ def main() -> int:
         ep += 1
     stream = torch.cat(parts)[: total * B]
     tr.start_stream(stream, gather=False)
+    cap0 = tr.setup.s.get("graph_capture", 0.0)
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
+    phases.add("graph_capture", tr.setup.s.get("graph_capture", 0.0) - cap0)
+    if args.warm_replay and args.steps > 0:
+        # every graph the timed region replays has run once before t0 (model, optimizer and step
+        # state restored bit for bit): the first timed replay pays no first-launch cost, and exactly
+        # --steps steps are timed after exactly --warmup warmup steps
+        with phases.phase("warm_replay"):
+            first = max(tr._chunks(args.steps)) if tr.use_graphs else 0
+            tr.engine.gather_rows(0, min(total, max(first, args.warmup)) * B)
+            tr.warm_graphs(args.steps)
     if comm is not None:   # RCCL lazily sets up its channels on the first collective: do it untimed
         tr.synchronize()
     tr.engine.gather_rows(0, args.warmup * B)
@@ -247,30 +294,36 @@ def main() -> int:
     # DDP correctness of the timed run: every rank must hold bitwise identical parameters
     in_sync = True
     if use_pg:
-        from pytorch_mnist_ddp_amd.parallel.distributed import params_fingerprint_equal
         in_sync = params_fingerprint_equal(ms.param, dev)
     comm_info = {"allreduce": tr.allreduce if world > 1 or comm is not None else None,
                  "rccl_world": comm.world_size if comm is not None else None,
+                 "rccl_comms": (1 if comm is not None else 0) + (1 if comm2 is not None else 0),
                  "allreduce_probe_us": tr.allreduce_timings or None,
                  "xgmi_validation": tr.xgmi_validation,
+                 "xgmi_ordering": tr.xgmi.ordering if tr.xgmi is not None else None,
                  "conv_bucket_split": tr.conv_split,
                  "xgmi_grids": ({k: v for k, v in tr.xgmi.grids.items() if not k.startswith("cap")}
                                 if tr.xgmi is not None else None)}
+    phases.update(tr.setup, prefix="trainer.")
 
-    # ---- the README workload end to end: 20 epochs train + rank-0 eval, fresh model
+    # ---- the README workload end to end: 20 epochs train + rank-0 eval, fresh model, on the SAME
+    # trainer (engine, graphs, communicators, all-reduce choice and validation reused, state reset)
     wall = None
     acc = None
+    desync_epoch = None
     if args.full_run and rank == 0:
         tr.evaluate()         # untimed, like the training kernels above: load the eval kernels' code
     if args.full_run:
+        from pytorch_mnist_ddp_amd.parallel.ddp import params_fingerprint
         torch.manual_seed(args.seed)
-        net2 = Net()
-        ms2 = ModelState(net2, dev, lr=1.0)
-        tr2 = FusedTrainer(ms2, train, test, B, 1000, num_samples=len(sampler), world_size=world, rank=rank,
-                           comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                           two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
+        tr.reset_model(Net())
         if use_pg:
-            _broadcast_params(tr2, comm)
+            _broadcast_params(tr, comm)
+        fps = []
+        if use_pg:
+            with torch.cuda.stream(tr.compute):
+                params_fingerprint([ms.param])      # load its kernels' code outside the timed window
+        tr.synchronize()
         if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
@@ -278,20 +331,35 @@ def main() -> int:
         sampler.set_epoch(1)
         idx = sampler.epoch_indices()
         for epoch in range(1, args.epochs + 1):
-            tr2.set_lr(1.0 * (0.7 ** (epoch - 1)))
-            tr2.train_epoch(epoch, idx, sync=False)      # enqueued; the GPU runs while the host
+            tr.set_lr(1.0 * (0.7 ** (epoch - 1)))
+            tr.train_epoch(epoch, idx, sync=False)       # enqueued; the GPU runs while the host
+            if use_pg:                                   # per-epoch cross-rank fingerprint, on the
+                with torch.cuda.stream(tr.compute):      # device (compared after the run: no sync)
+                    fps.append(params_fingerprint([ms.param]))
             if epoch < args.epochs:                      # draws the next epoch's sampler order
                 sampler.set_epoch(epoch + 1)
                 idx = sampler.epoch_indices()
             if rank == 0:
-                ls, correct, n = tr2.evaluate()
+                ls, correct, n = tr.evaluate()
                 acc = correct / max(1, n)
-        tr2.synchronize()
+        tr.synchronize()
         if use_pg:
             dist.barrier()
         w1 = time.perf_counter()
         wall = w1 - w0
         wall = _max_over_ranks(wall, dev)
+        if use_pg:                                       # which epoch (if any) first desynced
+            mine = torch.stack(fps)
+            allv = [torch.zeros_like(mine) for _ in range(world)]
+            if dist.get_backend() != "nccl":
+                mine = mine.cpu()
+                allv = [v.cpu() for v in allv]
+            dist.all_gather(allv, mine)
+            for e in range(len(fps)):
+                if any(not torch.equal(v[e], allv[0][e]) for v in allv):
+                    desync_epoch = e + 1
+                    in_sync = False
+                    break
 
     # ---- the reference's own metric, measured the reference's way (child job at the same N)
     script = None
@@ -336,13 +404,14 @@ def main() -> int:
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
                        "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
-                       **comm_info},
+                       "warm_replay": bool(args.warm_replay), **comm_info},
             "params_in_sync": in_sync,
+            "desync_epoch": desync_epoch,
             "total_cost_time_s": script.get("total_cost_time_s") if script else None,
             "reference_script": script,
             "wallclock_20ep_s": round(wall, 3) if wall is not None else None,
-            "wallclock_20ep_note": "in-process 20 epochs on built trainers: excludes PG init, data build, "
-                                   "model/comm setup, log syncs (total_cost_time_s is the reference's timer)",
+            "wallclock_20ep_note": "in-process 20 epochs on the built trainer (state reset): excludes PG init, "
+                                   "data build, model/comm setup, log syncs (total_cost_time_s is the reference's timer)",
             "baseline_wallclock_20ep_s": base,
             "vs_baseline_wallclock": (round(base / script["total_cost_time_s"], 1)
                                       if (base and script and script.get("total_cost_time_s")) else None),
@@ -350,13 +419,15 @@ def main() -> int:
             "final_test_acc": round(acc, 4) if acc is not None else None,
             "last_train_loss": round(final_loss, 4),
             "setup_s": round(t0 - t_setup, 2),
+            "setup_phases_s": phases.rounded(3),
         }
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     if not in_sync:
-        print("bench.py: DDP desync - ranks hold different parameters after the timed steps", file=sys.stderr)
+        where = f" (first differing epoch of the 20-epoch run: {desync_epoch})" if desync_epoch else ""
+        print(f"bench.py: DDP desync - ranks hold different parameters{where}", file=sys.stderr)
         return 1
     return 0
 

@@ -243,6 +243,7 @@ PYBIND11_MODULE(_C, m) {
         if (which != "in" && which != "out") throw std::runtime_error("dlpack: which must be 'in' or 'out'");
         return dlpack_f32(which == "in" ? c->in() : c->out(), c->numel(), c->device(), c);
       })
+      .def_property_readonly("ordering", &XgmiComm::ordering)
       .def_property_readonly("grids", [](const XgmiComm& c) {
         const XgmiGrids& g = c.grids();
         py::dict d;

@@ -98,7 +98,9 @@ struct FcBwdArgs {
   float* grad;                // flat fp32 grad buffer (writes fc1.w, fc1.b, fc2.w, fc2.b)
   uint8_t* dyc;               // compact grad wrt conv2 output: [B][144] records (see DYC_REC)
   float* loss_log;            // [steps] mean loss per step (indexed by state->step)
-  float grad_scale;           // 1/world_size (DDP averaging folded into the GEMM epilogue)
+  float grad_scale;           // extra gradient scale applied in the epilogue.  The engine passes 1.0: its
+                              // DDP averaging lives in the head (inv_batch = 1/(B*world)); only a caller
+                              // that leaves inv_batch at 1/B would pass 1/world_size here
   float inv_batch;
   float* part;                // B > FC_BWD_SPLIT_ROWS: [fc_bwd_splits(B)][FCB_PART_STRIDE] partial fc grads
   FcUpdate upd;               // optional fused fc Adadelta (zero-initialised = off)
@@ -133,7 +135,7 @@ struct ConvBwdArgs {
   float* c1part;              // [4*B][320] conv1 wgrad(288)+bias(32) partials (dgrad kernel)
   float* w2part;              // [G][18432 + 64] conv2 wgrad + bias partials
   float* grad;                // flat fp32 grad buffer (conv params written by the reduce kernel)
-  float grad_scale;
+  float grad_scale;           // as FcBwdArgs::grad_scale: 1.0 from the engine (averaging in the head)
   int wgrad_groups;           // G
   const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
   int* signal_ctr;            // optional: conv2_wgrad / conv2_dgrad add 1 at kernel start (schedule-3 hand-offs)
@@ -219,6 +221,7 @@ struct XgmiArgs {
   AdadeltaArgs ada;
   int max_wg;                        // residency cap on the launch grid (XgmiGrids; every rank the same)
   int release;                       // system-scope release fence before each stage flag store
+  int acquire;                       // system-scope acquire after each matched stage poll (opt-in)
 };
 // Every xGMI kernel's workgroup b spins until workgroup b of every peer arrives, so the workgroups
 // that can be spinning at the same moment - on one GPU: the fc-bucket kernel on the comm stream and

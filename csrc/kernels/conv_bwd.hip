@@ -14,7 +14,8 @@
 //    over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
 //    from ds_read_b64_tr_b16 with per-lane row addresses, so the im2col gather is free.
 //  * conv_grad_reduce_kernel: fixed-order (deterministic) sum of the partial slabs into the flat
-//    fp32 gradient buffer, scaled by 1/world_size (DDP averaging).
+//    fp32 gradient buffer, scaled by grad_scale (1.0 from the engine, whose head already carries
+//    the 1/(B*world) DDP averaging).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 #include "conv_grad_reduce.h"

@@ -844,7 +844,8 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
 }
 
 // S > 1: fixed-order sum of the split partials (fc1.w, fc1.b, fc2.w, fc2.b share the grad layout
-// [0, OFF_FC2_B + 10)), scaled by 1/world_size, plus the mean loss.
+// [0, OFF_FC2_B + 10)), scaled by grad_scale (1.0 from the engine: the head carries 1/(B*world)),
+// plus the mean loss.
 __global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B, int S) {
   constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;   // float4 columns (the tail pads into fc2.b's pad)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;

@@ -20,6 +20,32 @@
 // stores; flags are system-scope atomics carrying a per-WG call counter (monotonic, no reset, so
 // graph replays need no host work).  A wait that exceeds the timeout sets *err and returns; every
 // later call then returns at once and the host raises (XgmiComm::check).
+//
+// Cross-device ordering: why no release / acquire fence is needed by default.  Each rule below is
+// the gfx942/gfx950 mapping of the LLVM AMDGPU memory model (AMDGPUUsage, "memory model gfx942")
+// or a measured gfx950 fact from docs (MI355X_MICROARCH.md, visibility tables):
+//  R1  every buffer a peer reads or writes (input / output buckets, staging slots, flag blocks) is
+//      allocated hipDeviceMallocUncached (XgmiComm ctor): MTYPE UC, so no L2 of either GPU ever
+//      holds a line of it - the only stale-data path the system-scope fences exist for (buffer_wbl2
+//      writes back dirty L2 lines, buffer_inv sc0 sc1 drops clean non-coherent ones) has nothing to
+//      act on.  RCCL relies on the same property for its LL/LL128 FIFOs on MI300-class GPUs
+//      (uncached, peer-mapped, polled without reader-side invalidates).
+//  R2  every payload store a peer reads is `sc0 sc1` (st_sys / st_sys1) - the gfx942 mapping of a
+//      system-scope monotonic atomic store - or a plain store into an R1 buffer by a kernel that
+//      COMPLETED before this launch on the same stream (the gradient producers writing the input
+//      bucket: kernel boundary);
+//  R3  every storing wave runs `s_waitcnt vmcnt(0)` (gfx9 counts stores in vmcnt: the wait returns
+//      once each store is acknowledged by the memory side) and the workgroup barrier follows, before
+//      the ONE lane per peer that stores the flag - a system-scope atomic store;
+//  R4  the reader polls the flag with system-scope atomic loads and issues its payload loads only
+//      after the poll matched (and the workgroup barrier after it); every payload load is `sc0 sc1`
+//      (ld_sys / ld_sys1) - the gfx942 mapping of a system-scope monotonic atomic load, which must
+//      observe the latest value in coherence order and is never served from L1.
+// R1 + R2 + R3: when the flag becomes visible at a peer, every payload byte is in the owner's HBM;
+// R1 + R4: the peer's loads read HBM, not a cached copy.  The fences stay available as knobs
+// (MNIST_AMD_XGMI_RELEASE=1: buffer_wbl2 sc0 sc1 before every flag, +13 us per world-1 step;
+// MNIST_AMD_XGMI_ACQUIRE=1: buffer_inv sc0 sc1 after every matched poll) and XgmiComm::ordering()
+// names the mode in use (bench JSON "xgmi_ordering").
 #include <stdexcept>
 #include <string>
 
@@ -74,6 +100,7 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e, int kid) 
     }
   }
   const bool all = __syncthreads_and(ok);
+  if (a.acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // opt-in system-scope acquire (R1/R4 above)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the payload loads below
   return all;
 }

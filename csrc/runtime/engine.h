@@ -63,8 +63,10 @@ class Engine {
   ~Engine();
 
   void attach_comm(std::shared_ptr<RcclComm> comm);   // enables the overlapped DDP path
-  // second communicator for the fc bucket: lets it stay in flight across the step boundary
-  // (joined only before the next step's fc1) while the conv bucket reduces on the first
+  // optional second communicator for the fc bucket (opt-in, MNIST_AMD_RCCL_COMMS=2): its all-reduce
+  // may then overlap the conv bucket's on the first.  Concurrent collectives on two communicators are
+  // deadlock-prone in NCCL/RCCL, so by default schedule 3 runs both buckets on ONE communicator,
+  // ordered fc -> conv by a device counter (see enqueue_step)
   void attach_comm2(std::shared_ptr<RcclComm> comm);
   // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC over x->in() -> x->out()) in place
   // of the RCCL all-reduces of schedule 3; while attached the gradient producers write x->in()
@@ -88,7 +90,8 @@ class Engine {
   //   so it overlaps the conv backward, the conv bucket, the conv update AND the next trunk_fwd;
   // 3 = as 2, but the per-step fork / join are device-counter hand-offs (one-WG signal / wait
   //   kernels) instead of captured cross-queue edges; only each chunk's first fork and last join
-  //   are graph edges
+  //   are graph edges.  Needs only attach_comm (or the xGMI comm): with one RCCL communicator the
+  //   conv all-reduce waits on a counter for the fc all-reduce of the same step
   void set_dist_schedule(int s) { dist_sched_ = s; }
   // Schedule 3 spins on one stream until the other signals; that is only deadlock-free when the
   // compute and comm streams sit on different hardware queues (HIP shares queues beyond
@@ -157,7 +160,8 @@ class Engine {
   bool xgmi_fuse_update_ = true;
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
-  int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error
+  int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error,
+                                    // [3]/[4] conv split, [8..11] probes, [12] fc all-reduce done (1 comm)
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
   bool dgrad_update_ = true;

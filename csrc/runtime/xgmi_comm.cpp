@@ -205,15 +205,38 @@ XgmiArgs XgmiComm::args(int channel, int64_t offset, int64_t count) const {
   a.nvec = count / 4;
   a.timeout_ticks = timeout_ticks_;
   a.max_wg = XGMI_MAX_WG;
-  // system-scope release fence before every stage flag (buffer_wbl2 of the XCD's dirty L2 lines):
-  // off by default - the payload is already write-through (sc0 sc1) into uncached buckets and
-  // drained (vmcnt) before the flag, and the fence measured +13 us per world-1 step (100.5 vs 87.5)
-  static const int release = [] {
+  // system-scope release fence before every stage flag (buffer_wbl2 of the XCD's dirty L2 lines) /
+  // acquire after every matched poll: off by default - rules R1-R4 in xgmi_allreduce.hip order the
+  // payload without them; the release fence measured +13 us per world-1 step (100.5 vs 87.5)
+  a.release = fence_release();
+  a.acquire = fence_acquire();
+  return a;
+}
+
+int XgmiComm::fence_release() {
+  static const int v = [] {
     const char* e = getenv("MNIST_AMD_XGMI_RELEASE");
     return e ? atoi(e) : 0;
   }();
-  a.release = release;
-  return a;
+  return v;
+}
+
+int XgmiComm::fence_acquire() {
+  static const int v = [] {
+    const char* e = getenv("MNIST_AMD_XGMI_ACQUIRE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+std::string XgmiComm::ordering() const {
+  const char* uc = getenv("MNIST_AMD_XGMI_UNCACHED");
+  const bool uncached = uc ? atoi(uc) != 0 : kUncachedDefault;
+  std::string s = uncached ? "uncached+sc0sc1" : "cached+sc0sc1";
+  if (fence_release()) s += "+release";
+  if (fence_acquire()) s += "+acquire";
+  if (!fence_release() && !fence_acquire()) s += " (no fence: xgmi_allreduce.hip R1-R4)";
+  return s;
 }
 
 void XgmiComm::allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada) {

@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 #include <vector>
 
 #include "../include/kernels.h"
@@ -55,6 +56,10 @@ class XgmiComm {
   // device error code (0 = ok; else the first stage wait that timed out on this rank:
   // kernel id << 24 | stage << 16 | peer << 12 | workgroup); synchronous read
   int error() const;
+  // how peer-visible payload is ordered (bench JSON "xgmi_ordering"; rules in xgmi_allreduce.hip)
+  std::string ordering() const;
+  static int fence_release();   // MNIST_AMD_XGMI_RELEASE
+  static int fence_acquire();   // MNIST_AMD_XGMI_ACQUIRE
   const XgmiGrids& grids() const { return grids_; }
   void set_timeout_seconds(double s);
   int world_size() const { return world_; }

@@ -27,6 +27,7 @@ from .models.net import Net
 from .optim import Adadelta, StepLR
 from .utils.checkpoint import load_state_dict, save_state_dict
 from .utils.logging import test_line, total_time_line, train_line
+from .utils.profiling import PhaseTimes
 
 
 def _json_log(path, rec):
@@ -84,9 +85,12 @@ def run(argv=None, ddp_script: bool = True) -> int:
     args._ddp_script = ddp_script
     use_cuda = not args.no_cuda and torch.cuda.is_available()
     distributed, world, rank, gpu = False, 1, 0, 0
+    setup = PhaseTimes()             # startup phases inside the reference timer (--json-log "setup_s")
+    args._setup = setup
     if ddp_script:
         from .parallel.distributed import init_distributed_mode
-        init_distributed_mode(args)
+        with setup.phase("pg_init"):
+            init_distributed_mode(args)
         distributed = args.distributed
         if distributed:
             world, rank, gpu = args.world_size, args.rank, args.gpu
@@ -94,8 +98,9 @@ def run(argv=None, ddp_script: bool = True) -> int:
     device = torch.device(f"cuda:{gpu}" if use_cuda else "cpu") if ddp_script else \
         torch.device("cuda" if use_cuda else "cpu")
 
-    train_data = load_mnist(args.data_root, True, args.synthetic, args.synthetic_train_size, verbose=rank == 0)
-    test_data = load_mnist(args.data_root, False, args.synthetic, args.synthetic_test_size, verbose=rank == 0)
+    with setup.phase("data"):
+        train_data = load_mnist(args.data_root, True, args.synthetic, args.synthetic_train_size, verbose=rank == 0)
+        test_data = load_mnist(args.data_root, False, args.synthetic, args.synthetic_test_size, verbose=rank == 0)
     if ddp_script:
         train_stream = (DistributedIndexStream(len(train_data), world, rank, shuffle=True) if distributed
                         else RandomIndexStream(len(train_data)))
@@ -162,6 +167,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     from .engine.state import ModelState
     from .engine.trainer import FusedTrainer
     from .utils.profiling import roctx_range
+    setup = args._setup
+    t_model = time.perf_counter()
     ms = ModelState(model, device, lr=args.lr)
     model_for_save = model
     comm = comm2 = None
@@ -170,14 +177,19 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     if distributed:
         from .parallel.ddp import DistributedDataParallel, engine_bucket_layout
         from .parallel.distributed import create_rccl_comms
-        ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
-                                      bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
+        setup.add("model", time.perf_counter() - t_model)
+        with setup.phase("ddp_wrap"):
+            ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
+                                          bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
         model_for_save = ddp
         two_buckets = engine_bucket_layout(ddp.bucket_indices)   # raises on a layout the engine cannot run
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("--allreduce xgmi needs the two-bucket layout (default --bucket-cap-mb/--first-bucket-mb)")
         if allreduce != "xgmi":              # xgmi-only DDP needs no RCCL communicator at all
-            comm, comm2 = create_rccl_comms(world, rank, gpu)
+            with setup.phase("rccl_comms"):
+                comm, comm2 = create_rccl_comms(world, rank, gpu)
+    else:
+        setup.add("model", time.perf_counter() - t_model)
     # The optimizer here is the engine's fused Adadelta kernel (state in `ms`); StepLR(step_size=1)
     # (reference mnist_ddp.py:178, :189) reduces to lr <- lr * gamma after every epoch, computed in
     # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
@@ -211,6 +223,10 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         with roctx_range(f"train_epoch_{epoch}", args.profile):
             st = trainer.train_epoch(epoch, idx, args.log_interval,
                                      dry_run=args.dry_run, log_fn=log_fn if log_rank else None)
+        if epoch == 1:                     # the trainer's phases include epoch 1's graph captures
+            setup.update(trainer.setup, prefix="trainer.")
+            _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
+                                      "allreduce": trainer.allreduce if distributed else None})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
                "img_per_s": st.samples / max(st.train_seconds, 1e-9), "device_train_s": st.device_seconds}
         if st.device_seconds:

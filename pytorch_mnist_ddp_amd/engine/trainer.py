@@ -27,7 +27,18 @@ import torch
 
 from ..data.datasets import MNISTData
 from ..ops import native
+from ..utils.profiling import PhaseTimes
 from .state import FLAG_NO_DROPOUT, ModelState
+
+
+def _fault_delay(kind: str, rank: int) -> float:
+    """Seconds to hold rank ``rank`` back at fault point ``kind`` (``MNIST_AMD_FAULT=kind:rank:seconds``,
+    tests only); 0 when not injected."""
+    spec = os.environ.get("MNIST_AMD_FAULT", "")
+    parts = spec.split(":")
+    if len(parts) == 3 and parts[0] == kind and int(parts[1]) == rank:
+        return float(parts[2])
+    return 0.0
 
 
 @dataclass
@@ -48,6 +59,10 @@ class FusedTrainer:
                  fuse_fc_update: bool | None = None, allreduce: str | None = None):
         C = native.load()
         self.C, self.ms = C, mstate
+        # host seconds per setup phase (engine, xgmi_comm, allreduce_probe, stream_probe, validation,
+        # graph_capture): the N > 1 startup budget inside the reference's timer
+        self.setup = PhaseTimes()
+        _t_init = time.perf_counter()
         dev = mstate.device
         self.device = dev
         self.B, self.TB = int(batch_size), int(test_batch_size)
@@ -91,6 +106,11 @@ class FusedTrainer:
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay)
         self.engine.set_bucket_split(two_buckets)
+        self._graphs: dict[tuple[int, int], int] = {}
+        self._eval_graph: int | None = None
+        # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)
+        self.profile_left = 0
+        self.use_graphs = self.graph_steps > 0
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
@@ -109,10 +129,11 @@ class FusedTrainer:
         # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
         # (opt-in MNIST_AMD_DGRAD_UPDATE=1, bitwise equal; measured 81.6-82.2 vs 80.9-81.8 us/step)
         self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "0") == "1")
-        # DDP schedule: 3 (fc bucket on its own communicator, overlapping across the step boundary,
-        # device-counter stream hand-offs) when a second communicator is given, else 1
+        # DDP schedule: 3 (the fc bucket all-reduced + updated on the comm stream, overlapping the conv
+        # backward and the step boundary, device-counter stream hand-offs; with one communicator the
+        # conv all-reduce waits for the fc one on a counter) whenever a communicator is attached
         # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)
-        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "3" if comm2 is not None else "1"))
+        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "3"))
         self.engine.set_dist_schedule(sched)
         if comm is not None:
             self.engine.attach_comm(comm)
@@ -142,7 +163,8 @@ class FusedTrainer:
         self.xgmi_fuse = os.environ.get("MNIST_AMD_XGMI_FUSE", "1") != "0"
         if want:
             from ..parallel.distributed import choose_allreduce, create_xgmi_comm
-            self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad.numel())
+            with self.setup.phase("xgmi_comm"):
+                self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad.numel())
             if self.xgmi is not None and allreduce == "auto":
                 split = mstate.bucket_split
                 upd = []
@@ -156,7 +178,7 @@ class FusedTrainer:
                                               mstate.weight_decay, p_(scratch["w2f"]), p_(scratch["w2d"]),
                                               p_(mstate.w1), p_(mstate.w1t), 0, 2, True,
                                               int(torch.cuda.current_stream(dev).cuda_stream))]
-                with torch.cuda.stream(self.compute):
+                with torch.cuda.stream(self.compute), self.setup.phase("allreduce_probe"):
                     pick, self.allreduce_timings = choose_allreduce(
                         comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad,
                         (0, split), (split, mstate.grad.numel() - split), dev, rccl_extra=upd)
@@ -181,6 +203,7 @@ class FusedTrainer:
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3) or self.overlap_fc
         if uses_sched3:
             from ..parallel.distributed import STARTUP_TIMEOUT_S, _all_ok
+            _t_probe = time.perf_counter()
             ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
             if world_size > 1:
                 ok = _all_ok(ok, dev)
@@ -190,7 +213,7 @@ class FusedTrainer:
                 ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
                 if world_size > 1:
                     ok = _all_ok(ok, dev)
-            if not ok and self.overlap_fc:
+            if not ok and self.overlap_fc and self.xgmi is None and comm is None:
                 self.overlap_fc = False                  # single GPU: plain serial schedule instead
                 self.engine.set_overlap_fc_update(False)
                 ok = True
@@ -201,12 +224,16 @@ class FusedTrainer:
                 if rank == 0:
                     print("[engine] compute/comm streams share a hardware queue: DDP schedule 3 disabled",
                           flush=True)
-                self.engine.set_dist_schedule(2 if comm2 is not None else 1)
+                self.engine.set_dist_schedule(2 if comm2 is not None else 1)   # graph-edge joins
                 if self.xgmi is not None:
                     self.engine.attach_xgmi(None)
                     self.xgmi = None
+            self.setup.add("stream_probe", time.perf_counter() - _t_probe)
         if self.xgmi is not None and os.environ.get("MNIST_AMD_XGMI_VALIDATE", "1") != "0":
+            _t_val, _cap0 = time.perf_counter(), self.setup.s.get("graph_capture", 0.0)
             ok, self.xgmi_validation = self._validate_xgmi_schedule(train)
+            # (the training graph it captures is booked under graph_capture)
+            self.setup.add("validation", time.perf_counter() - _t_val - (self.setup.s.get("graph_capture", 0.0) - _cap0))
             if not ok:
                 if comm is None:
                     raise RuntimeError(f"xGMI schedule failed its startup validation ({self.xgmi_validation}) "
@@ -215,35 +242,44 @@ class FusedTrainer:
                     print(f"[xgmi] startup validation failed ({self.xgmi_validation}): using RCCL", flush=True)
                 self.engine.attach_xgmi(None)
                 self.xgmi = None
-                self.engine.set_dist_schedule(sched if comm2 is not None else 1)
+                self._graphs.clear()             # captured with the xGMI kernels: recapture on RCCL
+                self.engine.set_dist_schedule(sched)
+        if world_size > 1 and self.xgmi is None and comm is None:
+            # no transport left (xGMI setup / self-test / validation failed and no RCCL communicator
+            # was created, e.g. --allreduce xgmi): training on would let every rank drift apart
+            # silently with a gradient 1/world too small - fail instead
+            raise RuntimeError(f"world size {world_size}: the xGMI all-reduce is unavailable "
+                               f"({self.xgmi_validation or 'setup or self-test failed'}) and no RCCL "
+                               "communicator is attached; rerun with --allreduce rccl or auto")
         self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
         # the all-reduced gradients (xGMI: the communicator's output buffer; the inputs are written
         # to its input buffer instead of mstate.grad while it is attached)
         self.grad_out = self.xgmi.grad_out if self.xgmi is not None else None
-        self._graphs: dict[tuple[int, int], int] = {}
-        self._eval_graph: int | None = None
-        # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)
-        self.profile_left = 0
-        self.use_graphs = self.graph_steps > 0
+        self.setup.add("engine", time.perf_counter() - _t_init - self.setup.total())
 
     # ------------------------------------------------------------------ startup validation
-    def _validate_xgmi_schedule(self, train: MNISTData, steps: int = 3) -> tuple[bool, str]:
-        """Run the exact xGMI DDP schedule the trainer will use (eager schedule-3 steps, dropout off,
-        STARTUP_TIMEOUT_S stage timeouts) on scratch copies of the optimizer state before training starts; with the
-        fused kernels also the separate-launch schedule, which must give the same bits.  Passes when no
-        rank timed out, fused == separate, and every rank holds the same parameters afterwards.  Every
-        mode's verdict is collective (all ranks stop at the first failing mode, so no rank is left
-        waiting in kernels its peers never launch) and the message names every failing rank.  The
-        model state is restored either way."""
-        from ..parallel.distributed import gather_strings, params_fingerprint_equal
+    def _validate_xgmi_schedule(self, train: MNISTData) -> tuple[bool, str]:
+        """Run the production xGMI DDP schedule before training starts: the captured chunk graph of
+        ``graph_steps`` steps that training replays (cached and reused by training; eager steps only
+        when graphs are off), dropout off, STARTUP_TIMEOUT_S stage timeouts (baked into that graph's
+        kernel arguments), on the live state, which is restored bit for bit afterwards.  With the
+        fused kernels the separate-launch schedule runs too (its own graph, not kept) and must give
+        the same bits.  Passes when no rank timed out, fused == separate, and every rank holds the
+        same parameters afterwards.  Every mode's verdict is collective (all ranks stop at the first
+        failing mode, so no rank is left waiting in kernels its peers never launch) and the message
+        names every failing rank.  Fault injection for tests: ``MNIST_AMD_FAULT=validate_delay:R:S``
+        holds rank R's replay back S seconds (its peers' stage waits must time out)."""
+        from ..parallel.distributed import STARTUP_TIMEOUT_S, gather_strings, params_fingerprint_equal
         ms, eng = self.ms, self.engine
-        steps = max(1, min(steps, self.steps_per_epoch))
-        keys = ("param", "square_avg", "acc_delta")
+        n = self.graph_steps if self.use_graphs else 3
+        n = max(1, min(n, self.steps_per_epoch))
+        keys = ("param", "square_avg", "acc_delta", "state")
+        torch.cuda.synchronize(self.device)
         snap = {k: getattr(ms, k).clone() for k in keys}
-        idx = torch.arange(steps * self.B, dtype=torch.int64) % max(1, len(train))
+        idx = torch.arange(n * self.B, dtype=torch.int64) % max(1, len(train))
         modes = [True, False] if self.xgmi_fuse else [False]
+        delay = _fault_delay("validate_delay", self.rank)
         results, why = [], ""
-        from ..parallel.distributed import STARTUP_TIMEOUT_S
         self.xgmi.set_timeout_seconds(STARTUP_TIMEOUT_S)
         for fuse in modes:
             mode = "fused" if fuse else "separate"
@@ -257,7 +293,15 @@ class FusedTrainer:
                 eng.set_xgmi_fuse_update(fuse)
                 self.upload_indices(idx)
                 eng.begin_epoch(self.seed, 0, 0, FLAG_NO_DROPOUT)
-                eng.train_steps(steps, self.B, self.B)
+                if self.use_graphs:
+                    # the training graph itself for the trainer's mode; the other mode's is throwaway
+                    gid = self._graph(n, self.B) if fuse == self.xgmi_fuse else eng.capture_train(n, self.B, self.B)
+                    if delay:
+                        eng.synchronize()
+                        time.sleep(delay)
+                    eng.replay(gid)
+                else:
+                    eng.train_steps(n, self.B, self.B)
                 eng.synchronize()                       # raises on a stage / hand-off timeout
                 results.append(ms.param.clone())
                 if not torch.isfinite(results[-1]).all():
@@ -284,7 +328,24 @@ class FusedTrainer:
         torch.cuda.synchronize(self.device)
         if why:
             return False, why
-        return True, f"ok ({steps} steps, {'fused == separate' if len(modes) == 2 else 'separate'})"
+        what = "fused == separate" if len(modes) == 2 else "separate"
+        how = f"graph replay of the {n}-step training chunk" if self.use_graphs else f"{n} eager steps"
+        return True, f"ok ({how}, {what})"
+
+    def reset_model(self, module) -> None:
+        """Start over from ``module``'s parameters with fresh optimizer state (zero Adadelta
+        accumulators, dropout stream from the start) on this already-built trainer: engine, graphs,
+        communicators, probe and validation are reused (bench.py's in-process 20-epoch run)."""
+        self.synchronize()
+        ms = self.ms
+        with torch.no_grad():
+            ms.square_avg.zero_()
+            ms.acc_delta.zero_()
+            ms.grad.zero_()
+            self.loss_log.zero_()
+        ms.bind(module)                      # copies the parameters into the flat buffer + shadows
+        torch.cuda.synchronize(self.device)
+        self.rng_base = 0
 
     def check_errors(self) -> None:
         """Raise if a device-side hand-off or xGMI stage wait timed out (the per-epoch check; a 4-byte
@@ -300,7 +361,8 @@ class FusedTrainer:
         key = (n, batch)
         gid = self._graphs.get(key)
         if gid is None:
-            gid = self.engine.capture_train(n, batch, self.B)
+            with self.setup.phase("graph_capture"):
+                gid = self.engine.capture_train(n, batch, self.B)
             self._graphs[key] = gid
         return gid
 
@@ -422,6 +484,28 @@ class FusedTrainer:
         if self.use_graphs:
             for k in set(self._chunks(n)):
                 self._graph(k, self.B)
+
+    def warm_graphs(self, n: int) -> None:
+        """Replay once every graph ``run_steps(n)`` will use, then restore the model, optimizer and
+        step state bit for bit: a later timed ``run_steps(n)`` then starts on executables that have
+        already run (code objects resident, packets uploaded) without counting extra steps.  Runs
+        on every rank (the replays include the DDP collectives).  The rows the replays read must be
+        gathered (``engine.gather_rows``) beforehand."""
+        if not self.use_graphs or n <= 0:
+            return
+        ms = self.ms
+        torch.cuda.synchronize(self.device)
+        snap = {k: getattr(ms, k).clone() for k in ("param", "square_avg", "acc_delta", "state")}
+        torch.cuda.synchronize(self.device)
+        for k in sorted(set(self._chunks(n))):
+            self.engine.replay(self._graph(k, self.B))
+        self.synchronize()
+        with torch.no_grad():
+            for k, v in snap.items():
+                getattr(ms, k).copy_(v)
+        torch.cuda.synchronize(self.device)
+        self.engine.refresh_shadows()
+        torch.cuda.synchronize(self.device)
 
     def run_steps(self, n: int) -> None:
         """Enqueue ``n`` full-batch steps continuing from the device step counter (no host sync)."""

@@ -7,8 +7,9 @@ initial weights.  ``forward`` dispatches on the input device:
 
 * CPU: the reference math with torch ops (the ``mnist.py --no-cuda`` configuration);
 * GPU: the fused MI355X kernels (``ops.fused_net``) - gather/normalise-free conv trunk on
-  MFMA, split-K fc1, fused head - with autograd support through ``FusedNetFunction``
-  (bf16 MFMA operands, fp32 accumulation / parameters).  ``compute_dtype = torch.float32``
+  MFMA, split-K fc1, fused head - with autograd support through ``TrunkFunction`` +
+  ``HeadFunction`` (the fc gradients - and their DDP hooks - are final before the conv backward
+  is enqueued; bf16 MFMA operands, fp32 accumulation / parameters).  ``compute_dtype = torch.float32``
   selects the stock-torch fp32 path on the GPU instead (the ``--dtype fp32`` parity mode).
 """
 from __future__ import annotations

@@ -91,10 +91,24 @@ def barrier() -> None:
         dist.barrier()
 
 
-def create_rccl_comms(world_size: int, rank: int, device: int, n: int = 2):
-    """``n`` independent framework communicators (the fused engine's DDP schedule 2 reduces the
-    conv bucket on the first and the fc bucket on the second, concurrently)."""
-    return [create_rccl_comm(world_size, rank, device, tag=str(i)) for i in range(n)]
+def rccl_comm_count() -> int:
+    """Framework RCCL communicators the fused engine creates: 1 (default - both gradient buckets on
+    one communicator, ordered fc -> conv on the device, like DDP's single process group) or 2
+    (``MNIST_AMD_RCCL_COMMS=2``, opt-in: the fc bucket on its own communicator may overlap the conv
+    bucket's all-reduce; concurrent collectives on two communicators are deadlock-prone in NCCL/RCCL
+    when ranks interleave them differently, which is why it is not the default)."""
+    n = int(os.environ.get("MNIST_AMD_RCCL_COMMS", "1"))
+    if n not in (1, 2):
+        raise ValueError(f"MNIST_AMD_RCCL_COMMS must be 1 or 2, got {n}")
+    return n
+
+
+def create_rccl_comms(world_size: int, rank: int, device: int, n: int | None = None):
+    """``(comm, comm2)``: the engine's RCCL communicator and, when ``n`` (default
+    :func:`rccl_comm_count`) is 2, a second one for the fc bucket (else ``None``)."""
+    n = rccl_comm_count() if n is None else n
+    comms = [create_rccl_comm(world_size, rank, device, tag=str(i)) for i in range(n)]
+    return comms[0], (comms[1] if n > 1 else None)
 
 
 

@@ -45,3 +45,33 @@ class Timer:
             torch.cuda.synchronize()
         self.elapsed = time.perf_counter() - self.t0
         return False
+
+
+class PhaseTimes:
+    """Host wall-clock seconds per named setup phase (accumulated; insertion ordered), e.g. the
+    startup work that lands inside the reference's ``Total cost time`` (mnist_ddp.py:200-203):
+    process group, communicators, xGMI map + self-test, all-reduce probe, validation, capture."""
+
+    def __init__(self):
+        self.s: dict[str, float] = {}
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.add(name, time.perf_counter() - t0)
+
+    def add(self, name: str, seconds: float) -> None:
+        self.s[name] = self.s.get(name, 0.0) + seconds
+
+    def update(self, other: "PhaseTimes | dict", prefix: str = "") -> None:
+        for k, v in (other.s if isinstance(other, PhaseTimes) else other).items():
+            self.add(prefix + k, v)
+
+    def rounded(self, nd: int = 4) -> dict[str, float]:
+        return {k: round(v, nd) for k, v in self.s.items()}
+
+    def total(self) -> float:
+        return sum(self.s.values())

@@ -25,38 +25,39 @@ def _env(**kw):
     return dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_ONE_GPU="1", GPU_MAX_HW_QUEUES="2", **kw)
 
 
-@pytest.mark.timeout(240)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_ddp_matches_world1_large_batch(cuda_device, world):
     # W*B stays below FC1_BIG_MIN_B (512) so the world-1 run on the W*B batch uses the same forward
     # kernels as the shards: the forward is then row-wise bitwise identical and only the gradient
     # reductions differ in order (at W*B >= 512 fc1 switches to its 4-way split-K form, whose
     # different rounding of every row's z1 flips bf16 ties in h / dz1 - a legitimate but larger
     # difference than the summation-order noise floor samples)
-    B = 200 if world * 200 < 512 else 100
+    B = {2: 200, 4: 100, 8: 60}[world]
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "ddp_equivalence.py"), "--world", str(world),
-           "--same-device", "--steps", "10", "--batch", str(B), "--timeout", "200"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, env=_env())
+           "--same-device", "--steps", "10", "--batch", str(B), "--timeout", "260"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=_env())
     print(r.stdout[-2000:])
     assert r.returncode == 0 and "DDP_EQUIVALENCE PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
 
 
-@pytest.mark.timeout(240)
-def test_mnist_ddp_world2_xgmi_without_rccl(cuda_device, tmp_path):
-    n_train, B, W = 8000, 200, 2
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W", [2, 8])
+def test_mnist_ddp_xgmi_without_rccl(cuda_device, tmp_path, W):
+    n_train, B = 8000, 200 if W == 2 else 100
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
            "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
            "--batch-size", str(B), "--epochs", "2", "--synthetic", "--synthetic-train-size", str(n_train),
            "--synthetic-test-size", "1000", "--dist-backend", "gloo", "--allreduce", "xgmi", "--check-sync",
-           "--save-model"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, cwd=tmp_path, env=_env())
+           "--save-model", "--json-log", str(tmp_path / "log.jsonl")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=tmp_path, env=_env())
     out = r.stdout
     assert r.returncode == 0, (out[-3000:], r.stderr[-3000:])
     # every rank prints its init line and the timer; only rank 0 prints train / test lines
     assert len(re.findall(r"\| distributed init \(rank \d\): env://", out)) == W
     assert len(re.findall(r"Total cost time:[0-9.]+ ms", out)) == W
     train = re.findall(r"Train Epoch: (\d+) \[(\d+)/(\d+) \((\d+)%\)\]\tLoss: ([0-9.]+)", out)
-    steps = n_train // W // B                                   # 20 per rank per epoch
+    steps = n_train // W // B                                   # 20 (W=2) / 10 (W=8) per rank per epoch
     assert len(train) == 2 * len(range(0, steps, 10))           # rank 0 only, every 10 batches
     assert [int(t[1]) for t in train[:2]] == [0, W * 10 * B]    # world * batch_idx * len(data)
     assert all(int(t[2]) == n_train for t in train)
@@ -66,22 +67,53 @@ def test_mnist_ddp_world2_xgmi_without_rccl(cuda_device, tmp_path):
     assert sorted(sd) == sorted("module." + k for k in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
                                                         "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"))
     assert all(v.dtype == torch.float32 for v in sd.values())
+    # the startup inside the reference timer, per phase and per rank (--json-log "setup_s")
+    import json
+    recs = [json.loads(ln) for ln in open(tmp_path / "log.jsonl")]
+    setups = [x for x in recs if "setup_s" in x]
+    assert len(setups) == W and all(x["allreduce"] == "xgmi" for x in setups)
+    for x in setups:
+        assert {"pg_init", "data", "ddp_wrap", "trainer.xgmi_comm", "trainer.validation"} <= set(x["setup_s"])
+        assert "rccl_comms" not in x["setup_s"]                 # --allreduce xgmi: no RCCL communicator
 
 
-@pytest.mark.timeout(240)
-def test_bench_world2_reports_correctness(cuda_device, tmp_path):
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W", [2, 8])
+def test_bench_reports_correctness(cuda_device, tmp_path, W):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
-           "--nnodes", "1", "--nproc-per-node", "2", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "20", "--warmup", "5", "--epochs", "2", "--dist-backend", "gloo",
+           "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(W), "--steps", "20", "--warmup", "5", "--epochs", "2", "--dist-backend", "gloo",
            "--allreduce", "xgmi"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=220, cwd=tmp_path, env=_env())
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=tmp_path, env=_env())
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     j = json.loads(lines[0])
-    assert j["n_gpus"] == 2 and j["params_in_sync"] is True
+    assert j["n_gpus"] == W and j["params_in_sync"] is True and j["desync_epoch"] is None
     assert j["config"]["allreduce"] == "xgmi" and j["config"]["rccl_world"] is None
-    assert j["config"]["xgmi_validation"].startswith("ok")
+    assert j["config"]["rccl_comms"] == 0 and j["config"]["xgmi_ordering"].startswith("uncached")
+    assert j["config"]["xgmi_validation"].startswith("ok (graph replay")
+    assert "trainer.validation" in j["setup_phases_s"] and "warm_replay" in j["setup_phases_s"]
     rs = j["reference_script"]
-    assert rs["rc"] == 0 and rs["ranks_reporting"] == 2, rs
-    assert j["total_cost_time_s"] > 0
+    assert rs["rc"] == 0 and rs["ranks_reporting"] == W, rs
+    assert j["total_cost_time_s"] > 0 and rs["setup_phases_s"]["pg_init"] >= 0
+
+
+@pytest.mark.timeout(200)
+def test_validation_fault_in_replayed_graph_is_named(cuda_device, tmp_path):
+    """A rank held back while the startup validation REPLAYS the captured training graph: its peers'
+    stage waits time out inside the graph, the collective verdict names the ranks, and with no RCCL
+    communicator to fall back to (gloo + --allreduce xgmi) the run stops with that error instead of
+    training on a poisoned communicator."""
+    W = 4
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
+           "--batch-size", "100", "--epochs", "1", "--synthetic", "--synthetic-train-size", "4000",
+           "--synthetic-test-size", "1000", "--dist-backend", "gloo", "--allreduce", "xgmi"]
+    env = _env(MNIST_AMD_FAULT="validate_delay:2:6", MNIST_AMD_STARTUP_TIMEOUT="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=tmp_path, env=env)
+    err = r.stdout + r.stderr
+    assert r.returncode != 0, err[-3000:]
+    assert "failed its startup validation" in err, err[-3000:]
+    assert "timed out" in err and "rank " in err, err[-3000:]
+    assert "Train Epoch" not in r.stdout                         # nothing trained on the bad comm

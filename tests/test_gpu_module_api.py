@@ -138,7 +138,8 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         res = []
         # schedule 1 (one comm), schedule 2 (cross-step fc branch, two comms), eager schedule 2,
         # schedule 3 with RCCL and with the xGMI all-reduce (world 1: its output buffer path), no comm
-        for c, c2, gs, sched, ar in ((comm, None, 4, 1, "rccl"), (comm, comm2, 4, 2, "rccl"),
+        for c, c2, gs, sched, ar in ((comm, None, 4, 1, "rccl"), (comm, None, 4, 3, "rccl"),
+                                     (comm, None, 0, 3, "rccl"), (comm, comm2, 4, 2, "rccl"),
                                      (comm, comm2, 0, 2, "rccl"), (comm, comm2, 4, 3, "rccl"),
                                      (comm, comm2, 0, 3, "rccl"), (comm, comm2, 4, 3, "xgmi"),
                                      (comm, comm2, 0, 3, "xgmi"), (None, None, 4, 1, "rccl")):
@@ -155,6 +156,37 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         assert all(d == 0 for d in diffs), diffs
     finally:
         dist.destroy_process_group()
+
+
+def test_fc_bucket_hooks_fire_before_conv_backward(cuda_device, monkeypatch):
+    """Module path: autograd finalises the fc gradients (DDP bucket 0) and runs their hooks before
+    conv_bwd is enqueued, so DDP's bucket-0 all-reduce overlaps the conv backward as in torch DDP
+    (reference mnist_ddp.py:72); the conv gradients' hooks fire after it."""
+    from pytorch_mnist_ddp_amd.ops import native
+    C = native.load()
+    events = []
+
+    class Spy:
+        def __getattr__(self, name):
+            fn = getattr(C, name)
+            if name in ("conv_bwd", "fc_bwd"):
+                def wrapped(*a, **k):
+                    events.append(name)
+                    return fn(*a, **k)
+                return wrapped
+            return fn
+    monkeypatch.setattr(native, "load", lambda *a, **k: Spy())
+    torch.manual_seed(3)
+    net = Net().to(cuda_device)
+    for n, p_ in net.named_parameters():
+        p_.register_post_accumulate_grad_hook(lambda _p, n=n: events.append(n))
+    x, y = _data(64, cuda_device, seed=4)
+    F.nll_loss(net(x), y).backward()
+    torch.cuda.synchronize()
+    i = events.index("conv_bwd")
+    assert events.index("fc_bwd") < i
+    assert set(events[:i]) >= {"fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"}
+    assert set(events[i + 1:]) == {"conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"}
 
 
 def test_scripts_on_gpu(tmp_path):

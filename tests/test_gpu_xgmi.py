@@ -11,16 +11,18 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.timeout(200)
-@pytest.mark.parametrize("world,engine_steps,fault", [(2, 30, False), (4, 30, False), (4, 0, True)])
+@pytest.mark.timeout(260)
+@pytest.mark.parametrize("world,engine_steps,fault", [(2, 30, False), (3, 20, False), (4, 30, False), (8, 30, False),
+                                                       (4, 0, True)])
 def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps, fault):
-    """world 4 with engine steps runs the FUSED schedule (the production default) with 4 ranks'
-    spinning grids on one GPU: the residency planner must shrink them so all are resident."""
+    """With engine steps the FUSED schedule (the production default) runs with W ranks' spinning
+    grids on one GPU: the residency planner must shrink them so all are resident.  W = 3 and 8
+    execute those template instantiations of every xGMI kernel (8 = the headline config)."""
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "xgmi_check.py"), "--world", str(world),
-           "--same-device", "--iters", "20", "--engine-steps", str(engine_steps), "--timeout", "170"]
+           "--same-device", "--iters", "20", "--engine-steps", str(engine_steps), "--timeout", "230"]
     if fault:
         cmd.append("--fault-test")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=185, env=dict(os.environ, PYTHONPATH=ROOT))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=245, env=dict(os.environ, PYTHONPATH=ROOT))
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
 
@@ -34,7 +36,7 @@ def test_allreduce_auto_choice_plumbing_world1(cuda_device):
     from pytorch_mnist_ddp_amd.parallel.distributed import choose_allreduce, create_rccl_comms, create_xgmi_comm
     init_world1_pg("nccl", cuda_device)
     try:
-        c0, c1 = create_rccl_comms(1, 0, 0)
+        c0, c1 = create_rccl_comms(1, 0, 0, n=2)
         n, split = 1200000, 1181120
         g = torch.randn(n, device=cuda_device)
         x = create_xgmi_comm(1, 0, cuda_device, n)
@@ -80,3 +82,41 @@ def test_conv_bucket_split_bitwise_at_two_ranks(cuda_device):
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
     assert "conv split True" in r.stdout
+
+
+def test_rccl_single_communicator_schedule_world1(tmp_path):
+    """DDP schedule 3 on ONE RCCL communicator (the default: fc all-reduce on the comm stream, the
+    conv all-reduce on the compute stream ordered after it by a device counter) trains bitwise like
+    the opt-in two-communicator schedule and like the plain single-GPU step (world 1, --force-comm)."""
+    import json
+    outs = {}
+    runs = (("one", ["--force-comm"], {}), ("two", ["--force-comm"], {"MNIST_AMD_RCCL_COMMS": "2"}),
+            ("plain", [], {}))
+    for name, extra, env in runs:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--standalone",
+               "--local-addr", "127.0.0.1", os.path.join(ROOT, "bench.py"), "--allreduce", "rccl",
+               "--no-full-run", "--steps", "60", "--warmup", "10", *extra]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
+                           env=dict(os.environ, PYTHONPATH=ROOT, **env))
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        outs[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert outs["one"]["config"]["rccl_comms"] == 1 and outs["two"]["config"]["rccl_comms"] == 2
+    assert outs["plain"]["config"]["rccl_comms"] == 0
+    assert outs["one"]["last_train_loss"] == outs["two"]["last_train_loss"] == outs["plain"]["last_train_loss"]
+
+
+def test_world_gt1_without_transport_refuses(cuda_device, monkeypatch):
+    """world > 1 with neither an RCCL communicator nor a working xGMI one must raise instead of
+    training every rank alone on a gradient 1/world too small."""
+    import torch
+    import pytorch_mnist_ddp_amd.parallel.distributed as D
+    from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+    from pytorch_mnist_ddp_amd.engine.state import ModelState
+    from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+    from pytorch_mnist_ddp_amd.models.net import Net
+    monkeypatch.setattr(D, "create_xgmi_comm", lambda *a, **k: None)
+    torch.manual_seed(1)
+    ms = ModelState(Net(), cuda_device)
+    train = load_mnist(train=True, synthetic_data=True, synthetic_size=512, verbose=False)
+    with pytest.raises(RuntimeError, match="no RCCL communicator"):
+        FusedTrainer(ms, train, None, 64, 128, num_samples=512, world_size=2, rank=0, allreduce="xgmi")
