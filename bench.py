@@ -268,7 +268,7 @@ def main() -> int:
         # state restored bit for bit): the first timed replay pays no first-launch cost, and exactly
         # --steps steps are timed after exactly --warmup warmup steps
         with phases.phase("warm_replay"):
-            first = max(tr._chunks(args.steps)) if tr.use_graphs else 0
+            first = sum(set(tr._chunks(args.steps))) if tr.use_graphs else 0   # rows the replays read
             tr.engine.gather_rows(0, min(total, max(first, args.warmup)) * B)
             tr.warm_graphs(args.steps)
     if comm is not None:   # RCCL lazily sets up its channels on the first collective: do it untimed
@@ -282,6 +282,7 @@ def main() -> int:
     t0 = time.perf_counter()
     tr.engine.gather_rows(args.warmup * B, args.steps * B)   # the device DataLoader work is timed too
     tr.run_steps(args.steps)
+    t_enq = time.perf_counter()                              # host: every timed chunk enqueued
     tr.synchronize()
     torch.cuda.synchronize()
     if use_pg:
@@ -419,6 +420,7 @@ def main() -> int:
             "final_test_acc": round(acc, 4) if acc is not None else None,
             "last_train_loss": round(final_loss, 4),
             "setup_s": round(t0 - t_setup, 2),
+            "timed_enqueue_ms": round(1000.0 * (t_enq - t0), 3),
             "setup_phases_s": phases.rounded(3),
         }
         print(json.dumps(out), flush=True)

@@ -217,6 +217,35 @@ void Engine::enqueue_step(int batch, bool last) {
   if (cb.c1_rows > C1_PRE_MIN_SLABS && c1_prereduce_) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
+  if (local3 && par_wgrad_ && !dgrad_update_) {
+    // single GPU, conv backward on two queues: conv2_dgrad on the compute stream (its start counts
+    // sync_[0]), conv2_wgrad on the comm stream released by that count - the two share every CU
+    // (LDS 70 + 89 KB <= 160 KB) instead of running back to back - then the fc Adadelta step there
+    // ([1] = fc update done, which the next trunk_fwd's completion waits for).  The conv reduce +
+    // update waits on the compute stream for wgrad's slabs ([5] = wgrad done count).
+    ConvBwdArgs cbd = cb;
+    cbd.signal_ctr = sync_ + 0;
+    phase_begin("bwd_conv_dgrad||wgrad");
+    launch_conv_dgrad(cbd, B, compute_);
+    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    launch_conv_wgrad(cb, B, comm_stream_);
+    launch_stream_signal(sync_ + 5, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+    launch_stream_signal(sync_ + 1, comm_stream_);
+    side_pending_ = true;
+    phase_end();
+    phase_begin("grad_reduce+update");
+    launch_stream_wait(sync_ + 5, sync_ + 0, 0, sync_ + 2, compute_);
+    launch_adadelta_reduce(adc, cb, B, true, compute_);
+    phase_end();
+    if (last) {                                              // chunk end: one real join edge
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      side_pending_ = false;
+      side_forked_ = false;
+    }
+    return;
+  }
   if (sched3) {
     // xGMI: the reduced gradients land in the communicator's output buffer, the update reads there
     if (xgmi_) ad.grad = adc.grad = xgmi_->out();
@@ -234,7 +263,7 @@ void Engine::enqueue_step(int batch, bool last) {
         xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
       } else if (comm2_) {             // opt-in second communicator: may overlap comm_'s conv all-reduce
         comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-      } else {
+      } else if (comm_) {
         // one communicator for both buckets (DDP's single process group): the fc all-reduce runs here
         // and publishes its completion in sync_[12]; the compute stream's conv all-reduce waits for
         // it, so the communicator never has two collectives in flight and every rank issues them in
@@ -458,9 +487,8 @@ int Engine::capture_train(int n, int batch, int stride) {
   HIP_OK(hipStreamEndCapture(compute_, &g));
   hipGraphExec_t ex = nullptr;
   HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-  // upload the executable's packets / kernel arguments now (ordered on the compute stream), so the
-  // first replay - e.g. the first timed chunk of a bench - does not pay the upload inside its window
-  HIP_OK(hipGraphUpload(ex, compute_));
+  // (no hipGraphUpload: on this ROCm 7 runtime it segfaults right after instantiate - measured on
+  // the box; first-replay costs are taken by an untimed warm replay instead, FusedTrainer.warm_graphs)
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   return (int)graphs_.size() - 1;
@@ -508,9 +536,8 @@ int Engine::capture_eval(int n_total, int batch) {
   HIP_OK(hipStreamEndCapture(compute_, &g));
   hipGraphExec_t ex = nullptr;
   HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-  // upload the executable's packets / kernel arguments now (ordered on the compute stream), so the
-  // first replay - e.g. the first timed chunk of a bench - does not pay the upload inside its window
-  HIP_OK(hipGraphUpload(ex, compute_));
+  // (no hipGraphUpload: on this ROCm 7 runtime it segfaults right after instantiate - measured on
+  // the box; first-replay costs are taken by an untimed warm replay instead, FusedTrainer.warm_graphs)
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   return (int)graphs_.size() - 1;

@@ -108,6 +108,9 @@ class Engine {
   // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
   // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
   void set_dgrad_update(bool on) { dgrad_update_ = on; }
+  // single-GPU overlap schedule: conv2_wgrad on the comm stream concurrently with conv2_dgrad
+  // (device-counter hand-offs; both kernels fit one CU together)
+  void set_par_wgrad(bool on) { par_wgrad_ = on; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -161,10 +164,12 @@ class Engine {
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error,
-                                    // [3]/[4] conv split, [8..11] probes, [12] fc all-reduce done (1 comm)
+                                    // [3]/[4] conv split, [5] wgrad done (par_wgrad), [8..11] probes,
+                                    // [12] fc all-reduce done (1 comm)
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
   bool dgrad_update_ = true;
+  bool par_wgrad_ = false;
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
   hipEvent_t ev_c2_ = nullptr;

@@ -111,6 +111,7 @@ class FusedTrainer:
         # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)
         self.profile_left = 0
         self.use_graphs = self.graph_steps > 0
+        self.ramp = int(os.environ.get("MNIST_AMD_GRAPH_RAMP", "0"))   # see _chunks
         if concurrent is None:
             concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
         self.engine.set_concurrent(bool(concurrent))
@@ -129,6 +130,9 @@ class FusedTrainer:
         # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
         # (opt-in MNIST_AMD_DGRAD_UPDATE=1, bitwise equal; measured 81.6-82.2 vs 80.9-81.8 us/step)
         self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "0") == "1")
+        # single-GPU overlap schedule: conv2_wgrad on the comm stream concurrently with conv2_dgrad
+        # (MNIST_AMD_PAR_WGRAD=1; device-counter hand-offs, bitwise equal)
+        self.engine.set_par_wgrad(os.environ.get("MNIST_AMD_PAR_WGRAD", "0") == "1")
         # DDP schedule: 3 (the fc bucket all-reduced + updated on the comm stream, overlapping the conv
         # backward and the step boundary, device-counter stream hand-offs; with one communicator the
         # conv all-reduce waits for the fc one on a counter) whenever a communicator is attached
@@ -473,10 +477,18 @@ class FusedTrainer:
         self.rng_base += 2 * (idx.numel() // self.B)
 
     def _chunks(self, n: int) -> list[int]:
+        """Graph sizes ``run_steps(n)`` replays: ``graph_steps`` each, the last one shorter; with a
+        launch ramp (``self.ramp`` = r > 0) the first graphs are r, 2r, 4r, .. steps, so after a host
+        sync the GPU starts on a small graph while the host is still submitting the larger ones (a
+        graph's host-side launch grows with its node count, ~2.4 us per node on ROCm 7)."""
         c = self.graph_steps if self.graph_steps > 0 else max(1, n)
-        out = [c] * (n // c)
-        if n % c:
-            out.append(n % c)
+        k = min(self.ramp, c) if self.ramp > 0 else c
+        out = []
+        while n > 0:
+            take = min(k, n)
+            out.append(take)
+            n -= take
+            k = min(2 * k, c)
         return out
 
     def precapture(self, n: int) -> None:

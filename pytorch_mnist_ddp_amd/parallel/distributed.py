@@ -293,6 +293,11 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
         ok = False
     finally:
         x.set_timeout_seconds(60.0)
+        # the last call's peers may still be READING this rank's output shard (all-gather phase): the
+        # host-side zeroing below is outside the kernels' hand-off protocol, so every rank first waits
+        # until all ranks have finished their last call (seen at W = 8 on one GPU: a fast rank zeroed
+        # its output under a slow rank's phase-2 reads -> whole shards of zeros)
+        barrier()
         with torch.no_grad():
             grad_in.zero_()
             grad_out.zero_()
