@@ -147,7 +147,9 @@ void Engine::enqueue_step(int batch, bool last) {
   // so every row's bf16 gradient operands (dz1, dl) are bitwise those of the world-1 run on the
   // world*B batch (scaling by 1/B and then by 1/world rounds the fp32 constant differently and flips
   // bf16 ties: a systematic ~7e-6 gradient offset, tools/ddp_equivalence.py)
-  const float gscale = 1.0f;
+  const float gscale = kDdpEpilogueScale;
+  // two-pass capture (capture_train): M = enqueue the compute-stream work, S = the side streams'
+  const bool M = enq_main_, S = enq_side_;
 
   // pre-gathered epoch rows when available (one load level less on every step's critical path)
   const bool pre = buf_.epoch_u8 != nullptr;
@@ -178,18 +180,18 @@ void Engine::enqueue_step(int batch, bool last) {
     tf.wait_err = sync_ + 2;
   }
   phase_begin("fwd");
-  launch_trunk_fwd(tf, B, true, compute_);
+  if (M) launch_trunk_fwd(tf, B, true, compute_);
   if (side_pending_) {
     if (!hold) HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
     side_pending_ = false;
   }
-  launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
+  if (M) launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
   ha.labels = labels; ha.idx = idxp; ha.idx_step_stride = stride;
-  ha.state = buf_.state; ha.inv_batch = 1.0f / (float)(B * world_);
+  ha.state = buf_.state; ha.inv_batch = ddp_head_inv_batch(B, world_);
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
-  launch_head_train(ha, B, Bp, compute_);
+  if (M) launch_head_train(ha, B, Bp, compute_);
   phase_end();
   const bool dist = comm_ != nullptr || xgmi_ != nullptr;   // world_size 1 + comm: DDP schedule (tests)
   // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t
@@ -205,7 +207,7 @@ void Engine::enqueue_step(int batch, bool last) {
     w1t_in_alt_ = !w1t_in_alt_;
   }
   phase_begin("bwd_fc");
-  launch_fc_bwd(fb, B, Bp, compute_);
+  if (M) launch_fc_bwd(fb, B, Bp, compute_);
   phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
@@ -217,46 +219,18 @@ void Engine::enqueue_step(int batch, bool last) {
   if (cb.c1_rows > C1_PRE_MIN_SLABS && c1_prereduce_) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
-  if (local3 && par_wgrad_ && !dgrad_update_) {
-    // single GPU, conv backward on two queues: conv2_dgrad on the compute stream (its start counts
-    // sync_[0]), conv2_wgrad on the comm stream released by that count - the two share every CU
-    // (LDS 70 + 89 KB <= 160 KB) instead of running back to back - then the fc Adadelta step there
-    // ([1] = fc update done, which the next trunk_fwd's completion waits for).  The conv reduce +
-    // update waits on the compute stream for wgrad's slabs ([5] = wgrad done count).
-    ConvBwdArgs cbd = cb;
-    cbd.signal_ctr = sync_ + 0;
-    phase_begin("bwd_conv_dgrad||wgrad");
-    launch_conv_dgrad(cbd, B, compute_);
-    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    launch_conv_wgrad(cb, B, comm_stream_);
-    launch_stream_signal(sync_ + 5, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
-    launch_stream_signal(sync_ + 1, comm_stream_);
-    side_pending_ = true;
-    phase_end();
-    phase_begin("grad_reduce+update");
-    launch_stream_wait(sync_ + 5, sync_ + 0, 0, sync_ + 2, compute_);
-    launch_adadelta_reduce(adc, cb, B, true, compute_);
-    phase_end();
-    if (last) {                                              // chunk end: one real join edge
-      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-      side_pending_ = false;
-      side_forked_ = false;
-    }
-    return;
-  }
   if (sched3) {
     // xGMI: the reduced gradients land in the communicator's output buffer, the update reads there
     if (xgmi_) ad.grad = adc.grad = xgmi_->out();
     ConvBwdArgs cbs = cb;
     cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
     phase_begin("bwd_conv_wgrad");
-    launch_conv_wgrad(cbs, B, compute_);
+    if (M) launch_conv_wgrad(cbs, B, compute_);
     phase_end();
     phase_begin("allreduce_fc+update");
-    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
+    if (S) launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    if (!S) {
+    } else if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
       if (xgmi_) {
@@ -273,7 +247,7 @@ void Engine::enqueue_step(int batch, bool last) {
       }
       launch_adadelta(ad, ADA_FC, comm_stream_);
     }
-    launch_stream_signal(sync_ + 1, comm_stream_);           // fc update of this step done
+    if (S) launch_stream_signal(sync_ + 1, comm_stream_);    // fc update of this step done
     phase_end();
     side_pending_ = true;
     if (split) {
@@ -288,16 +262,18 @@ void Engine::enqueue_step(int batch, bool last) {
       ad2.state_inc = nullptr;
       ad2.w2d = w2d_next;
       cb.w2d = w2d_cur;
-      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
-      XgmiConvPart p2;
-      p2.lo = 0;
-      p2.hi = RED_W2_PARTS;
-      xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, conv2_stream_, ad2, p2);
-      launch_stream_signal(sync_ + 3, conv2_stream_);
+      if (S) {
+        launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
+        XgmiConvPart p2;
+        p2.lo = 0;
+        p2.hi = RED_W2_PARTS;
+        xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, conv2_stream_, ad2, p2);
+        launch_stream_signal(sync_ + 3, conv2_stream_);
+      }
       ConvBwdArgs cbd = cb;
       cbd.signal_ctr = sync_ + 4;
       phase_begin("bwd_conv_dgrad");
-      launch_conv_dgrad(cbd, B, compute_);
+      if (M) launch_conv_dgrad(cbd, B, compute_);
       phase_end();
       phase_begin("allreduce_conv+update");
       XgmiConvPart p1;
@@ -306,15 +282,18 @@ void Engine::enqueue_step(int batch, bool last) {
       p1.wait_a = sync_ + 3;
       p1.wait_b = sync_ + 4;
       p1.wait_err = sync_ + 2;
-      xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
+      if (M) xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
       phase_end();
       w2d_in_alt_ = !w2d_in_alt_;
       if (last) {
-        HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
-        HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
+        if (M) {
+          HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
+          HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
+        }
         if (w2d_in_alt_) {
-          HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
-                                compute_));
+          if (M)
+            HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                                  compute_));
           w2d_in_alt_ = false;
         }
       }
@@ -327,23 +306,24 @@ void Engine::enqueue_step(int batch, bool last) {
       u.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
       cb.w2d = w2d_cur;
       phase_begin("bwd_conv_dgrad+conv2_update");
-      launch_conv_dgrad_update(cb, u, B, compute_);
+      if (M) launch_conv_dgrad_update(cb, u, B, compute_);
       phase_end();
       phase_begin("conv1_update");
-      launch_adadelta_reduce_parts(adc, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+      if (M) launch_adadelta_reduce_parts(adc, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
       phase_end();
       w2d_in_alt_ = !w2d_in_alt_;
       if (last && w2d_in_alt_) {
-        HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+        if (M) HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
                               compute_));
         w2d_in_alt_ = false;
       }
     } else {
     phase_begin("bwd_conv_dgrad");
-    launch_conv_dgrad(cb, B, compute_);
+    if (M) launch_conv_dgrad(cb, B, compute_);
     phase_end();
     phase_begin("allreduce_conv+update");
-    if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
+    if (!M) {
+    } else if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
       xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc);
     } else if (local3) {             // single GPU: conv slab reduce + conv Adadelta in one launch
       launch_adadelta_reduce(adc, cb, B, true, compute_);
@@ -363,8 +343,10 @@ void Engine::enqueue_step(int batch, bool last) {
     phase_end();
     }
     if (last) {                                              // chunk end: one real join edge
-      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      if (M) {
+        HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+        HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      }
       side_pending_ = false;
       side_forked_ = false;
     }
@@ -461,6 +443,12 @@ void Engine::enqueue_step(int batch, bool last) {
   }
 }
 
+bool Engine::uses_side_streams() const {
+  // the schedule-3 family (device-counter hand-offs to the comm / conv2 streams), as enqueue_step decides it
+  const bool local3 = !comm_ && !xgmi_ && overlap_fc_update_ && !concurrent_;
+  return ((comm_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3) || local3;
+}
+
 void Engine::train_steps(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
@@ -474,8 +462,29 @@ int Engine::capture_train(int n, int batch, int stride) {
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
   try {
-    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+    if (side_first_ && uses_side_streams()) {
+      // Two passes: every side-stream node of the chunk is created first, then the compute chain.
+      // The runtime submits a graph's parallel branches one after the other, so in one pass the side
+      // chain (which the NEXT step's trunk_fwd waits for on a device counter) reached its queue only
+      // after the whole compute chain had been submitted - a 20-step graph's first step then stalled
+      // ~0.45 ms (host launch time) on every replay that starts from an idle GPU.  Host state (the
+      // ping-pong shadows, the fork) is replayed identically in both passes.
+      const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
+      enq_main_ = false;
+      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+      side_pending_ = sp;
+      w1t_in_alt_ = w1;
+      w2d_in_alt_ = w2;
+      side_forked_ = true;                 // the fork (chunk start -> side streams) is captured
+      enq_main_ = true;
+      enq_side_ = false;
+      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+      enq_side_ = true;
+    } else {
+      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+    }
   } catch (...) {
+    enq_main_ = enq_side_ = true;
     side_pending_ = false;
     side_forked_ = false;
     w1t_in_alt_ = false;

@@ -108,9 +108,9 @@ class Engine {
   // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
   // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
   void set_dgrad_update(bool on) { dgrad_update_ = on; }
-  // single-GPU overlap schedule: conv2_wgrad on the comm stream concurrently with conv2_dgrad
-  // (device-counter hand-offs; both kernels fit one CU together)
-  void set_par_wgrad(bool on) { par_wgrad_ = on; }
+  // capture a chunk's side-stream nodes before its compute chain (default on; see capture_train)
+  void set_side_first(bool on) { side_first_ = on; }
+
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -145,6 +145,7 @@ class Engine {
 
  private:
   void enqueue_step(int batch, bool last);
+  bool uses_side_streams() const;
   void enqueue_eval(int n_total, int batch);
   void alloc_workspace();
 
@@ -164,12 +165,13 @@ class Engine {
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error,
-                                    // [3]/[4] conv split, [5] wgrad done (par_wgrad), [8..11] probes,
+                                    // [3]/[4] conv split, [8..11] probes,
                                     // [12] fc all-reduce done (1 comm)
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
   bool dgrad_update_ = true;
-  bool par_wgrad_ = false;
+  bool side_first_ = true;
+  bool enq_main_ = true, enq_side_ = true;   // two-pass capture: which streams enqueue_step feeds
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
   hipEvent_t ev_c2_ = nullptr;

@@ -3,7 +3,8 @@
 // tools/sanitize_host.sh):
 //   * the engine's workspace carve (offsets of every activation buffer for a batch capacity);
 //   * the xGMI IPC export record: encode / decode / validation against this communicator;
-//   * the residency planner's grid fitting.
+//   * the residency planner's grid fitting;
+//   * the DDP gradient scaling constants the engine hands its kernels.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -15,6 +16,18 @@
 #include "../include/kernels.h"
 
 namespace mnist {
+
+// ---------------------------------------------------------------------------- DDP gradient scaling
+// The engine folds DDP's 1/world averaging into the head's loss-gradient scale: every rank's head
+// scales by 1/(B * world) and the all-reduce SUMS, so each row's bf16 gradient operands are bitwise
+// those of the world-1 run on the world*B batch.  The GEMM / slab-reduce epilogues then get 1.0
+// (FcBwdArgs::grad_scale, ConvBwdArgs::grad_scale) - a caller that also divided there would
+// average twice.
+inline float ddp_head_inv_batch(int batch, int world) {
+  if (batch < 1 || world < 1) throw std::runtime_error("ddp scale: bad batch / world");
+  return 1.0f / (float)(batch * world);
+}
+constexpr float kDdpEpilogueScale = 1.0f;
 
 // ---------------------------------------------------------------------------- engine workspace
 struct WorkspaceLayout {

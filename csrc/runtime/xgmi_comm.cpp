@@ -4,8 +4,12 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
+#include <vector>
 
 #include "../include/kernels.h"
 #include "host_logic.h"
@@ -15,6 +19,31 @@ namespace mnist {
 namespace {
 void ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi: ") + what + ": " + hipGetErrorString(e));
+}
+
+// Process-wide free list of exported buffers, keyed by (device, bytes, uncached).  Exported buffers
+// are never returned to the allocator (see the constructor), but a later communicator of the same
+// shape reuses them instead of allocating again, so the probe / validation / test communicators of
+// a long-lived process no longer grow device memory by ~9.6 MB each.  Reuse hands out the SAME
+// memory under the SAME IPC handle, so a peer's import cache maps the right pages; the 16-byte
+// signatures are rewritten by every new communicator, so a peer that kept a stale mapping of an
+// older communicator's buffer is still refused by connect().
+std::mutex g_pool_mu;
+std::map<std::tuple<int, size_t, bool>, std::vector<void*>> g_pool;
+
+void* pool_take(int device, size_t bytes, bool uncached) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto it = g_pool.find({device, bytes, uncached});
+  if (it == g_pool.end() || it->second.empty()) return nullptr;
+  void* p = it->second.back();
+  it->second.pop_back();
+  return p;
+}
+
+void pool_give(int device, size_t bytes, bool uncached, void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool[{device, bytes, uncached}].push_back(p);
 }
 
 void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
@@ -49,9 +78,14 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   // from the old one.
   const char* uc = getenv("MNIST_AMD_XGMI_UNCACHED");
   const bool uncached = uc ? atoi(uc) != 0 : kUncachedDefault;
-  auto alloc = [uncached](void** p, size_t bytes, const char* what) {
-    if (uncached) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
-    else ok(hipMalloc(p, bytes), what);
+  uncached_ = uncached;
+  auto alloc = [this, uncached, device](void** p, size_t bytes, const char* what) {
+    *p = pool_take(device, bytes, uncached);
+    if (!*p) {
+      if (uncached) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
+      else ok(hipMalloc(p, bytes), what);
+    }
+    owned_.push_back({*p, bytes});
   };
   // every exported buffer ends in a 16-byte signature {magic, rank, pid, buffer id} that peers read
   // back through their mappings after connect() (a mapping that does not show it is refused)
@@ -87,7 +121,9 @@ XgmiComm::~XgmiComm() {
   hipSetDevice(device_);
   hipDeviceSynchronize();
   for (void* p : opened_) hipIpcCloseMemHandle(p);
-  // in_, out_, flags_, stage_ were exported: deliberately not freed (see the constructor)
+  // in_, out_, flags_, stage_ were exported: never freed (see the constructor), but returned to
+  // the process-wide free list for the next communicator of the same shape
+  for (auto& b : owned_) pool_give(device_, b.second, uncached_, b.first);
   if (ctr_) hipFree(ctr_);
   if (err_) hipFree(err_);
 }

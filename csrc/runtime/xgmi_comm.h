@@ -75,6 +75,8 @@ class XgmiComm {
   int64_t numel_;
   int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
   float* stage_ = nullptr;   // [channels][2][oneshot_max_], IPC exported
+  std::vector<std::pair<void*, size_t>> owned_;   // the exported buffers (back to the free list)
+  bool uncached_ = true;
   int64_t oneshot_max_;
   int* ctr_ = nullptr;       // [channels][XGMI_MAX_WG], local
   int* err_ = nullptr;

@@ -123,6 +123,22 @@ static void test_records() {
   }
 }
 
+static void test_ddp_scale() {
+  // world W: head 1/(B*W), epilogues 1.0 - the W-rank SUM of per-rank gradients is the mean-NLL
+  // gradient of the W*B batch; the same constant as the world-1 run on W*B rows (bitwise)
+  CHECK(ddp_head_inv_batch(200, 8) == 1.0f / 1600.0f);
+  CHECK(ddp_head_inv_batch(1600, 1) == ddp_head_inv_batch(200, 8));
+  CHECK(ddp_head_inv_batch(200, 1) == 1.0f / 200.0f);
+  CHECK(kDdpEpilogueScale == 1.0f);
+  bool threw = false;
+  try {
+    ddp_head_inv_batch(0, 8);
+  } catch (const std::runtime_error&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
 static void test_fit() {
   int a = 145, b = 309;
   double l = fit_grid_pair(&a, 8, 1024, &b, 39, 1024, 1, 0.5);
@@ -146,6 +162,7 @@ int main() {
   test_workspace();
   test_records();
   test_fit();
+  test_ddp_scale();
   if (failures) {
     fprintf(stderr, "HOST_LOGIC_TEST FAILED (%d)\n", failures);
     return 1;

@@ -130,9 +130,9 @@ class FusedTrainer:
         # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
         # (opt-in MNIST_AMD_DGRAD_UPDATE=1, bitwise equal; measured 81.6-82.2 vs 80.9-81.8 us/step)
         self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "0") == "1")
-        # single-GPU overlap schedule: conv2_wgrad on the comm stream concurrently with conv2_dgrad
-        # (MNIST_AMD_PAR_WGRAD=1; device-counter hand-offs, bitwise equal)
-        self.engine.set_par_wgrad(os.environ.get("MNIST_AMD_PAR_WGRAD", "0") == "1")
+        # captured chunks: side-stream nodes first, then the compute chain (MNIST_AMD_SIDE_FIRST=0: one
+        # pass in step order; see Engine::capture_train)
+        self.engine.set_side_first(os.environ.get("MNIST_AMD_SIDE_FIRST", "1") == "1")
         # DDP schedule: 3 (the fc bucket all-reduced + updated on the comm stream, overlapping the conv
         # backward and the step boundary, device-counter stream hand-offs; with one communicator the
         # conv all-reduce waits for the fc one on a counter) whenever a communicator is attached
