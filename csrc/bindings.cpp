@@ -313,6 +313,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_conv_split", &Engine::set_conv_split)
       .def("set_dgrad_update", &Engine::set_dgrad_update)
       .def("set_side_first", &Engine::set_side_first)
+      .def("set_side_conv2", &Engine::set_side_conv2)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

@@ -175,6 +175,11 @@ struct AdadeltaArgs {
   uint16_t* w1;
   uint16_t* w1t;
   StepState* state_inc;       // if non-null, block 0 advances state->step (end-of-step marker)
+  // optional completion hold (adadelta_reduce_kernel): the launch completes only once
+  // *hold_a >= *hold_b (read when its last workgroup gets there); timeout -> *hold_err = 1
+  const int* hold_a;
+  const int* hold_b;
+  int* hold_err;
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
 void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);

@@ -135,6 +135,10 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
     bid -= 1;
   }
   conv_reduce_update(a, c, B, bid + bid0, red);
+  // single-GPU side-conv2 schedule: the step's last kernel completes only once the comm stream has
+  // published this step's conv2 update, so the next trunk_fwd (stream order) reads the new weights
+  if (a.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hold_err);
 }
 
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s) {

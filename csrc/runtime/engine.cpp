@@ -27,11 +27,23 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_w_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_c2_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   alloc_workspace();   // (the wgrad stream of the concurrent schedule is created on demand: every
                        // stream may take a hardware queue, and queues are a shared resource)
 }
 
 Engine::~Engine() {
+  if (side_thread_.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(side_mu_);
+      side_stop_ = true;
+    }
+    side_cv_.notify_all();
+    side_thread_.join();
+  }
+  for (auto g : side_graphs_)
+    if (g) hipGraphExecDestroy(g);
   for (auto g : graphs_) hipGraphExecDestroy(g);
   for (auto g : graph_defs_) hipGraphDestroy(g);
   if (ev_fc_) hipEventDestroy(ev_fc_);
@@ -39,6 +51,8 @@ Engine::~Engine() {
   if (ev_done_) hipEventDestroy(ev_done_);
   if (ev_w_) hipEventDestroy(ev_w_);
   if (ev_c2_) hipEventDestroy(ev_c2_);
+  if (ev_fork_) hipEventDestroy(ev_fork_);
+  if (ev_join_) hipEventDestroy(ev_join_);
   if (wgrad_stream_) hipStreamDestroy(wgrad_stream_);
   if (ws_) hipFree(ws_);
 }
@@ -297,6 +311,42 @@ void Engine::enqueue_step(int batch, bool last) {
           w2d_in_alt_ = false;
         }
       }
+    } else if (local3 && side_conv2_) {
+      // single GPU: conv2's slab reduce + update on the comm stream (after the fc update), released by
+      // dgrad's start (= wgrad done, counter [4]) and running under conv2_dgrad, which reads this
+      // step's w2d while the update writes the other copy (ping-pong, as the split path); counter [3]
+      // = conv2 updates published.  Only conv1's 20 reduce workgroups stay on the compute stream, and
+      // that launch holds its completion until [3] catches up, so the next trunk_fwd reads the new
+      // conv2 weights.
+      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
+      AdadeltaArgs u2 = adc;
+      u2.state_inc = nullptr;
+      u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
+      cb.w2d = w2d_cur;
+      if (S) {
+        launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+        launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
+        launch_stream_signal(sync_ + 3, comm_stream_);
+      }
+      ConvBwdArgs cbd = cb;
+      cbd.signal_ctr = sync_ + 4;
+      phase_begin("bwd_conv_dgrad");
+      if (M) launch_conv_dgrad(cbd, B, compute_);
+      phase_end();
+      phase_begin("conv1_update");
+      AdadeltaArgs u1 = adc;
+      u1.hold_a = sync_ + 3;
+      u1.hold_b = sync_ + 4;
+      u1.hold_err = sync_ + 2;
+      if (M) launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+      phase_end();
+      w2d_in_alt_ = !w2d_in_alt_;
+      if (last && w2d_in_alt_) {
+        if (M)
+          HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                                compute_));
+        w2d_in_alt_ = false;
+      }
     } else if (local3 && dgrad_update_) {
       // single GPU: conv2's reduce + update inside the dgrad launch (it reads this step's w2d while
       // the update writes the other copy: ping-pong as in the split path), conv1's after it
@@ -343,7 +393,7 @@ void Engine::enqueue_step(int batch, bool last) {
     phase_end();
     }
     if (last) {                                              // chunk end: one real join edge
-      if (M) {
+      if (M && !skip_join_) {
         HIP_OK(hipEventRecord(ev_done_, comm_stream_));
         HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
       }
@@ -459,16 +509,19 @@ void Engine::train_steps(int n, int batch, int stride) {
 int Engine::capture_train(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
+  const bool conv_split_on = xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2;
+  // RCCL side chains stay in ONE graph: launched as a separate side graph, the RCCL schedule ran
+  // 340 us per world-1 step instead of 101 (measured on the box; the xGMI and single-GPU side chains
+  // gain from the split: 100 -> 86 / 95 -> 77 us over a 20-step window)
+  const bool rccl_side = comm_ && !xgmi_;
+  if (side_first_ && uses_side_streams() && !conv_split_on && !rccl_side) return capture_train_split(n, batch);
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
   try {
     if (side_first_ && uses_side_streams()) {
-      // Two passes: every side-stream node of the chunk is created first, then the compute chain.
-      // The runtime submits a graph's parallel branches one after the other, so in one pass the side
-      // chain (which the NEXT step's trunk_fwd waits for on a device counter) reached its queue only
-      // after the whole compute chain had been submitted - a 20-step graph's first step then stalled
-      // ~0.45 ms (host launch time) on every replay that starts from an idle GPU.  Host state (the
-      // ping-pong shadows, the fork) is replayed identically in both passes.
+      // one graph, two passes: the side-stream nodes are created first, then the compute chain (the
+      // runtime submits a multi-stream graph's branches one after the other, in creation order:
+      // 120 -> 101 us per step for the RCCL schedule over a 20-step window)
       const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
       enq_main_ = false;
       for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
@@ -484,11 +537,7 @@ int Engine::capture_train(int n, int batch, int stride) {
       for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
     }
   } catch (...) {
-    enq_main_ = enq_side_ = true;
-    side_pending_ = false;
-    side_forked_ = false;
-    w1t_in_alt_ = false;
-    w2d_in_alt_ = false;
+    reset_host_state();
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
     throw;
@@ -500,7 +549,91 @@ int Engine::capture_train(int n, int batch, int stride) {
   // the box; first-replay costs are taken by an untimed warm replay instead, FusedTrainer.warm_graphs)
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
+  side_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
+}
+
+void Engine::reset_host_state() {
+  enq_main_ = enq_side_ = true;
+  skip_join_ = false;
+  side_pending_ = false;
+  side_forked_ = false;
+  w1t_in_alt_ = false;
+  w2d_in_alt_ = false;
+}
+
+// Schedule-3 chunks as TWO graphs: the side chain (comm stream: per step a counter wait, the fc
+// all-reduce / Adadelta step, a counter signal) and the compute chain, captured in two passes over
+// the same steps (host state - ping-pong shadows, the pending hand-off - replayed identically) and
+// launched concurrently from two host threads (replay()).  One multi-stream graph submitted its
+// side branch only after the whole compute branch (~3.6 us of host time per node), so after every
+// host sync the second step's trunk_fwd sat ~0.45 ms (20-step chunk) on the device counter the
+// side chain had not yet reached the queue to signal: the driver's 20-step bench window read
+// 93-97 us/step against 73.5 steady state.  The fork (chunk start -> comm stream) and the join
+// (comm stream -> compute) become two events at replay.
+int Engine::capture_train_split(int n, int batch) {
+  const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
+  hipGraph_t gs = nullptr, gm = nullptr;
+  try {
+    side_forked_ = true;                   // the fork is an event at replay, not a captured edge
+    enq_main_ = false;
+    HIP_OK(hipStreamBeginCapture(comm_stream_, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+    HIP_OK(hipStreamEndCapture(comm_stream_, &gs));
+    side_pending_ = sp;
+    w1t_in_alt_ = w1;
+    w2d_in_alt_ = w2;
+    side_forked_ = true;
+    enq_main_ = true;
+    enq_side_ = false;
+    skip_join_ = true;                     // the join is an event at replay
+    HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
+    HIP_OK(hipStreamEndCapture(compute_, &gm));
+    enq_side_ = true;
+    skip_join_ = false;
+  } catch (...) {
+    reset_host_state();
+    hipGraph_t junk = nullptr;
+    hipStreamCaptureStatus st;
+    if (hipStreamIsCapturing(comm_stream_, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
+      hipStreamEndCapture(comm_stream_, &junk);
+    if (junk) hipGraphDestroy(junk);
+    junk = nullptr;
+    if (hipStreamIsCapturing(compute_, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
+      hipStreamEndCapture(compute_, &junk);
+    if (junk) hipGraphDestroy(junk);
+    if (gs) hipGraphDestroy(gs);
+    if (gm) hipGraphDestroy(gm);
+    throw;
+  }
+  hipGraphExec_t xs = nullptr, xm = nullptr;
+  HIP_OK(hipGraphInstantiate(&xs, gs, nullptr, nullptr, 0));
+  HIP_OK(hipGraphInstantiate(&xm, gm, nullptr, nullptr, 0));
+  graph_defs_.push_back(gs);
+  graph_defs_.push_back(gm);
+  graphs_.push_back(xm);
+  side_graphs_.push_back(xs);
+  return (int)graphs_.size() - 1;
+}
+
+// --- side-graph launcher thread: hipGraphLaunch(side, comm stream) + the join event, concurrently
+// with the compute graph's launch on the calling thread
+void Engine::side_worker() {
+  std::unique_lock<std::mutex> lk(side_mu_);
+  for (;;) {
+    side_cv_.wait(lk, [this] { return side_stop_ || side_job_ != nullptr; });
+    if (side_stop_) return;
+    hipGraphExec_t job = side_job_;
+    lk.unlock();
+    hipError_t e = hipGraphLaunch(job, comm_stream_);
+    if (e == hipSuccess) e = hipEventRecord(ev_join_, comm_stream_);
+    lk.lock();
+    side_err_ = e;
+    side_job_ = nullptr;
+    side_done_ = true;
+    side_cv_.notify_all();
+  }
 }
 
 void Engine::gather_rows(int64_t start, int64_t n) {
@@ -512,7 +645,30 @@ void Engine::gather_rows(int64_t start, int64_t n) {
 
 void Engine::replay(int id) {
   if (id < 0 || id >= (int)graphs_.size()) throw std::runtime_error("bad graph id");
-  HIP_OK(hipGraphLaunch(graphs_[id], compute_));
+  hipGraphExec_t side = side_graphs_[id];
+  if (!side) {
+    HIP_OK(hipGraphLaunch(graphs_[id], compute_));
+    return;
+  }
+  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chain ordered after earlier compute work
+  HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
+  {
+    std::lock_guard<std::mutex> lk(side_mu_);
+    if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
+    side_job_ = side;
+    side_done_ = false;
+  }
+  side_cv_.notify_all();
+  const hipError_t em = hipGraphLaunch(graphs_[id], compute_);
+  hipError_t es;
+  {
+    std::unique_lock<std::mutex> lk(side_mu_);
+    side_cv_.wait(lk, [this] { return side_done_; });
+    es = side_err_;
+  }
+  HIP_OK(em);
+  HIP_OK(es);
+  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain
 }
 
 void Engine::enqueue_eval(int n_total, int batch) {
@@ -549,6 +705,7 @@ int Engine::capture_eval(int n_total, int batch) {
   // the box; first-replay costs are taken by an untimed warm replay instead, FusedTrainer.warm_graphs)
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
+  side_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
 }
 

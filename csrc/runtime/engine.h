@@ -18,8 +18,11 @@
 #include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <condition_variable>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -108,8 +111,11 @@ class Engine {
   // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
   // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
   void set_dgrad_update(bool on) { dgrad_update_ = on; }
-  // capture a chunk's side-stream nodes before its compute chain (default on; see capture_train)
+  // schedule-3 chunks as two graphs (side chain + compute chain) launched concurrently from two host
+  // threads (default on; see capture_train_split).  Off: one multi-stream graph per chunk.
   void set_side_first(bool on) { side_first_ = on; }
+  // single-GPU overlap schedule: conv2's slab reduce + update on the comm stream under conv2_dgrad
+  void set_side_conv2(bool on) { side_conv2_ = on; }
 
 
   // --- training
@@ -146,6 +152,9 @@ class Engine {
  private:
   void enqueue_step(int batch, bool last);
   bool uses_side_streams() const;
+  int capture_train_split(int n, int batch);
+  void reset_host_state();
+  void side_worker();
   void enqueue_eval(int n_total, int batch);
   void alloc_workspace();
 
@@ -171,7 +180,17 @@ class Engine {
   bool overlap_fc_update_ = false;
   bool dgrad_update_ = true;
   bool side_first_ = true;
+  bool side_conv2_ = false;
   bool enq_main_ = true, enq_side_ = true;   // two-pass capture: which streams enqueue_step feeds
+  bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
+  std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  std::thread side_thread_;                   // launches side graphs concurrently with the compute graph
+  std::mutex side_mu_;
+  std::condition_variable side_cv_;
+  hipGraphExec_t side_job_ = nullptr;
+  bool side_done_ = false, side_stop_ = false;
+  hipError_t side_err_ = hipSuccess;
   bool conv_split_ = false;
   hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
   hipEvent_t ev_c2_ = nullptr;
