@@ -283,11 +283,12 @@ def main() -> int:
     tr.engine.gather_rows(args.warmup * B, args.steps * B)   # the device DataLoader work is timed too
     tr.run_steps(args.steps)
     t_enq = time.perf_counter()                              # host: every timed chunk enqueued
-    tr.synchronize()
+    tr.engine.sync_streams()
     torch.cuda.synchronize()
     if use_pg:
         dist.barrier()
     t1 = time.perf_counter()
+    tr.check_errors()          # device hand-off / xGMI error flags of the timed steps (after the clock)
     elapsed = t1 - t0
     elapsed = _max_over_ranks(elapsed, dev)
     final_loss = float(tr.loss_log[(total - 1) % tr.loss_log.numel()].item()) if tr.loss_log.numel() else float("nan")

@@ -325,6 +325,7 @@ PYBIND11_MODULE(_C, m) {
       .def("refresh_shadows", &Engine::refresh_shadows)
       .def("broadcast_params", &Engine::broadcast_params)
       .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("sync_streams", &Engine::sync_streams, py::call_guard<py::gil_scoped_release>())
       .def("errors", &Engine::errors)
       .def("check_errors", &Engine::check_errors)
       .def_static("describe_xgmi_error", &Engine::describe_xgmi_error)

@@ -767,11 +767,15 @@ void Engine::check_errors() const {
                              describe_xgmi_error(e.second));
 }
 
-void Engine::synchronize() {
+void Engine::sync_streams() {
   HIP_OK(hipStreamSynchronize(compute_));
   if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
   if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
   if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
+}
+
+void Engine::synchronize() {
+  sync_streams();
   check_errors();
 }
 

@@ -139,6 +139,7 @@ class Engine {
   void refresh_shadows();
   void broadcast_params(int root);                   // DDP construction: rank-0 params to all
   void synchronize();                                // all streams, then check_errors()
+  void sync_streams();                               // all streams, no error-flag read-back
   // device error flags: (schedule-3 hand-off timeout, xGMI error code); a 4-byte D2H each, call
   // after the work of interest has completed (e.g. once per epoch)
   std::pair<int, int> errors() const;
