@@ -300,7 +300,7 @@ void Engine::enqueue_step(int batch, bool last) {
       phase_end();
       w2d_in_alt_ = !w2d_in_alt_;
       if (last) {
-        if (M) {
+        if (M && !skip_join_) {            // (split capture: the replay's join event covers it)
           HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
           HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
         }
@@ -509,7 +509,9 @@ void Engine::train_steps(int n, int batch, int stride) {
 int Engine::capture_train(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
-  const bool conv_split_on = xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2;
+  // a conv split on its own third stream needs one graph; on the comm stream it is part of the side chain
+  const bool conv_split_on = xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2 &&
+                             conv2_stream_ != comm_stream_;
   // RCCL side chains stay in ONE graph: launched as a separate side graph, the RCCL schedule ran
   // 340 us per world-1 step instead of 101 (measured on the box; the xGMI and single-GPU side chains
   // gain from the split: 100 -> 86 / 95 -> 77 us over a 20-step window)
@@ -739,7 +741,7 @@ bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
 
 bool Engine::probe_stream_handoff(double timeout_s) {
   if (!probe_stream_pair(compute_, comm_stream_, timeout_s)) return false;
-  if (conv2_stream_ && (!probe_stream_pair(compute_, conv2_stream_, timeout_s) ||
+  if (conv2_stream_ && conv2_stream_ != comm_stream_ && (!probe_stream_pair(compute_, conv2_stream_, timeout_s) ||
                         !probe_stream_pair(comm_stream_, conv2_stream_, timeout_s)))
     return false;
   return true;

@@ -201,10 +201,16 @@ class FusedTrainer:
                 # dgrad.  Bitwise equal; at world 1 it costs 1-2 us/step (88.0-89.1 vs 87.0-87.1: two
                 # more hand-off kernels and a third graph branch) and what it saves at world > 1 (the
                 # conv2 slab reduce off the critical path) is unmeasured on one GPU, so it is off.
-                if self.xgmi_fuse and os.environ.get("MNIST_AMD_CONV_SPLIT", "0") == "1":
+                # MNIST_AMD_CONV_SPLIT=comm queues the conv2 part on the comm stream after the fc
+                # bucket instead (no third stream; part of the side graph of every chunk)
+                split_mode = os.environ.get("MNIST_AMD_CONV_SPLIT", "0")
+                if self.xgmi_fuse and split_mode == "1":
                     self.conv2_stream = torch.cuda.Stream(device=dev)
                     self.engine.set_conv_split(True, int(self.conv2_stream.cuda_stream))
                     self.conv_split = True
+                elif self.xgmi_fuse and split_mode == "comm":
+                    self.engine.set_conv_split(True, int(self.comm_stream.cuda_stream))
+                    self.conv_split = "comm"
         # schedule 3 spins on one stream for the other: make sure they sit on different hardware
         # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
         uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3) or self.overlap_fc

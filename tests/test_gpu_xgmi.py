@@ -71,17 +71,19 @@ def test_trainer_auto_probe_path_world1(tmp_path):
 
 
 @pytest.mark.timeout(200)
-def test_conv_bucket_split_bitwise_at_two_ranks(cuda_device):
-    """Opt-in conv bucket split (MNIST_AMD_CONV_SPLIT=1): the startup validation inside the engine
+@pytest.mark.parametrize("mode", ["1", "comm"])
+def test_conv_bucket_split_bitwise_at_two_ranks(cuda_device, mode):
+    """Opt-in conv bucket split (MNIST_AMD_CONV_SPLIT=1: a third stream, =comm: queued on the comm
+    stream after the fc bucket, inside the side graph): the startup validation inside the engine
     check compares it bitwise with the separate launches, at 2 ranks on one GPU (4 HW queues per
     process: the split's third stream needs its own queue)."""
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "xgmi_check.py"), "--world", "2", "--same-device",
            "--iters", "10", "--engine-steps", "20", "--timeout", "170"]
-    env = dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_CONV_SPLIT="1", GPU_MAX_HW_QUEUES="4")
+    env = dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_CONV_SPLIT=mode, GPU_MAX_HW_QUEUES="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=185, env=env)
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
-    assert "conv split True" in r.stdout
+    assert ("conv split True" if mode == "1" else "conv split comm") in r.stdout
 
 
 def test_rccl_single_communicator_schedule_world1(tmp_path):
