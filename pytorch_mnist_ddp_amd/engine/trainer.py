@@ -201,9 +201,11 @@ class FusedTrainer:
                 # dgrad.  Bitwise equal; at world 1 it costs 1-2 us/step (88.0-89.1 vs 87.0-87.1: two
                 # more hand-off kernels and a third graph branch) and what it saves at world > 1 (the
                 # conv2 slab reduce off the critical path) is unmeasured on one GPU, so it is off.
-                # MNIST_AMD_CONV_SPLIT=comm queues the conv2 part on the comm stream after the fc
-                # bucket instead (no third stream; part of the side graph of every chunk)
-                split_mode = os.environ.get("MNIST_AMD_CONV_SPLIT", "0")
+                # MNIST_AMD_CONV_SPLIT=comm (default) queues the conv2 part on the comm stream after the
+                # fc bucket instead (no third stream; part of every chunk's side graph): at world 1
+                # neutral (78.9-80.3 vs 79.1-79.6 us/step), at world > 1 it takes conv2's slab reduce
+                # + exchange + update (98 % of the conv bucket) off the critical path; bitwise equal
+                split_mode = os.environ.get("MNIST_AMD_CONV_SPLIT", "comm")
                 if self.xgmi_fuse and split_mode == "1":
                     self.conv2_stream = torch.cuda.Stream(device=dev)
                     self.engine.set_conv_split(True, int(self.conv2_stream.cuda_stream))
