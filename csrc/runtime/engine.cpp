@@ -29,6 +29,7 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_c2_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_join2_, hipEventDisableTiming));
   alloc_workspace();   // (the wgrad stream of the concurrent schedule is created on demand: every
                        // stream may take a hardware queue, and queues are a shared resource)
 }
@@ -44,6 +45,8 @@ Engine::~Engine() {
   }
   for (auto g : side_graphs_)
     if (g) hipGraphExecDestroy(g);
+  for (auto g : side2_graphs_)
+    if (g) hipGraphExecDestroy(g);
   for (auto g : graphs_) hipGraphExecDestroy(g);
   for (auto g : graph_defs_) hipGraphDestroy(g);
   if (ev_fc_) hipEventDestroy(ev_fc_);
@@ -53,6 +56,7 @@ Engine::~Engine() {
   if (ev_c2_) hipEventDestroy(ev_c2_);
   if (ev_fork_) hipEventDestroy(ev_fork_);
   if (ev_join_) hipEventDestroy(ev_join_);
+  if (ev_join2_) hipEventDestroy(ev_join2_);
   if (wgrad_stream_) hipStreamDestroy(wgrad_stream_);
   if (ws_) hipFree(ws_);
 }
@@ -164,6 +168,8 @@ void Engine::enqueue_step(int batch, bool last) {
   const float gscale = kDdpEpilogueScale;
   // two-pass capture (capture_train): M = enqueue the compute-stream work, S = the side streams'
   const bool M = enq_main_, S = enq_side_;
+  // conv2-stream work: its own pass when that stream is a third one, else part of the comm pass
+  const bool T = (conv2_stream_ && conv2_stream_ != comm_stream_) ? enq_side2_ : enq_side_;
 
   // pre-gathered epoch rows when available (one load level less on every step's critical path)
   const bool pre = buf_.epoch_u8 != nullptr;
@@ -276,7 +282,7 @@ void Engine::enqueue_step(int batch, bool last) {
       ad2.state_inc = nullptr;
       ad2.w2d = w2d_next;
       cb.w2d = w2d_cur;
-      if (S) {
+      if (T) {
         launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
         XgmiConvPart p2;
         p2.lo = 0;
@@ -509,14 +515,11 @@ void Engine::train_steps(int n, int batch, int stride) {
 int Engine::capture_train(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
-  // a conv split on its own third stream needs one graph; on the comm stream it is part of the side chain
-  const bool conv_split_on = xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2 &&
-                             conv2_stream_ != comm_stream_;
   // RCCL side chains stay in ONE graph: launched as a separate side graph, the RCCL schedule ran
   // 340 us per world-1 step instead of 101 (measured on the box; the xGMI and single-GPU side chains
   // gain from the split: 100 -> 86 / 95 -> 77 us over a 20-step window)
   const bool rccl_side = comm_ && !xgmi_;
-  if (side_first_ && uses_side_streams() && !conv_split_on && !rccl_side) return capture_train_split(n, batch);
+  if (side_first_ && uses_side_streams() && !rccl_side) return capture_train_split(n, batch);
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
   try {
@@ -556,7 +559,7 @@ int Engine::capture_train(int n, int batch, int stride) {
 }
 
 void Engine::reset_host_state() {
-  enq_main_ = enq_side_ = true;
+  enq_main_ = enq_side_ = enq_side2_ = true;
   skip_join_ = false;
   side_pending_ = false;
   side_forked_ = false;
@@ -574,48 +577,56 @@ void Engine::reset_host_state() {
 // 93-97 us/step against 73.5 steady state.  The fork (chunk start -> comm stream) and the join
 // (comm stream -> compute) become two events at replay.
 int Engine::capture_train_split(int n, int batch) {
+  // xGMI conv bucket split on a third stream: its chain (conv2 reduce + exchange + update, released
+  // by conv2_dgrad's start) is a third graph, so it starts under dgrad instead of queueing behind
+  // the fc bucket on the comm stream
+  const bool third = conv2_stream_ && conv2_stream_ != comm_stream_ && xgmi_ && xgmi_fuse_update_ && conv_split_ &&
+                     xgmi_->channels() > XGMI_CH_CONV2;
   const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
-  hipGraph_t gs = nullptr, gm = nullptr;
-  try {
-    side_forked_ = true;                   // the fork is an event at replay, not a captured edge
-    enq_main_ = false;
-    HIP_OK(hipStreamBeginCapture(comm_stream_, hipStreamCaptureModeRelaxed));
-    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
-    HIP_OK(hipStreamEndCapture(comm_stream_, &gs));
+  hipGraph_t gs = nullptr, g2 = nullptr, gm = nullptr;
+  auto pass = [&](hipStream_t s, bool m, bool side, bool side2, hipGraph_t* out) {
     side_pending_ = sp;
     w1t_in_alt_ = w1;
     w2d_in_alt_ = w2;
-    side_forked_ = true;
-    enq_main_ = true;
-    enq_side_ = false;
-    skip_join_ = true;                     // the join is an event at replay
-    HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
+    side_forked_ = true;                   // forks / joins are events at replay, not captured edges
+    enq_main_ = m;
+    enq_side_ = side;
+    enq_side2_ = side2;
+    skip_join_ = true;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
-    HIP_OK(hipStreamEndCapture(compute_, &gm));
-    enq_side_ = true;
+    HIP_OK(hipStreamEndCapture(s, out));
+  };
+  try {
+    pass(comm_stream_, false, true, false, &gs);
+    if (third) pass(conv2_stream_, false, false, true, &g2);
+    pass(compute_, true, false, false, &gm);
+    enq_main_ = enq_side_ = enq_side2_ = true;
     skip_join_ = false;
   } catch (...) {
     reset_host_state();
-    hipGraph_t junk = nullptr;
     hipStreamCaptureStatus st;
-    if (hipStreamIsCapturing(comm_stream_, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
-      hipStreamEndCapture(comm_stream_, &junk);
-    if (junk) hipGraphDestroy(junk);
-    junk = nullptr;
-    if (hipStreamIsCapturing(compute_, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
-      hipStreamEndCapture(compute_, &junk);
-    if (junk) hipGraphDestroy(junk);
-    if (gs) hipGraphDestroy(gs);
-    if (gm) hipGraphDestroy(gm);
+    for (hipStream_t s : {comm_stream_, conv2_stream_, compute_}) {
+      hipGraph_t junk = nullptr;
+      if (s && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
+        hipStreamEndCapture(s, &junk);
+      if (junk) hipGraphDestroy(junk);
+    }
+    for (hipGraph_t g : {gs, g2, gm})
+      if (g) hipGraphDestroy(g);
     throw;
   }
-  hipGraphExec_t xs = nullptr, xm = nullptr;
+  hipGraphExec_t xs = nullptr, x2 = nullptr, xm = nullptr;
   HIP_OK(hipGraphInstantiate(&xs, gs, nullptr, nullptr, 0));
+  if (g2) HIP_OK(hipGraphInstantiate(&x2, g2, nullptr, nullptr, 0));
   HIP_OK(hipGraphInstantiate(&xm, gm, nullptr, nullptr, 0));
   graph_defs_.push_back(gs);
+  if (g2) graph_defs_.push_back(g2);
   graph_defs_.push_back(gm);
   graphs_.push_back(xm);
   side_graphs_.push_back(xs);
+  side2_graphs_.resize(graphs_.size(), nullptr);
+  side2_graphs_.back() = x2;
   return (int)graphs_.size() - 1;
 }
 
@@ -626,10 +637,12 @@ void Engine::side_worker() {
   for (;;) {
     side_cv_.wait(lk, [this] { return side_stop_ || side_job_ != nullptr; });
     if (side_stop_) return;
-    hipGraphExec_t job = side_job_;
+    hipGraphExec_t job = side_job_, job2 = side2_job_;
     lk.unlock();
     hipError_t e = hipGraphLaunch(job, comm_stream_);
     if (e == hipSuccess) e = hipEventRecord(ev_join_, comm_stream_);
+    if (e == hipSuccess && job2) e = hipGraphLaunch(job2, conv2_stream_);
+    if (e == hipSuccess && job2) e = hipEventRecord(ev_join2_, conv2_stream_);
     lk.lock();
     side_err_ = e;
     side_job_ = nullptr;
@@ -652,12 +665,15 @@ void Engine::replay(int id) {
     HIP_OK(hipGraphLaunch(graphs_[id], compute_));
     return;
   }
-  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chain ordered after earlier compute work
+  hipGraphExec_t side2 = id < (int)side2_graphs_.size() ? side2_graphs_[id] : nullptr;
+  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chains ordered after earlier compute work
   HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
+  if (side2) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fork_, 0));
   {
     std::lock_guard<std::mutex> lk(side_mu_);
     if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
     side_job_ = side;
+    side2_job_ = side2;
     side_done_ = false;
   }
   side_cv_.notify_all();
@@ -670,7 +686,8 @@ void Engine::replay(int id) {
   }
   HIP_OK(em);
   HIP_OK(es);
-  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain
+  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain(s)
+  if (side2) HIP_OK(hipStreamWaitEvent(compute_, ev_join2_, 0));
 }
 
 void Engine::enqueue_eval(int n_total, int batch) {

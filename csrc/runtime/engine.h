@@ -183,13 +183,15 @@ class Engine {
   bool side_first_ = true;
   bool side_conv2_ = false;
   bool enq_main_ = true, enq_side_ = true;   // two-pass capture: which streams enqueue_step feeds
+  bool enq_side2_ = true;                     // split capture: the third (conv2) stream's pass
   bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
   std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  std::vector<hipGraphExec_t> side2_graphs_;  // per graph id: its conv2-stream graph (third-stream split) or null
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_join2_ = nullptr;
   std::thread side_thread_;                   // launches side graphs concurrently with the compute graph
   std::mutex side_mu_;
   std::condition_variable side_cv_;
-  hipGraphExec_t side_job_ = nullptr;
+  hipGraphExec_t side_job_ = nullptr, side2_job_ = nullptr;
   bool side_done_ = false, side_stop_ = false;
   hipError_t side_err_ = hipSuccess;
   bool conv_split_ = false;
