@@ -279,9 +279,12 @@ def main() -> int:
     if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(tr.compute)                                   # device-side view of the same window
     tr.engine.gather_rows(args.warmup * B, args.steps * B)   # the device DataLoader work is timed too
     tr.run_steps(args.steps)
+    ev1.record(tr.compute)                                   # (after the chunk's join: all streams)
     t_enq = time.perf_counter()                              # host: every timed chunk enqueued
     tr.engine.sync_streams()
     torch.cuda.synchronize()
@@ -422,6 +425,7 @@ def main() -> int:
             "last_train_loss": round(final_loss, 4),
             "setup_s": round(t0 - t_setup, 2),
             "timed_enqueue_ms": round(1000.0 * (t_enq - t0), 3),
+            "timed_device_ms": round(ev0.elapsed_time(ev1), 3),
             "setup_phases_s": phases.rounded(3),
         }
         print(json.dumps(out), flush=True)
