@@ -59,6 +59,12 @@ struct HeadArgs {
   const float* dlogp;         // module API backward: upstream grad wrt log-probs [B][10] (replaces NLL)
 };
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s);
+// fc1 + training head in one launch (B < FC1_BIG_MIN_B, fc1 MR = 2; opt-in MNIST_AMD_FUSE_HEAD=1, slower):
+// ctr / hdone = FC1_HEAD_MAX_TILES zero-initialised ints each (self re-arming), err = error flag
+constexpr int FC1_HEAD_MAX_TILES = (FC1_BIG_MIN_B + 31) / 32;   // 16
+bool fc1_head_fusable(int B);
+void launch_fc1_head_train(const uint16_t* p, const uint16_t* w1, const HeadArgs& a, int B, int Bp, int* ctr,
+                           int* hdone, int* err, hipStream_t s);
 void launch_head_eval(const HeadArgs& a, int B, hipStream_t s);
 // module API forward: log-probs with (train) or without (eval) dropout-2
 void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);

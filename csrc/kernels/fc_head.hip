@@ -20,10 +20,11 @@ namespace mnist {
 // ============================================================================================
 // MR = 16-row M-tiles per workgroup: MR = 2 (default) halves the w1 fragment traffic per output
 // (each wave's B fragments feed two M-tiles) at half the workgroups; bitwise the MR = 1 result.
-template <int MR>
-__global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
-                                                      const uint16_t* __restrict__ w1,
-                                                      float* __restrict__ z1part, int B) {
+// One fc1 workgroup (row tile x K-chunk) of the R x 32 grid, linear id `lin`; returns the row tile.
+// SC1: z1part written with sc1 (write-through) stores, for the fused head consumers below.
+template <int MR, bool SC1>
+__device__ __forceinline__ int fc1_tile(const uint16_t* __restrict__ p, const uint16_t* __restrict__ w1,
+                                        float* __restrict__ z1part, int B, int R, int lin) {
   constexpr int KC = NFLAT / FC1_KSPLIT;   // 288
   constexpr int KS = KC / 32;              // 9
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -32,8 +33,6 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
   // give every XCD 4 whole K-chunks (all row tiles of each): a chunk's 74 KB w1 slice is then
   // fetched into ONE XCD's L2 instead of all eight (grid = R x 32, R*32 divisible by 8)
   static_assert(FC1_KSPLIT == 32, "4 K-chunks per XCD");
-  const int R = gridDim.x;
-  const int lin = blockIdx.x + R * blockIdx.y;
   const int xcd = lin & 7, j = lin >> 3;
   const int chunk = 4 * xcd + j / R;
   const int tile = j - (j / R) * R;
@@ -67,11 +66,24 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
       const int b = (tile * MR + t) * 16 + 4 * kg + r;
       if (b < B) {
         float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
-        dst[0] = acc0[r];
-        dst[16] = acc1[r];
+        if constexpr (SC1) {
+          __hip_atomic_store(dst, acc0[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dst + 16, acc1[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          dst[0] = acc0[r];
+          dst[16] = acc1[r];
+        }
       }
     }
   }
+  return tile;
+}
+
+template <int MR>
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
+                                                      const uint16_t* __restrict__ w1,
+                                                      float* __restrict__ z1part, int B) {
+  fc1_tile<MR, false>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
 }
 
 // Large batches: 64 rows x 128 columns per workgroup, K split 4 ways (2304 = 36 stages of 64),
@@ -263,10 +275,10 @@ __device__ __forceinline__ void log_softmax10(const float* x, float* lp) {
 // a branch-guarded load ends in vmcnt(0), which used to finish the label + bias round trip before
 // the partial-sum loads even went out.  Arithmetic (order and expression forms) is that of
 // head_forward_row / the module head, so the results are bitwise unchanged.
-template <int KS, bool IDX>
-__global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int b = blockIdx.x * (blockDim.x >> 6) + wave;
+// One wave = one batch row b.  SC1: the split-K partials are read with sc1 loads (they were
+// published by other workgroups of the same launch: fc1_head_train_kernel).
+template <int KS, bool IDX, bool SC1>
+__device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, int lane) {
   if (b >= B) {  // padding rows of the bf16 operands consumed by the backward GEMMs
     a.dz1[(int64_t)b * NH + lane] = 0;
     a.dz1[(int64_t)b * NH + lane + 64] = 0;
@@ -288,7 +300,11 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
 #pragma unroll
   for (int c = 0; c < KS; ++c)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) part[c][j] = a.z1part[((int64_t)c * B + b) * NH + lane + 64 * j];
+    for (int j = 0; j < 2; ++j) {
+      const float* src = a.z1part + ((int64_t)c * B + b) * NH + lane + 64 * j;
+      if constexpr (SC1) part[c][j] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else part[c][j] = *src;
+    }
 #pragma unroll
   for (int j = 0; j < 2; ++j) bf1[j] = a.b_fc1[lane + 64 * j];
 #pragma unroll
@@ -356,6 +372,75 @@ __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
     for (int c = 0; c < NCLS; ++c) v = (lane == c) ? dl[c] : v;
     a.dl_bf[(int64_t)b * 16 + lane] = f2bf(v);
   }
+}
+
+template <int KS, bool IDX>
+__global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
+  head_train_row<KS, IDX, false>(a, B, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), threadIdx.x & 63);
+}
+
+// fc1 (B < FC1_BIG_MIN_B) and the training head in ONE launch.  Workgroups [0, 32R) are fc1's
+// (row tile of 32 rows x K-chunk, exactly fc1_fwd_kernel<2>'s), each publishing its sc1-stored
+// partials with one agent-scope counter add per row tile after every wave's vmcnt(0) + a barrier;
+// workgroups [32R, 32R + Bp/4) are the head's (4 rows each, exactly head_train_kernel's math), each
+// polling its tile's counter, then reading the partials with sc1 loads.  Dispatch is in grid order
+// on every XCD and producers never wait, so the consumers always make progress; the tile's last
+// head workgroup re-arms the two counters for the next launch (stream-ordered).  Saves the fc1 ->
+// head kernel boundary and lets the head's workgroups be resident before their data is.
+template <bool IDX>
+__global__ __launch_bounds__(256) void fc1_head_train_kernel(const uint16_t* __restrict__ p,
+                                                             const uint16_t* __restrict__ w1, HeadArgs a, int B,
+                                                             int R, int* ctr, int* hdone, int* err) {
+  const int nF = R * FC1_KSPLIT;
+  if ((int)blockIdx.x < nF) {
+    const int tile = fc1_tile<2, true>(p, w1, const_cast<float*>(a.z1part), B, R, blockIdx.x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int h = blockIdx.x - nF;
+  const int tile = (4 * h) / 32;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(ctr + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < FC1_KSPLIT) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {   // 60 s: report, do not hang
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
+  head_train_row<FC1_KSPLIT, IDX, true>(a, B, 4 * h + (threadIdx.x >> 6), threadIdx.x & 63);
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(hdone + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 32 / 4 - 1) {
+    __hip_atomic_store(ctr + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm (next launch)
+    __hip_atomic_store(hdone + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool fc1_head_fusable(int B) {
+  if (fc1_ksplit(B) != FC1_KSPLIT) return false;
+  const char* e = getenv("MNIST_AMD_FC1_MR");              // the fused form is fc1's MR = 2 tiling
+  if (e && atoi(e) != 2) return false;
+  // opt-in (MNIST_AMD_FUSE_HEAD=1): measured SLOWER at B = 200 - 600 steps 71.4 -> 76.4-77.3 us,
+  // the 20-step window 75.8-77.4 -> 82.3-83.3 (bitwise equal losses): the head workgroups wait for
+  // the LAST of their tile's 32 chunk workgroups and then read the partials with write-through
+  // visibility, which costs more than the kernel boundary it removes
+  const char* f = getenv("MNIST_AMD_FUSE_HEAD");
+  return f && f[0] == '1';
+}
+
+void launch_fc1_head_train(const uint16_t* p, const uint16_t* w1, const HeadArgs& a, int B, int Bp, int* ctr,
+                           int* hdone, int* err, hipStream_t s) {
+  const int R = (B + 31) / 32;
+  if (Bp != 32 * R || R > FC1_HEAD_MAX_TILES) throw std::runtime_error("fc1_head_train: bad batch");
+  const dim3 g(R * FC1_KSPLIT + Bp / 4), t(256);
+  if (a.idx) hipLaunchKernelGGL(fc1_head_train_kernel<true>, g, t, 0, s, p, w1, a, B, R, ctr, hdone, err);
+  else hipLaunchKernelGGL(fc1_head_train_kernel<false>, g, t, 0, s, p, w1, a, B, R, ctr, hdone, err);
 }
 
 __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {

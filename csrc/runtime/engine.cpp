@@ -205,13 +205,15 @@ void Engine::enqueue_step(int batch, bool last) {
     if (!hold) HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
     side_pending_ = false;
   }
-  if (M) launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
+  const bool fuse_head = fc1_head_fusable(B);
+  if (M && !fuse_head) launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
   ha.labels = labels; ha.idx = idxp; ha.idx_step_stride = stride;
   ha.state = buf_.state; ha.inv_batch = ddp_head_inv_batch(B, world_);
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
-  if (M) launch_head_train(ha, B, Bp, compute_);
+  if (M && fuse_head) launch_fc1_head_train(p_, buf_.w1, ha, B, Bp, sync_ + 16, sync_ + 32, sync_ + 2, compute_);
+  else if (M) launch_head_train(ha, B, Bp, compute_);
   phase_end();
   const bool dist = comm_ != nullptr || xgmi_ != nullptr;   // world_size 1 + comm: DDP schedule (tests)
   // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t

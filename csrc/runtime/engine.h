@@ -175,7 +175,8 @@ class Engine {
   bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
   bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
   int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error,
-                                    // [3]/[4] conv split, [8..11] probes,
+                                    // [3]/[4] conv split, [8..11] probes, [16..31] / [32..47] fc1+head
+                                    // tile counters (FC1_HEAD_MAX_TILES each),
                                     // [12] fc all-reduce done (1 comm)
   bool fuse_fc_update_ = false;
   bool overlap_fc_update_ = false;
