@@ -520,7 +520,8 @@ int Engine::capture_train(int n, int batch, int stride) {
   // RCCL side chains stay in ONE graph: launched as a separate side graph, the RCCL schedule ran
   // 340 us per world-1 step instead of 101 (measured on the box; the xGMI and single-GPU side chains
   // gain from the split: 100 -> 86 / 95 -> 77 us over a 20-step window)
-  const bool rccl_side = comm_ && !xgmi_;
+  static const bool rccl_split = [] { const char* e = getenv("MNIST_AMD_RCCL_SPLIT"); return e && e[0] == '1'; }();
+  const bool rccl_side = comm_ && !xgmi_ && !rccl_split;
   if (side_first_ && uses_side_streams() && !rccl_side) return capture_train_split(n, batch);
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
@@ -671,6 +672,19 @@ void Engine::replay(int id) {
   HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chains ordered after earlier compute work
   HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
   if (side2) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fork_, 0));
+  static const bool threaded = [] { const char* e = getenv("MNIST_AMD_SIDE_THREAD"); return !(e && e[0] == '0'); }();
+  if (!threaded) {                                      // (A/B knob) side graphs first, same thread
+    HIP_OK(hipGraphLaunch(side, comm_stream_));
+    HIP_OK(hipEventRecord(ev_join_, comm_stream_));
+    if (side2) {
+      HIP_OK(hipGraphLaunch(side2, conv2_stream_));
+      HIP_OK(hipEventRecord(ev_join2_, conv2_stream_));
+    }
+    HIP_OK(hipGraphLaunch(graphs_[id], compute_));
+    HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));
+    if (side2) HIP_OK(hipStreamWaitEvent(compute_, ev_join2_, 0));
+    return;
+  }
   {
     std::lock_guard<std::mutex> lk(side_mu_);
     if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
