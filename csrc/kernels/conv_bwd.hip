@@ -25,6 +25,19 @@
 
 namespace mnist {
 
+// Phase timing of the per-item dgrad (tools/dgrad_phase.hip compiles this file with
+// MNIST_DGRAD_PHASE_TIMING): thread 0 of every workgroup records s_memtime at each phase boundary.
+#ifdef MNIST_DGRAD_PHASE_TIMING
+constexpr int kDgPhaseMaxWG = 32768;
+__device__ uint64_t g_dg_phase[kDgPhaseMaxWG * 8];
+__device__ int g_dg_stagger;                     // persistent form: ticks the second half of the grid waits
+#define DG_MARK(i)                                                                             \
+  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < kDgPhaseMaxWG)                 \
+    g_dg_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime();
+#else
+#define DG_MARK(i)
+#endif
+
 namespace {
 constexpr int DG_ROWS = 7;                              // conv1-output rows per dgrad WG (4 strips)
 constexpr int DG_TROWS = DG_ROWS + 2;                   // dy rows incl. halo (top 2)
@@ -37,7 +50,7 @@ constexpr int DG_TCOLS = H2 + 4;                        // 28 (2 zero columns ea
 constexpr int DG_PITCH = 28;
 constexpr int DYS_BYTES = DG_TROWS * DG_PITCH * C2 * 2; // 32256
 constexpr int W2DS_BYTES = 9 * C1 * C2 * 2;             // 36864
-constexpr int XS2_BYTES = DG_TROWS * IMG * 4;           // 1008 -> pad 1024
+constexpr int XS2_BYTES = 256 * 4;                     // DG_TROWS * IMG = 252 input pixels + 4 zeros
 constexpr int RED_BYTES = 4 * 32 * 10 * 4;              // 5120
 constexpr int DG_LDS = DYS_BYTES + W2DS_BYTES + 1024;   // 70144: two per CU; the conv1-gradient
                                                         // reduction scratch aliases the dy tile
@@ -221,12 +234,35 @@ __device__ __forceinline__ void dgrad_red_reduce(const ConvBwdArgs& a, int strip
 // partials in red (the caller reduces them later).  The staggered-halves dgrad that used this
 // (one 8-wave workgroup per CU, halves alternating MFMA and staging phases) measured slower than
 // two independent per-item workgroups per CU (B = 8192: 1.56 vs 1.24 ms/step) and was removed.
-template <int XM, bool STAG, class Prefetch>
+// conv1 ReLU mask operand of the epilogue = the stored bf16 a1 values of this wave's 3 M-tiles
+// (lane: channel m and m + 16 of pixels 4kg..4kg+3 of each tile)
+constexpr int DG_MT = 3;
+struct DgMask {
+  uint16_t v[DG_MT][4][2];
+};
+__device__ __forceinline__ void dgrad_mask_load(const ConvBwdArgs& a, int strip, int b, int wave, DgMask& M) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kg = lane >> 4;
+  const int r0 = strip * DG_ROWS;
+  const int npix = ((strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS) * H1;
+#pragma unroll
+  for (int i = 0; i < DG_MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int q = 16 * (3 * wave + i) + 4 * kg + r;
+      q = q < npix ? q : npix - 1;
+      const uint16_t* src = a.a1 + ((int64_t)b * H1 * H1 + r0 * H1 + q) * C1 + m;
+      M.v[i][r][0] = src[0];
+      M.v[i][r][1] = src[16];
+    }
+}
+
+// PRE: the caller issued the mask loads (dgrad_mask_load) before staging, so their HBM latency
+// hides under the staging phase too; else they are issued here, ahead of the MFMA loop.
+template <int XM, bool STAG, bool PRE, class Prefetch>
 __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip, int b, uint16_t* dys,
                                                 const uint16_t* w2ds, float* xs, float* red, int wave,
-                                                int ltid, float xv, Prefetch prefetch) {
+                                                int ltid, float xv, const DgMask& pre, Prefetch prefetch) {
   const int lane = threadIdx.x & 63, tid = ltid;
-  const int r0 = strip * DG_ROWS;
   const int nrows = (strip == 3) ? (H1 - 3 * DG_ROWS) : DG_ROWS;   // 7,7,7,5
   const int npix = nrows * H1;
 
@@ -235,7 +271,7 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   // bank-conflict free but needs 13 tiles per strip - an unbalanced, branchy split that measured
   // slower; this balanced split keeps the row&7 swizzle at ~1.6x the ideal read cost.)
   const int m = lane & 15, kg = lane >> 4;
-  constexpr int MT = 3;
+  constexpr int MT = DG_MT;
   // A-fragment addresses without per-read VALU: for tap t = 3d + c the LDS row is R_c - 28d with
   // R_c = qbase - c, and (R_c - 28d) & 7 = (R_c & 7) ^ 4(d & 1), so the swizzled chunk of co-half h is
   // ((kg ^ (R_c & 7)) ^ 4(h ^ (d & 1))): per (M-tile, c) two base addresses (chunk bit 2 clear / set)
@@ -244,10 +280,12 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   const uint16_t* abase[MT][3][2];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    int q = 16 * (3 * wave + i) + m;
-    if (q >= npix) q = 0;
+    const int q = 16 * (3 * wave + i) + m;
     const int qy = q / H1, qx = q - qy * H1;
-    const int qbase = (qy + 2) * DG_PITCH + qx + 2;     // LDS row of the un-shifted pixel
+    // LDS row of the un-shifted pixel.  A pixel past the strip reads a window of padding zeros
+    // (rows 1-3, columns 27 / 0 / 1: every tap lands on one), so its accumulator row is exactly 0
+    // and the epilogue needs no pixel-range mask.
+    const int qbase = q < npix ? (qy + 2) * DG_PITCH + qx + 2 : 3 * DG_PITCH + 1;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const int rc = qbase - c;
@@ -262,19 +300,11 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   floatx4 acc[MT][2];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // conv1 ReLU mask for the epilogue = (a1 > 0): prefetch the stored bf16 a1 values now so the
+  // conv1 ReLU mask for the epilogue = (a1 > 0): the stored bf16 a1 values, loaded ahead so the
   // loads overlap the MFMA loop (no conv1 recompute)
-  uint16_t a1v[MT][4][2];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int q = 16 * (3 * wave + i) + 4 * kg + r;
-      q = q < npix ? q : npix - 1;
-      const uint16_t* src = a.a1 + ((int64_t)b * H1 * H1 + r0 * H1 + q) * C1 + m;
-      a1v[i][r][0] = src[0];
-      a1v[i][r][1] = src[16];
-    }
+  DgMask own;
+  if constexpr (!PRE) dgrad_mask_load(a, strip, b, wave, own);
+  const DgMask& mk = PRE ? pre : own;
   prefetch();
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) {
@@ -289,11 +319,13 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bf[nt], acc[i][nt]);
   }
+  DG_MARK(3);
 
   if constexpr (!STAG) {
-    if (tid < DG_TROWS * IMG) xs[tid] = dgrad_xs_value<XM>(xv);   // input rows: first read below
+    xs[tid] = dgrad_xs_value<XM>(xv);             // input rows (entries 252-255: zeros), first read below
     __syncthreads();
   }
+  DG_MARK(5);
 
   // ---- conv1 ReLU mask (a1 > 0), then the conv1 weight/bias gradient of this strip as a
   // second, tiny MFMA: D[tap][ci] = sum_px X[px][tap] * d[px][ci] on v_mfma_f32_16x16x16_bf16
@@ -303,20 +335,25 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   floatx4 dw[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
   {
     const int tap = lane & 15, ty = tap / 3, tx = tap - 3 * ty;
+    const int toff = tap < 9 ? ty * IMG + tx : 0;          // xs offset of the tap (any valid one past 8)
+    const float xconst = tap == 9 ? 1.0f : 0.0f;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
+      // xs index of input pixel (py + ty, px + tx) of output pixel q = 26 py + px is q + 2 py + toff;
+      // the lane's 4 pixels q0..q0+3 step along a row and wrap at most once (+2 past the row end).
+      // Pixels past the strip read any in-range entry (their gradient rows are 0, see qbase).
+      const int q0 = 16 * (3 * wave + i) + 4 * kg;
+      const int qy0 = q0 / H1, qx0 = q0 - qy0 * H1;
+      const int a0 = q0 + 2 * qy0 + toff;
       float xf[4], df[2][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int q = 16 * (3 * wave + i) + 4 * kg + j;
-        const int qc = q < npix ? q : npix - 1;
-        const int py = qc / H1, px = qc - py * H1;
-        xf[j] = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
+        const int aj = min(a0 + j + (qx0 + j >= H1 ? 2 : 0), 255);
+        const float xr = xs[aj];
+        xf[j] = tap < 9 ? xr : xconst;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const uint16_t av = a1v[i][j][nt];
-          df[nt][j] = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
-        }
+        for (int nt = 0; nt < 2; ++nt)       // conv1 ReLU mask: bf16 a1 > 0 <=> as int16 > 0
+          df[nt][j] = (int16_t)mk.v[i][j][nt] > 0 ? acc[i][nt][j] : 0.0f;
       }
       // bf16 operands two at a time (one v_cvt_pk_bf16_f32 per pair)
       const short4_t ax = __builtin_bit_cast(short4_t, uint2{pack2bf(xf[0], xf[1]), pack2bf(xf[2], xf[3])});
@@ -327,6 +364,7 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
       }
     }
   }
+  DG_MARK(6);
   // dw[nt]: lane l holds D[tap = 4(l>>4) + r][ci = 16nt + (l&15)]
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
@@ -341,15 +379,15 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   }
 }
 
-template <int XM, class Prefetch>
+template <int XM, bool PRE = false, class Prefetch>
 __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, int b, unsigned char* smem, float xv,
-                                              Prefetch prefetch) {
+                                              const DgMask& pre, Prefetch prefetch) {
   uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
   const uint16_t* w2ds = reinterpret_cast<const uint16_t*>(smem + DYS_BYTES);
   float* xs = reinterpret_cast<float*>(smem + DYS_BYTES + W2DS_BYTES);
   float* red = reinterpret_cast<float*>(smem);   // aliases the dy tile: written after the barrier
                                                   // that ends every wave's MFMA loop
-  dgrad_compute_p<XM, false>(a, strip, b, dys, w2ds, xs, red, threadIdx.x >> 6, threadIdx.x, xv, prefetch);
+  dgrad_compute_p<XM, false, PRE>(a, strip, b, dys, w2ds, xs, red, threadIdx.x >> 6, threadIdx.x, xv, pre, prefetch);
 }
 
 template <int XM>
@@ -361,14 +399,26 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const StepState* st = a.state ? a.state : &g_zero_state;
   const int step = st->step;                      // oldest load: the input-row chain hangs off it
+  DG_MARK(0);
   uint4 w[9];
   dgrad_w2d_load(a, tid, w);
   DgLoad L;
   dgrad_fetch<XM>(a, strip, b, step, tid, L);
+#ifndef MNIST_DGRAD_LATE_MASK
+  DgMask mk;                                      // issued last: first needed in the epilogue
+  dgrad_mask_load(a, strip, b, tid >> 6, mk);
+  constexpr bool kPre = true;
+#else
+  const DgMask mk{};                              // A/B (tools/dgrad_phase.hip): issue under the MFMA loop
+  constexpr bool kPre = false;
+#endif
   dgrad_w2d_store(smem, tid, w);
+  DG_MARK(1);
   dgrad_dy_store(smem, strip, tid, L);
   __syncthreads();
-  dgrad_compute<XM>(a, strip, b, smem, L.xv, [] {});
+  DG_MARK(2);
+  dgrad_compute<XM, kPre>(a, strip, b, smem, L.xv, mk, [] {});
+  DG_MARK(4);
 }
 
 template <int XM>
@@ -392,6 +442,12 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const StepState* st = a.state ? a.state : &g_zero_state;
   const int step = st->step;
+#ifdef MNIST_DGRAD_PHASE_TIMING
+  if (2 * it >= G && g_dg_stagger > 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)g_dg_stagger) __builtin_amdgcn_s_sleep(2);
+  }
+#endif
   uint4 w[9];
   dgrad_w2d_load(a, tid, w);
   DgLoad L;
@@ -404,9 +460,9 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs
     __syncthreads();
     const int nx = (it + G < n) ? it + G : it;   // clamped: the last item's prefetch is a re-read
     if constexpr (PF)
-      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
+      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
     else
-      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, [] {});
+      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [] {});
     __syncthreads();                              // the next dy store must not overtake the red reads
   }
 }
@@ -598,10 +654,12 @@ static int dgrad_strips() {
 int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
 
 // Grid of the persistent 4-strip dgrad: MNIST_AMD_DGRAD_PERSIST = 0 -> per-item kernel (returns 0),
-// unset / 1 -> 2 x CUs workgroups when that covers the 4B items in at most two rounds (B <= 256 on
-// 256 CUs; measured B = 200: 80.4 vs 82.6 us/step), else the per-item kernel (B = 8192: 1.44 vs
-// 1.35 ms/step - at large B independent per-item workgroups overlap one's staging with the other's
-// MFMAs better than the item loop does); N > 1 -> min(4B, N) workgroups.  Read per call (host).
+// unset / 1 -> 2 x CUs workgroups (measured B = 200: 80.4 vs 82.6 us/step; B = 8192, since the
+// branch-free conv1-gradient epilogue: 0.980 vs 1.062 ms/step - the item loop stages the conv2
+// weights once and hides the next item's record / input-row chain under the MFMA loop, where the
+// per-item kernel waits out that chain in every workgroup; round 2 measured the per-item kernel
+// faster at 8192, 1.35 vs 1.44, with the old epilogue); N > 1 -> min(4B, N) workgroups.  Read per
+// call (host).
 static int dgrad_persist_grid(int B) {
   const char* e = getenv("MNIST_AMD_DGRAD_PERSIST");
   const int v = e ? atoi(e) : 1;
@@ -615,7 +673,6 @@ static int dgrad_persist_grid(int B) {
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
     g = 2 * cus;
-    if (4 * B > 2 * g) return 0;
   }
   return g < 4 * B ? g : 4 * B;
 }
