@@ -37,6 +37,16 @@ __device__ int g_dg_stagger;                     // persistent form: ticks the s
 #else
 #define DG_MARK(i)
 #endif
+// Phase timing of conv2_wgrad_kernel (tools/wgrad_phase.hip: MNIST_WGRAD_PHASE_TIMING).
+#ifdef MNIST_WGRAD_PHASE_TIMING
+constexpr int kWgPhaseMaxWG = 1024;
+__device__ uint64_t g_wg_phase[kWgPhaseMaxWG * 8];
+#define WG_MARK(i)                                                                             \
+  if (threadIdx.x == 0 && blockIdx.x < kWgPhaseMaxWG)                                         \
+    g_wg_phase[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();
+#else
+#define WG_MARK(i)
+#endif
 
 namespace {
 constexpr int DG_ROWS = 7;                              // conv1-output rows per dgrad WG (4 strips)
@@ -83,6 +93,22 @@ __device__ __forceinline__ uint4 dyc_expand(uint4 g, uint2 route, int q) {
   // per route word (4 channels): 0xFF in the bytes whose code == q (SWAR zero-byte test), then
   // v_perm_b32 doubles each byte into the 16-bit lane of its bf16
   const uint32_t rep = (uint32_t)q * 0x01010101u;
+  uint32_t keep[2];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const uint32_t x = (w ? route.y : route.x) ^ rep;                        // 0 byte <=> match
+    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 <=> no match
+    keep[w] = ~((nz >> 7) * 0xFFu);                                            // 0xFF <=> match
+  }
+  uint4 o;
+  o.x = g.x & __builtin_amdgcn_perm(0u, keep[0], 0x01010000u);
+  o.y = g.y & __builtin_amdgcn_perm(0u, keep[0], 0x03030202u);
+  o.z = g.z & __builtin_amdgcn_perm(0u, keep[1], 0x01010000u);
+  o.w = g.w & __builtin_amdgcn_perm(0u, keep[1], 0x03030202u);
+  return o;
+}
+// dyc_expand with the window code pre-multiplied (rep = q * 0x01010101; q = 4 selects nothing)
+__device__ __forceinline__ uint4 dyc_expand_rep(uint4 g, uint2 route, uint32_t rep) {
   uint32_t keep[2];
 #pragma unroll
   for (int w = 0; w < 2; ++w) {
@@ -811,11 +837,13 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
   }
 
   WgradChunk k;
+  WG_MARK(0);
   if (nchunks > 0) {
     wgrad_fetch(a, r0, min(r0 + WG_CH, r1), tid, k);
     wgrad_store(smem, tid, r0, k, bsum);
   }
   __syncthreads();
+  WG_MARK(1);
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = r0 + ch * WG_CH, c1 = min(c0 + WG_CH, r1);
     const bool more = ch + 1 < nchunks;
@@ -846,9 +874,12 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
         }
       }
     }
+    if (ch == 0) { WG_MARK(2); }             // chunk 0's MFMAs issued (wave 0)
     if (more) wgrad_store(smem + ((ch + 1) & 1) * WBUF_BYTES, tid, c1, k, bsum);
     __syncthreads();
+    if (ch == 0) { WG_MARK(3); }             // chunk 1 staged (barrier)
   }
+  WG_MARK(4);
   // slab layout = MFMA-native [co-tile 4][n-tile 18][lane 64][4]: one coalesced float4 per tile
   float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
 #pragma unroll
@@ -870,6 +901,227 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
     for (int kk = 0; kk < WG_THREADS / 8; ++kk) s += red[j * WG_THREADS + kk * 8 + c8];
     out[18432 + 8 * c8 + j] = s;
   }
+  WG_MARK(5);
+}
+
+// --------------------------------------------------------------------------------------------
+// conv2_wgrad, VALU-lean form (default below the staggered threshold).  Same workgroup geometry,
+// chunk pipeline, wave tiling and slab layout as conv2_wgrad_kernel, with the VALU work that made
+// it issue-bound taken out (PMC at B = 200: ~1570 VALU instructions per wave against 133 MFMAs; a
+// wave64 VALU instruction holds its SIMD for 2-4 cycles, so VALU issue - not the MFMA pipe or the
+// LDS - set the kernel's time; tools/wgrad_phase.hip):
+//  * staging: every chunk-invariant part of a thread's three dense dy chunks (row / column inside
+//    the chunk, LDS slot, 2x2-window code) is computed once; per chunk a record offset costs a
+//    compare against the (scalar) image boundary.  Rows past the chunk are zeroed by expanding with
+//    window code 4, which matches no argmax route; a1 loads are clamped into the chunk's own rows
+//    (finite values under zero dy) instead of masked;
+//  * conv2 bias gradient on the MFMA pipe: one extra n-tile of ones, computed by the two waves
+//    whose n-group has 4 tiles (so every SIMD issues 10 + 10 or 10 + 8 MFMAs per k-step), instead
+//    of 16 VALU per staged chunk plus an LDS reduction;
+//  * MFMA loop: k-steps unrolled, the n-group a template parameter, so every fragment read is a
+//    base register + an immediate; the B-row base of each (k-step, lo/hi) lane row is precomputed
+//    once per kernel and only the image-boundary shift (52 a1 pixels) is selected per chunk.
+// The sums differ from conv2_wgrad_kernel's only in the bias (MFMA accumulation order).
+namespace {
+constexpr int WL_KS = WG_CHPX / 32;                         // 6 k-steps per full chunk
+constexpr int WL_VD = WDY_BYTES / 16 / WG_THREADS, WL_VA = (WA1_BYTES / 16 + WG_THREADS - 1) / WG_THREADS;
+// a1 tile planar by channel half ([ci / 16][pixel][16 ci], 32 B per pixel): with the k -> pixel map
+// below, lanes 0-31 of a B-fragment read take 8 consecutive pixels = all 64 banks once (the NHWC
+// tile's 64-B pixel pitch put lanes 0-3 and 8-11 on the same banks: 2-way conflicts on 10 of the
+// 14 fragment reads per k-step)
+constexpr int WL_PLANE = WG_A1ROWS * H1 * 16 * 2;            // 9984 B
+struct WlPlan {
+  int prow[WL_VD], recoff[WL_VD], dsti[WL_VD];
+  uint32_t rep[WL_VD];
+};
+struct WlChunk {
+  uint4 vd[WL_VD], va[WL_VA];
+  uint2 rt[WL_VD];
+};
+__device__ __forceinline__ void wl_plan(WlPlan& P, int tid, int r0) {
+  const int c8 = tid & 7;
+#pragma unroll
+  for (int i = 0; i < WL_VD; ++i) {
+    const int pix = (tid >> 3) + (WG_THREADS / 8) * i;
+    const int pr = pix / H2, x = pix - pr * H2;
+    P.prow[i] = pr;
+    P.recoff[i] = (x >> 1) * DYC_REC + c8 * 16;
+    P.dsti[i] = pix * 8 + (c8 ^ swz_dy(pix));
+    P.rep[i] = (uint32_t)((((r0 + pr) & 1) << 1) | (x & 1)) * 0x01010101u;
+  }
+}
+// global loads of chunk [c0, c1): records of rows past the chunk are clamped into it (zeroed at the
+// store), a1 chunks past the chunk's rows clamped to its last one (finite, only met by zero dy)
+__device__ __forceinline__ void wl_fetch(const ConvBwdArgs& a, const WlPlan& P, int tid, int c0, int c1, WlChunk& k) {
+  const int b0 = c0 / H2, y0 = c0 - b0 * H2;               // scalar
+  const uint8_t* recb = a.dyc + (int64_t)b0 * DYC_BYTES_PER_IMAGE;
+  const int c8 = tid & 7;
+#pragma unroll
+  for (int i = 0; i < WL_VD; ++i) {
+    const int t = y0 + min(P.prow[i], c1 - c0 - 1);
+    const bool nx = t >= H2;
+    const int y = nx ? t - H2 : t;
+    const int off = (nx ? (int)DYC_BYTES_PER_IMAGE : 0) + (y >> 1) * (HP * DYC_REC) + P.recoff[i];
+    k.vd[i] = *reinterpret_cast<const uint4*>(recb + off);
+    k.rt[i] = *reinterpret_cast<const uint2*>(recb + off + DYC_ROUTE - c8 * 8);
+  }
+  const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
+  const int na1 = (A1 - A0) * H1 * 4;
+  const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
+#pragma unroll
+  for (int i = 0; i < WL_VA; ++i) k.va[i] = asrc[min(tid + WG_THREADS * i, na1 - 1)];
+}
+__device__ __forceinline__ void wl_store(const WlPlan& P, unsigned char* buf, int tid, int c0, int c1, const WlChunk& k) {
+  uint4* dys = reinterpret_cast<uint4*>(buf);
+  uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
+#pragma unroll
+  for (int i = 0; i < WL_VD; ++i) {
+    const uint32_t rp = P.prow[i] < c1 - c0 ? P.rep[i] : 0x04040404u;   // code 4: no route matches -> 0
+    dys[P.dsti[i]] = dyc_expand_rep(k.vd[i], k.rt[i], rp);
+  }
+#pragma unroll
+  for (int i = 0; i < WL_VA; ++i) {
+    const int c = tid + WG_THREADS * i;              // NHWC chunk: pixel c >> 2, channels 8(c & 3)..
+    if (c < WA1_BYTES / 16) a1s[(c >> 1) & 1 ? WL_PLANE / 16 + (c >> 2) * 2 + (c & 1) : (c >> 2) * 2 + (c & 1)] = k.va[i];
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void wgrad_lean_mfma(const unsigned char* buf, int nks, int bnd, const int (&aoffb)[2][2],
+                                                const int (&tb)[WL_KS][2], const int (&rr)[WL_KS][2],
+                                                floatx4 (&acc)[2][5], floatx4 (&accb)[2]) {
+  constexpr int NT0 = NG < 2 ? 5 * NG : 10 + 4 * (NG - 2), NN = NG < 2 ? 5 : 4;
+  const unsigned char* pa[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) pa[i][h] = buf + aoffb[i][h];
+  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+#pragma unroll
+  for (int ks = 0; ks < WL_KS; ++ks) {
+    if (ks < nks) {                                       // wave-uniform
+      bf16x8 A[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        A[i] = tr_frag(reinterpret_cast<const uint16_t*>(pa[i][0] + ks * 32 * C2 * 2),
+                       reinterpret_cast<const uint16_t*>(pa[i][1] + ks * 32 * C2 * 2));
+      const unsigned char* pb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pb[h] = buf + WDY_BYTES + tb[ks][h] + (rr[ks][h] >= bnd ? 52 * 32 : 0);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        const int nt = NT0 + j, t = nt >> 1;
+        const int toffb = ((t / 3) * H1 + (t % 3)) * 32 + (nt & 1) * WL_PLANE;
+        const bf16x8 Bf = tr_frag(reinterpret_cast<const uint16_t*>(pb[0] + toffb),
+                                  reinterpret_cast<const uint16_t*>(pb[1] + toffb));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
+      }
+      if constexpr (NG == 2) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) accb[i] = mfma16x16x32(A[i], ones, accb[i]);
+      }
+    }
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int mt0 = 2 * (wave & 1), ng = wave >> 1;
+  const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
+  const int G = gridDim.x, g = blockIdx.x;
+  if (a.signal_ctr && g == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const int rows = H2 * B;
+  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
+  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
+
+  // ---- chunk-invariant staging plan (dense dy chunk c = tid + 512 i: pixel c >> 3, channels
+  // 8(c & 7)..; every chunk starts on a row of the parity of r0, so the window code is fixed)
+  WlPlan P;
+  wl_plan(P, tid, r0);
+  WlChunk k;
+  // ---- per-lane fragment bases: A (dy) rows lo / hi of each co-tile, B (a1) rows per k-step
+  // k -> pixel: k = 8 gq + j holds pixel 4 gq + j (j < 4, the "lo" read) or 16 + 4 gq + j - 4 (the
+  // "hi" read), so each read's lanes 0-31 / 32-63 take 8 consecutive pixels (A and B agree)
+  const int clo = 4 * gq + q, chi = clo + 16;
+  int aoffb[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cb = 16 * (mt0 + i) + 4 * pp;
+    aoffb[i][0] = (clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7))) * 2;
+    aoffb[i][1] = (chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7))) * 2;
+  }
+  int tb[WL_KS][2], rr[WL_KS][2];
+#pragma unroll
+  for (int ks = 0; ks < WL_KS; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = 32 * ks + (h ? chi : clo), r = p / H2;
+      rr[ks][h] = r;
+      tb[ks][h] = (p + 2 * r) * 32 + 8 * pp;              // a1 pixel p + 2r of the 26-wide tile (bytes, plane 0)
+    }
+
+  floatx4 acc[2][5], accb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    accb[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  WG_MARK(0);
+  if (nchunks > 0) {
+    wl_fetch(a, P, tid, r0, min(r0 + WG_CH, r1), k);
+    wl_store(P, smem, tid, r0, min(r0 + WG_CH, r1), k);
+  }
+  __syncthreads();
+  WG_MARK(1);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int c0 = r0 + ch * WG_CH, c1 = min(c0 + WG_CH, r1);
+    const bool more = ch + 1 < nchunks;
+    if (more) wl_fetch(a, P, tid, c1, min(c1 + WG_CH, r1), k);   // in flight under the MFMAs
+    asm volatile("" ::: "memory");    // keep the next chunk's LDS stores after the MFMA loop (the
+                                      // compiler hoisted the a1 stores - and their vmcnt waits - above it)
+    const unsigned char* buf = smem + (ch & 1) * WBUF_BYTES;
+    const int nks = ((c1 - c0) * H2 + 31) / 32;
+    const int bnd = H2 - (c0 - (c0 / H2) * H2);             // first chunk row of the next image
+    switch (ng) {                                           // wave-uniform
+      case 0: wgrad_lean_mfma<0>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
+      case 1: wgrad_lean_mfma<1>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
+      case 2: wgrad_lean_mfma<2>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
+      default: wgrad_lean_mfma<3>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
+    }
+#ifdef MNIST_WGRAD_PHASE_TIMING
+    if (ch == 0) { WG_MARK(2); }
+#endif
+    asm volatile("" ::: "memory");
+    if (more) wl_store(P, smem + ((ch + 1) & 1) * WBUF_BYTES, tid, c1, min(c1 + WG_CH, r1), k);
+    __syncthreads();
+#ifdef MNIST_WGRAD_PHASE_TIMING
+    if (ch == 0) { WG_MARK(3); }
+#endif
+  }
+  WG_MARK(4);
+  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (j < nn) {
+        const int tile = (mt0 + i) * 18 + nt0 + j;
+        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
+      }
+  // bias: column 0 of the ones-tile accumulators (every column holds the same row sums)
+  if (ng == 2 && (lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + i) + 4 * gq) = accb[i];
+  }
+  WG_MARK(5);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1093,8 +1345,15 @@ static bool wgrad_staggered(const ConvBwdArgs& a, int B) {
   if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
   return (int64_t)H2 * B >= (int64_t)4 * WG_CH * a.wgrad_groups;
 }
+// MNIST_AMD_WGRAD_LEAN=0: the previous 8-wave lockstep kernel instead of the VALU-lean one
+static bool wgrad_lean() {
+  const char* e = getenv("MNIST_AMD_WGRAD_LEAN");
+  return !(e && e[0] == '0');
+}
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  if (!wgrad_staggered(a, B))
+  if (!wgrad_staggered(a, B) && wgrad_lean())
+    hipLaunchKernelGGL(conv2_wgrad_lean_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
+  else if (!wgrad_staggered(a, B))
     hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
   else
     hipLaunchKernelGGL(conv2_wgrad_stag_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
