@@ -924,44 +924,55 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
 // The sums differ from conv2_wgrad_kernel's only in the bias (MFMA accumulation order).
 namespace {
 constexpr int WL_KS = WG_CHPX / 32;                         // 6 k-steps per full chunk
-constexpr int WL_VD = WDY_BYTES / 16 / WG_THREADS, WL_VA = (WA1_BYTES / 16 + WG_THREADS - 1) / WG_THREADS;
 // a1 tile planar by channel half ([ci / 16][pixel][16 ci], 32 B per pixel): with the k -> pixel map
 // below, lanes 0-31 of a B-fragment read take 8 consecutive pixels = all 64 banks once (the NHWC
 // tile's 64-B pixel pitch put lanes 0-3 and 8-11 on the same banks: 2-way conflicts on 10 of the
 // 14 fragment reads per k-step)
 constexpr int WL_PLANE = WG_A1ROWS * H1 * 16 * 2;            // 9984 B
-struct WlPlan {
-  int prow[WL_VD], recoff[WL_VD], dsti[WL_VD];
-  uint32_t rep[WL_VD];
+template <int NTH>
+struct WlPlanT {
+  static constexpr int VD = WDY_BYTES / 16 / NTH;
+  // record byte offset in the image row pair (x / 2, channel chunk; < 4096) | 2x2-window code << 12 |
+  // chunk row << 16
+  int rec[VD];
+  int dst0;           // LDS uint4 index of chunk 0 (chunk i: + NTH i; the dy swizzle repeats every 8 pixels)
 };
-struct WlChunk {
-  uint4 vd[WL_VD], va[WL_VA];
-  uint2 rt[WL_VD];
+template <int NTH>
+struct WlChunkT {
+  static constexpr int VD = WDY_BYTES / 16 / NTH, VA = (WA1_BYTES / 16 + NTH - 1) / NTH;
+  uint4 vd[VD], va[VA];
+  uint2 rt[VD];
 };
-__device__ __forceinline__ void wl_plan(WlPlan& P, int tid, int r0) {
+// chunk-invariant staging plan of thread tid (dense dy chunk c = tid + NTH i: pixel c >> 3, channels
+// 8(c & 7)..; every chunk of the workgroup starts on a row of the parity of r0 (chunks are 8 rows),
+// so the 2x2-window code of each pixel is fixed)
+template <int NTH>
+__device__ __forceinline__ void wl_plan(WlPlanT<NTH>& P, int tid, int r0) {
   const int c8 = tid & 7;
+  static_assert((NTH / 8) % 8 == 0, "pixel step of the chunks keeps the dy swizzle");
+  P.dst0 = (tid >> 3) * 8 + (c8 ^ swz_dy(tid >> 3));
 #pragma unroll
-  for (int i = 0; i < WL_VD; ++i) {
-    const int pix = (tid >> 3) + (WG_THREADS / 8) * i;
+  for (int i = 0; i < WlPlanT<NTH>::VD; ++i) {
+    const int pix = (tid >> 3) + (NTH / 8) * i;
     const int pr = pix / H2, x = pix - pr * H2;
-    P.prow[i] = pr;
-    P.recoff[i] = (x >> 1) * DYC_REC + c8 * 16;
-    P.dsti[i] = pix * 8 + (c8 ^ swz_dy(pix));
-    P.rep[i] = (uint32_t)((((r0 + pr) & 1) << 1) | (x & 1)) * 0x01010101u;
+    static_assert((HP - 1) * DYC_REC + 7 * 16 < 4096, "record offset below the code bits");
+    P.rec[i] = (x >> 1) * DYC_REC + c8 * 16 + (((((r0 + pr) & 1) << 1) | (x & 1)) << 12) + (pr << 16);
   }
 }
 // global loads of chunk [c0, c1): records of rows past the chunk are clamped into it (zeroed at the
 // store), a1 chunks past the chunk's rows clamped to its last one (finite, only met by zero dy)
-__device__ __forceinline__ void wl_fetch(const ConvBwdArgs& a, const WlPlan& P, int tid, int c0, int c1, WlChunk& k) {
+template <int NTH>
+__device__ __forceinline__ void wl_fetch(const ConvBwdArgs& a, const WlPlanT<NTH>& P, int tid, int c0, int c1,
+                                         WlChunkT<NTH>& k) {
   const int b0 = c0 / H2, y0 = c0 - b0 * H2;               // scalar
   const uint8_t* recb = a.dyc + (int64_t)b0 * DYC_BYTES_PER_IMAGE;
   const int c8 = tid & 7;
 #pragma unroll
-  for (int i = 0; i < WL_VD; ++i) {
-    const int t = y0 + min(P.prow[i], c1 - c0 - 1);
+  for (int i = 0; i < WlChunkT<NTH>::VD; ++i) {
+    const int t = y0 + min(P.rec[i] >> 16, c1 - c0 - 1);
     const bool nx = t >= H2;
     const int y = nx ? t - H2 : t;
-    const int off = (nx ? (int)DYC_BYTES_PER_IMAGE : 0) + (y >> 1) * (HP * DYC_REC) + P.recoff[i];
+    const int off = (nx ? (int)DYC_BYTES_PER_IMAGE : 0) + (y >> 1) * (HP * DYC_REC) + (P.rec[i] & 0xFFF);
     k.vd[i] = *reinterpret_cast<const uint4*>(recb + off);
     k.rt[i] = *reinterpret_cast<const uint2*>(recb + off + DYC_ROUTE - c8 * 8);
   }
@@ -969,33 +980,71 @@ __device__ __forceinline__ void wl_fetch(const ConvBwdArgs& a, const WlPlan& P, 
   const int na1 = (A1 - A0) * H1 * 4;
   const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
 #pragma unroll
-  for (int i = 0; i < WL_VA; ++i) k.va[i] = asrc[min(tid + WG_THREADS * i, na1 - 1)];
+  for (int i = 0; i < WlChunkT<NTH>::VA; ++i) k.va[i] = asrc[min(tid + NTH * i, na1 - 1)];
 }
-__device__ __forceinline__ void wl_store(const WlPlan& P, unsigned char* buf, int tid, int c0, int c1, const WlChunk& k) {
+template <int NTH>
+__device__ __forceinline__ void wl_store(const WlPlanT<NTH>& P, unsigned char* buf, int tid, int c0, int c1,
+                                         const WlChunkT<NTH>& k) {
   uint4* dys = reinterpret_cast<uint4*>(buf);
   uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
 #pragma unroll
-  for (int i = 0; i < WL_VD; ++i) {
-    const uint32_t rp = P.prow[i] < c1 - c0 ? P.rep[i] : 0x04040404u;   // code 4: no route matches -> 0
-    dys[P.dsti[i]] = dyc_expand_rep(k.vd[i], k.rt[i], rp);
+  for (int i = 0; i < WlChunkT<NTH>::VD; ++i) {
+    const uint32_t code = (P.rec[i] >> 16) < c1 - c0 ? ((uint32_t)P.rec[i] >> 12) & 3u : 4u;   // 4: no route matches -> 0
+    const uint32_t rp = code * 0x01010101u;
+    dys[P.dst0 + NTH * i] = dyc_expand_rep(k.vd[i], k.rt[i], rp);
   }
 #pragma unroll
-  for (int i = 0; i < WL_VA; ++i) {
-    const int c = tid + WG_THREADS * i;              // NHWC chunk: pixel c >> 2, channels 8(c & 3)..
+  for (int i = 0; i < WlChunkT<NTH>::VA; ++i) {
+    const int c = tid + NTH * i;                     // NHWC chunk: pixel c >> 2, channels 8(c & 3)..
     if (c < WA1_BYTES / 16) a1s[(c >> 1) & 1 ? WL_PLANE / 16 + (c >> 2) * 2 + (c & 1) : (c >> 2) * 2 + (c & 1)] = k.va[i];
   }
 }
+// per-lane fragment bases.  k -> pixel: k = 8 gq + j holds pixel 4 gq + j (j < 4, the "lo" read) or
+// 16 + 4 gq + j - 4 (the "hi" read), so each read's lanes 0-31 / 32-63 take 8 consecutive pixels
+// (A and B agree).  A: dy rows lo / hi of co-tiles mt0, mt0 + 1 (bytes); B: plane-0 byte offset of the
+// a1 pixel under each (k-step, lo / hi) lane row, before the image-boundary shift, and its dy row
+struct WlFrag {
+  int aoffb[2];       // co-tiles mt0, mt0 + 1, lo row (the hi row, pixel + 16, is + 2048 B: same swizzle)
+  uint32_t tb[WL_KS / 2][2];   // B pixel byte offsets (< 2^13) of k-steps 2m (low half) and 2m + 1
+  int c[2];           // the lane's lo / hi pixel inside a k-step: row of pixel 32 ks + c = (32 ks + c) / 24
+  __device__ __forceinline__ int tbo(int ks, int h) const { return (int)((tb[ks >> 1][h] >> (16 * (ks & 1))) & 0xFFFFu); }
+};
+__device__ __forceinline__ void wl_frag(WlFrag& F, int lane, int mt0) {
+  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int clo = 4 * gq + q, chi = clo + 16;
+  F.c[0] = clo;
+  F.c[1] = chi;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cb = 16 * (mt0 + i) + 4 * pp;
+    F.aoffb[i] = (clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7))) * 2;
+  }
+#pragma unroll
+  for (int m = 0; m < WL_KS / 2; ++m)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = 32 * (2 * m + e) + (h ? chi : clo), r = p / H2;
+        v |= (uint32_t)((p + 2 * r) * 32 + 8 * pp) << (16 * e);   // a1 pixel p + 2r of the 26-wide tile
+      }
+      F.tb[m][h] = v;
+    }
+}
 
-template <int NG>
-__device__ __forceinline__ void wgrad_lean_mfma(const unsigned char* buf, int nks, int bnd, const int (&aoffb)[2][2],
-                                                const int (&tb)[WL_KS][2], const int (&rr)[WL_KS][2],
-                                                floatx4 (&acc)[2][5], floatx4 (&accb)[2]) {
-  constexpr int NT0 = NG < 2 ? 5 * NG : 10 + 4 * (NG - 2), NN = NG < 2 ? 5 : 4;
+// MFMA loop of one staged chunk: n-tiles NT0..NT0+NN-1 of co-tiles mt0, mt0+1 (acc[i][j]); BIAS bit i:
+// also accumulate co-tile mt0+i against a tile of ones (the conv2 bias gradient, every column equal)
+// (NB = 1: the one bias tile goes to accb[0]).  A lane row is past the image boundary when its dy row
+// (32 ks + c) / 24 >= bnd, i.e. c >= 24 bnd - 32 ks (a scalar per k-step)
+template <int NT0, int NN, int BIAS, int NJ, int NB>
+__device__ __forceinline__ void wl_mfma(const unsigned char* buf, int nks, int bnd, const WlFrag& F,
+                                        floatx4 (&acc)[2][NJ], floatx4 (&accb)[NB]) {
   const unsigned char* pa[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) pa[i][h] = buf + aoffb[i][h];
+    for (int h = 0; h < 2; ++h) pa[i][h] = buf + F.aoffb[i] + h * 16 * C2 * 2;
   const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
   const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
 #pragma unroll
@@ -1008,7 +1057,7 @@ __device__ __forceinline__ void wgrad_lean_mfma(const unsigned char* buf, int nk
                        reinterpret_cast<const uint16_t*>(pa[i][1] + ks * 32 * C2 * 2));
       const unsigned char* pb[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) pb[h] = buf + WDY_BYTES + tb[ks][h] + (rr[ks][h] >= bnd ? 52 * 32 : 0);
+      for (int h = 0; h < 2; ++h) pb[h] = buf + WDY_BYTES + F.tbo(ks, h) + (F.c[h] >= H2 * bnd - 32 * ks ? 52 * 32 : 0);
 #pragma unroll
       for (int j = 0; j < NN; ++j) {
         const int nt = NT0 + j, t = nt >> 1;
@@ -1017,20 +1066,26 @@ __device__ __forceinline__ void wgrad_lean_mfma(const unsigned char* buf, int nk
                                   reinterpret_cast<const uint16_t*>(pb[1] + toffb));
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
+        // NN = 9 (staggered form): at most 3 B fragments in flight, which keeps the kernel at
+        // <= 224 VGPRs (two waves per SIMD then leave 64 registers a lane for the comm stream's fc
+        // Adadelta waves, 61 VGPRs; at 250 they could not co-reside and the overlapped update was held
+        // back until wgrad ended: B = 8192 0.986 -> 1.051 ms/step)
+        if (NN == 9 && j % 3 == 2) __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (NG == 2) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) accb[i] = mfma16x16x32(A[i], ones, accb[i]);
-      }
+      for (int i = 0; i < 2; ++i)
+        if (BIAS & (1 << i)) accb[NB == 1 ? 0 : i] = mfma16x16x32(A[i], ones, accb[NB == 1 ? 0 : i]);
     }
   }
 }
+
 }  // namespace
 
 __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArgs a, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  // 8 waves = 2 co-tile pairs x 4 groups of the 18 (tap, ci-half) n-tiles (5, 5, 4, 4); the two
+  // waves of group 2 also carry the bias tile (10 MFMAs per k-step like groups 0 and 1)
   const int mt0 = 2 * (wave & 1), ng = wave >> 1;
   const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
   const int G = gridDim.x, g = blockIdx.x;
@@ -1040,32 +1095,11 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
   const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
   const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
 
-  // ---- chunk-invariant staging plan (dense dy chunk c = tid + 512 i: pixel c >> 3, channels
-  // 8(c & 7)..; every chunk starts on a row of the parity of r0, so the window code is fixed)
-  WlPlan P;
+  WlPlanT<WG_THREADS> P;
   wl_plan(P, tid, r0);
-  WlChunk k;
-  // ---- per-lane fragment bases: A (dy) rows lo / hi of each co-tile, B (a1) rows per k-step
-  // k -> pixel: k = 8 gq + j holds pixel 4 gq + j (j < 4, the "lo" read) or 16 + 4 gq + j - 4 (the
-  // "hi" read), so each read's lanes 0-31 / 32-63 take 8 consecutive pixels (A and B agree)
-  const int clo = 4 * gq + q, chi = clo + 16;
-  int aoffb[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int cb = 16 * (mt0 + i) + 4 * pp;
-    aoffb[i][0] = (clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7))) * 2;
-    aoffb[i][1] = (chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7))) * 2;
-  }
-  int tb[WL_KS][2], rr[WL_KS][2];
-#pragma unroll
-  for (int ks = 0; ks < WL_KS; ++ks)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int p = 32 * ks + (h ? chi : clo), r = p / H2;
-      rr[ks][h] = r;
-      tb[ks][h] = (p + 2 * r) * 32 + 8 * pp;              // a1 pixel p + 2r of the 26-wide tile (bytes, plane 0)
-    }
-
+  WlChunkT<WG_THREADS> k;
+  WlFrag F;
+  wl_frag(F, lane, mt0);
   floatx4 acc[2][5], accb[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1084,21 +1118,18 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
     const int c0 = r0 + ch * WG_CH, c1 = min(c0 + WG_CH, r1);
     const bool more = ch + 1 < nchunks;
     if (more) wl_fetch(a, P, tid, c1, min(c1 + WG_CH, r1), k);   // in flight under the MFMAs
-    asm volatile("" ::: "memory");    // keep the next chunk's LDS stores after the MFMA loop (the
-                                      // compiler hoisted the a1 stores - and their vmcnt waits - above it)
     const unsigned char* buf = smem + (ch & 1) * WBUF_BYTES;
     const int nks = ((c1 - c0) * H2 + 31) / 32;
     const int bnd = H2 - (c0 - (c0 / H2) * H2);             // first chunk row of the next image
     switch (ng) {                                           // wave-uniform
-      case 0: wgrad_lean_mfma<0>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
-      case 1: wgrad_lean_mfma<1>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
-      case 2: wgrad_lean_mfma<2>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
-      default: wgrad_lean_mfma<3>(buf, nks, bnd, aoffb, tb, rr, acc, accb); break;
+      case 0: wl_mfma<0, 5, 0>(buf, nks, bnd, F, acc, accb); break;
+      case 1: wl_mfma<5, 5, 0>(buf, nks, bnd, F, acc, accb); break;
+      case 2: wl_mfma<10, 4, 3>(buf, nks, bnd, F, acc, accb); break;
+      default: wl_mfma<14, 4, 0>(buf, nks, bnd, F, acc, accb); break;
     }
 #ifdef MNIST_WGRAD_PHASE_TIMING
     if (ch == 0) { WG_MARK(2); }
 #endif
-    asm volatile("" ::: "memory");
     if (more) wl_store(P, smem + ((ch + 1) & 1) * WBUF_BYTES, tid, c1, min(c1 + WG_CH, r1), k);
     __syncthreads();
 #ifdef MNIST_WGRAD_PHASE_TIMING
@@ -1119,9 +1150,104 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
   if (ng == 2 && (lane & 15) == 0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + i) + 4 * gq) = accb[i];
+      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + i) + 4 * (lane >> 4)) = accb[i];
   }
   WG_MARK(5);
+}
+
+// conv2_wgrad, staggered halves (B >= 342), VALU-lean: conv2_wgrad_stag_kernel's schedule (two
+// 4-wave halves alternating MFMA and staging phases on alternate chunks, half 1 handing its sums to
+// half 0 at the end) on the lean staging plan, fragment bases and planar a1 tile of
+// conv2_wgrad_lean_kernel.  Each wave carries one bias tile (co-tile mt0 + hw/2: 19 MFMAs per
+// k-step on every wave).
+// <= 224 VGPRs: two waves per SIMD then leave 64 registers a lane, so the comm stream's fc Adadelta
+// waves (61 VGPRs) stay co-resident under it (at 250 they could not, and the overlapped update was
+// held back until wgrad ended: B = 8192 0.986 -> 1.051 ms/step)
+__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdArgs a, int B) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int half = wave >> 2, hw = wave & 3, htid = tid & 255;
+  const int mt0 = 2 * (hw & 1), nt0 = 9 * (hw >> 1);
+  const int G = gridDim.x, g = blockIdx.x;
+  if (a.signal_ctr && g == 0 && tid == 0)
+    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  const int rows = H2 * B;
+  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
+  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
+
+  floatx4 acc[2][9], accb[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  WlPlanT<256> P;
+  wl_plan(P, htid, r0);
+  WlChunkT<256> k;
+  WlFrag F;
+  wl_frag(F, lane, mt0);
+  auto chunk_lo = [&](int ch) { return r0 + ch * WG_CH; };
+  auto chunk_hi = [&](int ch) { return min(r0 + (ch + 1) * WG_CH, r1); };
+  unsigned char* mybuf = smem + half * WBUF_BYTES;
+
+  // prologue: half 0 stages chunk 0 and prefetches chunk 2; half 1 prefetches chunk 1
+  if (half == 0) {
+    if (nchunks > 0) {
+      wl_fetch(a, P, htid, chunk_lo(0), chunk_hi(0), k);
+      wl_store(P, mybuf, htid, chunk_lo(0), chunk_hi(0), k);
+    }
+    if (nchunks > 2) wl_fetch(a, P, htid, chunk_lo(2), chunk_hi(2), k);
+  } else if (nchunks > 1) {
+    wl_fetch(a, P, htid, chunk_lo(1), chunk_hi(1), k);
+  }
+  __syncthreads();
+  for (int ph = 0; ph < nchunks; ++ph) {
+    if ((ph & 1) == half) {                             // MFMAs of chunk ph (half-uniform)
+      const int c0 = chunk_lo(ph), c1 = chunk_hi(ph);
+      const int nks = ((c1 - c0) * H2 + 31) / 32;
+      const int bnd = H2 - (c0 - (c0 / H2) * H2);
+      switch (hw) {                                     // wave-uniform
+        case 0: wl_mfma<0, 9, 1>(mybuf, nks, bnd, F, acc, accb); break;
+        case 1: wl_mfma<0, 9, 1>(mybuf, nks, bnd, F, acc, accb); break;
+        case 2: wl_mfma<9, 9, 2>(mybuf, nks, bnd, F, acc, accb); break;
+        default: wl_mfma<9, 9, 2>(mybuf, nks, bnd, F, acc, accb); break;
+      }
+    } else if (ph + 1 < nchunks) {                      // stage chunk ph+1, prefetch chunk ph+3
+      wl_store(P, mybuf, htid, chunk_lo(ph + 1), chunk_hi(ph + 1), k);
+      if (ph + 3 < nchunks) wl_fetch(a, P, htid, chunk_lo(ph + 3), chunk_hi(ph + 3), k);
+    }
+    __syncthreads();
+  }
+  // half 1 -> half 0 through LDS ([hw][i][j][lane] float4 + [hw][lane] bias), half 0 adds in fixed order
+  floatx4* xch = reinterpret_cast<floatx4*>(smem);
+  floatx4* xb = xch + 4 * 18 * 64;
+  static_assert((4 * 18 * 64 + 4 * 64) * 16 <= WG_LDS, "accumulator exchange fits the chunk buffers");
+  const int bi = hw >> 1;                               // this wave's bias tile: co-tile mt0 + bi
+  const floatx4 mb = accb[0];
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) xch[((hw * 2 + i) * 9 + j) * 64 + lane] = acc[i][j];
+    xb[hw * 64 + lane] = mb;
+  }
+  __syncthreads();
+  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
+  if (half == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const floatx4 o = xch[((hw * 2 + i) * 9 + j) * 64 + lane];
+        const floatx4 v = {acc[i][j][0] + o[0], acc[i][j][1] + o[1], acc[i][j][2] + o[2], acc[i][j][3] + o[3]};
+        const int tile = (mt0 + i) * 18 + nt0 + j;
+        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = v;
+      }
+    if ((lane & 15) == 0) {
+      const floatx4 o = xb[hw * 64 + lane];
+      const floatx4 v = {mb[0] + o[0], mb[1] + o[1], mb[2] + o[2], mb[3] + o[3]};
+      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + bi) + 4 * (lane >> 4)) = v;
+    }
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1345,7 +1471,7 @@ static bool wgrad_staggered(const ConvBwdArgs& a, int B) {
   if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
   return (int64_t)H2 * B >= (int64_t)4 * WG_CH * a.wgrad_groups;
 }
-// MNIST_AMD_WGRAD_LEAN=0: the previous 8-wave lockstep kernel instead of the VALU-lean one
+// MNIST_AMD_WGRAD_LEAN=0: the previous lockstep / staggered kernels instead of the VALU-lean ones
 static bool wgrad_lean() {
   const char* e = getenv("MNIST_AMD_WGRAD_LEAN");
   return !(e && e[0] == '0');
@@ -1353,6 +1479,8 @@ static bool wgrad_lean() {
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   if (!wgrad_staggered(a, B) && wgrad_lean())
     hipLaunchKernelGGL(conv2_wgrad_lean_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
+  else if (wgrad_lean())
+    hipLaunchKernelGGL(conv2_wgrad_lstag_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
   else if (!wgrad_staggered(a, B))
     hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
   else

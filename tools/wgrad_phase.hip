@@ -3,7 +3,8 @@
 // prints per-phase medians over workgroups plus the kernel's event time (synthetic records + a1).
 // build: hipcc -x hip --offload-arch=gfx950 -O3 -fno-slp-vectorize -Icsrc/kernels tools/wgrad_phase.hip -o tools/wgrad_phase.bin
 // usage: tools/wgrad_phase.bin [B [G [FORM]]]   (G = workgroups, 0 = conv_wgrad_groups(B); FORM 0: the
-//        8-wave lockstep kernel, 1: conv2_wgrad_stag_kernel (event time only), 2: the VALU-lean kernel)
+//        8-wave lockstep kernel, 1: conv2_wgrad_stag_kernel (event time only), 2: the VALU-lean kernel,
+//        3: the VALU-lean staggered kernel (event time only))
 #define MNIST_WGRAD_PHASE_TIMING 1
 #ifndef WGRAD_SRC
 #define WGRAD_SRC "../csrc/kernels/conv_bwd.hip"
@@ -27,8 +28,8 @@ int main(int argc, char** argv) {
   using namespace mnist;
   const int B = argc > 1 ? atoi(argv[1]) : 200;
   const int G = argc > 2 && atoi(argv[2]) > 0 ? atoi(argv[2]) : conv_wgrad_groups(B);
-  const int form = argc > 3 ? atoi(argv[3]) : 0;   // 0 plain, 1 staggered, 2 lean
-  const bool stag = form == 1;
+  const int form = argc > 3 ? atoi(argv[3]) : 0;   // 0 plain, 1 staggered, 2 lean, 3 lean staggered
+  const bool stag = form == 1 || form == 3;
   if (G > kWgPhaseMaxWG || G < 1) { printf("G out of range (max %d)\n", kWgPhaseMaxWG); return 1; }
   std::vector<uint8_t> rec((size_t)B * DYC_BYTES_PER_IMAGE);
   for (size_t i = 0; i < rec.size(); ++i) {
@@ -41,7 +42,8 @@ int main(int argc, char** argv) {
   ConvBwdArgs a{};
   a.dyc = dyc; a.a1 = a1; a.w2part = w2part; a.grad_scale = 1.0f; a.wgrad_groups = G;
   auto launch = [&] {
-    if (stag) hipLaunchKernelGGL(conv2_wgrad_stag_kernel, dim3(G), dim3(WG_THREADS), 0, nullptr, a, B);
+    if (form == 3) hipLaunchKernelGGL(conv2_wgrad_lstag_kernel, dim3(G), dim3(WG_THREADS), 0, nullptr, a, B);
+    else if (stag) hipLaunchKernelGGL(conv2_wgrad_stag_kernel, dim3(G), dim3(WG_THREADS), 0, nullptr, a, B);
     else if (form == 2) hipLaunchKernelGGL(conv2_wgrad_lean_kernel, dim3(G), dim3(WG_THREADS), 0, nullptr, a, B);
     else hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(G), dim3(WG_THREADS), 0, nullptr, a, B);
   };
@@ -56,7 +58,7 @@ int main(int argc, char** argv) {
   float ms = 0; CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= kReps;
   if (stag) {
-    printf("B=%d  conv2_wgrad_stag_kernel G=%d: %.2f us (events, mean of %d back-to-back)\n", B, G, ms * 1000, kReps);
+    printf("B=%d  %s G=%d: %.2f us (events, mean of %d back-to-back)\n", B, form == 3 ? "conv2_wgrad_lstag_kernel" : "conv2_wgrad_stag_kernel", G, ms * 1000, kReps);
     return 0;
   }
   std::vector<uint64_t> t((size_t)G * 8);
