@@ -123,6 +123,29 @@ __device__ __forceinline__ uint4 dyc_expand_rep(uint4 g, uint2 route, uint32_t r
   o.w = g.w & __builtin_amdgcn_perm(0u, keep[1], 0x03030202u);
   return o;
 }
+// dyc_expand for all four window pixels of one chunk, sharing the route decoding: v_perm_b32's
+// sign selectors (8..11 = 0xFF if bit 15 / 31 / 47 / 63 of {src0, src1} is set) expand a match flag
+// straight into a 16-bit lane mask, so per route word the four flags only need to sit at bits 15 / 31
+// of two words: channels 0 / 2 of the word from (route << 15, route << 14) (the code's bit 0 / bit 1),
+// channels 1 / 3 from (route << 7, route << 6).  Per pixel 2 x (2 bit-ops + 2 perms + 2 ands)
+// instead of ~24 VALU; the same bits as dyc_expand (routes are 0..3).
+struct DycRoute {
+  uint32_t e0x, e1x, o0x, o1x, e0y, e1y, o0y, o1y;
+};
+__device__ __forceinline__ DycRoute dyc_route(uint2 r) {
+  return DycRoute{r.x << 15, r.x << 14, r.x << 7, r.x << 6, r.y << 15, r.y << 14, r.y << 7, r.y << 6};
+}
+template <int Q>
+__device__ __forceinline__ uint32_t dyc_flag(uint32_t b0, uint32_t b1) {
+  return ((Q & 1) ? b0 : ~b0) & ((Q & 2) ? b1 : ~b1);
+}
+template <int Q>
+__device__ __forceinline__ uint4 dyc_expand_q(uint4 g, const DycRoute& R) {
+  const uint32_t mex = dyc_flag<Q>(R.e0x, R.e1x), mox = dyc_flag<Q>(R.o0x, R.o1x);
+  const uint32_t mey = dyc_flag<Q>(R.e0y, R.e1y), moy = dyc_flag<Q>(R.o0y, R.o1y);
+  return uint4{g.x & __builtin_amdgcn_perm(mex, mox, 0x08080A0Au), g.y & __builtin_amdgcn_perm(mex, mox, 0x09090B0Bu),
+               g.z & __builtin_amdgcn_perm(mey, moy, 0x08080A0Au), g.w & __builtin_amdgcn_perm(mey, moy, 0x09090B0Bu)};
+}
 __device__ __forceinline__ const uint8_t* dyc_record(const uint8_t* dyc, int b, int y, int x) {
   return dyc + (int64_t)b * DYC_BYTES_PER_IMAGE + ((y >> 1) * HP + (x >> 1)) * DYC_REC;
 }
@@ -212,12 +235,17 @@ __device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, i
       const int c8 = jb & 7, pc = (jb >> 3) % HP, pr = (jb >> 3) / HP;
       const int ly0 = 2 * (py0 + pr) - (r0 - 2);  // tile row of the window's top pixel row (-1..9)
       const bool ok = (L.okm >> k) & 1u;
+      const DycRoute R = dyc_route(L.rt[k]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int ly = ly0 + (q >> 1);
         if (ly >= 0 && ly < DG_TROWS) {
           const int row = ly * DG_PITCH + 2 * pc + (q & 1) + 2;
-          dys[row * 8 + (c8 ^ swz8(row))] = ok ? dyc_expand(L.v[k], L.rt[k], q) : z;
+          uint4 e = q == 0 ? dyc_expand_q<0>(L.v[k], R) : q == 1 ? dyc_expand_q<1>(L.v[k], R)
+                  : q == 2 ? dyc_expand_q<2>(L.v[k], R) : dyc_expand_q<3>(L.v[k], R);
+          const uint32_t okm = ok ? ~0u : 0u;           // per component (a select of the uint4 went
+          e.x &= okm; e.y &= okm; e.z &= okm; e.w &= okm;   // through scratch memory)
+          dys[row * 8 + (c8 ^ swz8(row))] = e;
         }
       }
     }
