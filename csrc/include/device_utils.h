@@ -55,6 +55,16 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* row_lo, const uint16_t
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its global
+// loads and stores.  __syncthreads() is a workgroup fence + s_barrier, and the fence drains every
+// outstanding global access (vmcnt(0)) first - a prefetch issued before it lands before anyone
+// passes.  Only where the barrier publishes LDS data (no global data passes between waves).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

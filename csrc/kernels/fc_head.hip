@@ -743,29 +743,37 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
       for (int nt = 0; nt < 4; ++nt)
         Bw[ks][nt] = ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
   }
-  for (int t = 0; t < MR; ++t) {
-    const int b0 = (bb * MR + t) * 16;
-    if (b0 >= B) break;                                // workgroup-uniform
-    // Every load of the tile is issued before the first wait: the pmask words unconditionally
-    // (clamped row, value masked after) - loads under a branch each end in vmcnt(0), which turned
-    // the tile's staging into four dependent round trips.
-    uint32_t pmv[4];
+  // The next row tile's pmask words and dz1 fragments are loaded under this tile's MFMAs and
+  // record epilogue (the tiles of a workgroup ran back to back, each paying a full HBM round trip
+  // first: role B alone 98.5 us at B = 8192), and the tile barriers are LDS-only (lds_barrier) so
+  // that prefetch stays in flight across them.
+  // Every load of a tile is unconditional (clamped row, value masked after): loads under a branch
+  // each end in vmcnt(0), which turned the tile's staging into dependent round trips.
+  uint32_t pmv[4];
+  bf16x8 Af[NH / 32];
+  auto tile_loads = [&](int b0, uint32_t (&pm)[4], bf16x8 (&af)[NH / 32]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = tid + 256 * k, bl = idx >> 6, c = idx & 63;
       const int row = b0 + bl < B ? b0 + bl : B - 1;
-      pmv[k] = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)row * NFLAT + ((s0 >> 2) * C2 + c) * 4);
+      pm[k] = *reinterpret_cast<const uint32_t*>(a.pmask + (int64_t)row * NFLAT + ((s0 >> 2) * C2 + c) * 4);
     }
-    const uint16_t* arow = a.dz1 + (int64_t)(b0 + m) * NH + 8 * kg;   // rows < Bp: zero padding rows
-    bf16x8 Af[NH / 32], Bs[CACHE_W ? 1 : NH / 32][4];
+    const int arow_b = b0 + m < Bp ? b0 + m : Bp - 1;   // rows < Bp: zero padding rows
+    const uint16_t* arow = a.dz1 + (int64_t)arow_b * NH + 8 * kg;
 #pragma unroll
-    for (int ks = 0; ks < NH / 32; ++ks) {
-      Af[ks] = ld16(arow + ks * 32);
-      if (!CACHE_W) {
+    for (int ks = 0; ks < NH / 32; ++ks) af[ks] = ld16(arow + ks * 32);
+  };
+  tile_loads(bb * MR * 16, pmv, Af);
+  for (int t = 0; t < MR; ++t) {
+    const int b0 = (bb * MR + t) * 16;
+    if (b0 >= B) break;                                // workgroup-uniform
+    bf16x8 Bs[CACHE_W ? 1 : NH / 32][4];
+    if (!CACHE_W) {
+#pragma unroll
+      for (int ks = 0; ks < NH / 32; ++ks)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           Bs[CACHE_W ? 0 : ks][nt] = ld16(a.w1t + (int64_t)((16 * nt + m) * NPOOL + s0 + wave) * NH + ks * 32 + 8 * kg);
-      }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -783,7 +791,9 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
         acc[nt] = mfma16x16x32(Af[ks], Bf, acc[nt]);
       }
     }
-    __syncthreads();
+    const int nb0 = b0 + 16;
+    if (t + 1 < MR && nb0 < B) tile_loads(nb0, pmv, Af);   // workgroup-uniform; in flight below
+    lds_barrier();
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -795,7 +805,7 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
         reinterpret_cast<uint16_t*>(rec)[c] = f2bf(v);
         rec[DYC_ROUTE + c] = (uint8_t)(mk & 3);
       }
-    __syncthreads();
+    lds_barrier();
     // 16 runs of 4 contiguous records (768 B) -> 48 x 16 B per image row, 3 per thread
     constexpr int RUN16 = 4 * DYC_REC / 16;
 #pragma unroll
@@ -806,7 +816,7 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
         dst[off] = reinterpret_cast<const uint4*>(recs)[cidx];
       }
     }
-    if (t + 1 < MR) __syncthreads();                   // pms / recs are rewritten by the next tile
+    if (t + 1 < MR) lds_barrier();                     // pms / recs are rewritten by the next tile
   }
 }
 
