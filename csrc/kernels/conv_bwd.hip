@@ -377,7 +377,7 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
 
   if constexpr (!STAG) {
     xs[tid] = dgrad_xs_value<XM>(xv);             // input rows (entries 252-255: zeros), first read below
-    __syncthreads();
+    lds_barrier();
   }
   DG_MARK(5);
 
@@ -428,7 +428,7 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
       if (t < 10) red[(wave * 32 + nt * 16 + m) * 10 + t] = dw[nt][r];
     }
   if constexpr (!STAG) {
-    __syncthreads();
+    lds_barrier();
     dgrad_red_reduce(a, strip, b, red, tid);
   }
 }
@@ -469,8 +469,8 @@ __device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int stri
   dgrad_w2d_store(smem, tid, w);
   DG_MARK(1);
   dgrad_dy_store(smem, strip, tid, L);
-  __syncthreads();
-  DG_MARK(2);
+  lds_barrier();        // LDS-only barriers in the dgrad item: the mask loads / the persistent form's
+  DG_MARK(2);           // next-item prefetch and the c1part stores stay in flight across them
   dgrad_compute<XM, kPre>(a, strip, b, smem, L.xv, mk, [] {});
   DG_MARK(4);
 }
@@ -511,13 +511,13 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs
     if (!PF && it != (int)blockIdx.x) dgrad_fetch<XM>(a, it & 3, it >> 2, step, tid, L);
     dgrad_dy_store(smem, it & 3, tid, L);
     const float xv = L.xv;
-    __syncthreads();
+    lds_barrier();
     const int nx = (it + G < n) ? it + G : it;   // clamped: the last item's prefetch is a re-read
     if constexpr (PF)
       dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
     else
       dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [] {});
-    __syncthreads();                              // the next dy store must not overtake the red reads
+    lds_barrier();                              // the next dy store must not overtake the red reads
   }
 }
 
