@@ -295,3 +295,25 @@ def test_wgrad_staggered_halves_agree(cuda_device, monkeypatch, B):
     g0, g1 = grads["0"], grads["1"]
     rel = ((g1 - g0).norm() / g0.norm()).item()
     assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("B", [200, 512])
+def test_wgrad_lean_matches_previous_kernels(cuda_device, monkeypatch, B):
+    """VALU-lean conv2_wgrad (planar a1 tile, k -> pixel remap, bias on a ones-tile MFMA; B = 512 takes
+    the lean staggered form) vs the previous kernels (MNIST_AMD_WGRAD_LEAN=0): the same conv gradients
+    up to fp32 summation order, and the lean form repeats bit for bit."""
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(31))
+    grads = {}
+    for form in ("0", "1", "1"):
+        monkeypatch.setenv("MNIST_AMD_WGRAD_LEAN", form)
+        _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=B, B=B, dropout=False)
+        t.train_epoch(1, idx)
+        t.synchronize()
+        torch.cuda.synchronize()
+        g = ms.grad.clone()
+        if form in grads:
+            assert torch.equal(grads[form], g)
+        grads[form] = g
+    g0, g1 = grads["0"], grads["1"]
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 1e-5, rel
