@@ -75,26 +75,29 @@ namespace mnist {
 // ---- epoch pre-gather (the device-side DataLoader): rows [start, start+n) of the epoch's index
 // vector -> contiguous image rows + labels, so the per-step kernels address the batch directly
 // (one load level instead of step -> index -> image).  16-B chunks, 49 per 784-B image.
+// One wave per gathered row: the row's source index is wave-uniform (one scalar load), lanes 0..48
+// copy its 49 16-B chunks.  (The flat form - one chunk per thread, row = i / 49 in 64-bit integer
+// math per thread - paid a 64-bit division and a dependent per-lane index load for every chunk.)
 __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src_u8,
                                                           const int32_t* __restrict__ src_labels,
                                                           const int32_t* __restrict__ idx, int64_t start,
                                                           int64_t n, uint8_t* __restrict__ dst_u8,
                                                           int32_t* __restrict__ dst_labels) {
   constexpr int CH = 784 / 16;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n * CH) return;
-  const int64_t r = start + i / CH;
-  const int c = (int)(i % CH);
-  const int64_t img = idx[r];
-  reinterpret_cast<uint4*>(dst_u8 + r * 784)[c] = reinterpret_cast<const uint4*>(src_u8 + img * 784)[c];
-  if (c == 0) dst_labels[r] = src_labels[img];
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n) return;                                  // wave-uniform
+  const int64_t r = start + w;
+  const int64_t img = __builtin_amdgcn_readfirstlane(idx[r]);
+  if (lane < CH)
+    reinterpret_cast<uint4*>(dst_u8 + r * 784)[lane] = reinterpret_cast<const uint4*>(src_u8 + img * 784)[lane];
+  if (lane == CH) dst_labels[r] = src_labels[img];
 }
 
 void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const int32_t* idx, int64_t start,
                         int64_t n, uint8_t* dst_u8, int32_t* dst_labels, hipStream_t s) {
   if (n <= 0) return;
-  const int64_t total = n * (784 / 16);
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src_u8, src_labels,
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src_u8, src_labels,
                      idx, start, n, dst_u8, dst_labels);
 }
 
