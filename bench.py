@@ -28,8 +28,14 @@ the run fails if they differ), and the JSON names the all-reduce actually used (
 ``--cpu`` instead measures the reference's CPU config (``mnist.py --no-cuda``, batch 64) on this
 host's CPU cores against BASELINE.md's 3,518 img/s anchor.
 
-Launch: ``python bench.py`` (1 GPU) or
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (bench.py starts its N ranks
+itself: a ``torch.distributed.run --standalone`` child job, launched before this process touches a
+GPU, whose rank 0 JSON line is re-printed), or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
+
+If any rank fails (transport setup, startup validation, a hang caught by a watchdog, a desync),
+rank 0 still prints ONE JSON line - ``value`` null, ``error`` and every rank's failure record
+(decoded error, transport, setup phases) - and the exit code is non-zero.
 """
 from __future__ import annotations
 
@@ -55,8 +61,8 @@ from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream  # noqa: 
 from pytorch_mnist_ddp_amd.engine.state import ModelState  # noqa: E402
 from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer  # noqa: E402
 from pytorch_mnist_ddp_amd.models.net import Net  # noqa: E402
-from pytorch_mnist_ddp_amd.parallel.distributed import (_max_over_ranks, broadcast_,  # noqa: E402
-                                                        create_rccl_comms, params_fingerprint_equal)
+from pytorch_mnist_ddp_amd.parallel.distributed import (_max_over_ranks, barrier,  # noqa: E402
+                                                        params_fingerprint_equal, start_rccl_comm)
 from pytorch_mnist_ddp_amd.utils.profiling import PhaseTimes  # noqa: E402
 
 METRIC = "images/sec + 20-epoch wallclock, MNIST CNN DDP at 1/2/4/8 MI355X"
@@ -164,17 +170,10 @@ def cpu_bench(steps: int, warmup: int, batch: int = 64) -> int:
 # reference README.md:55-59 (20-epoch wallclock at B=200/GPU) -> images/s = 20*60000/t
 BASELINE_WALLCLOCK = {1: 242.3, 2: 137.1, 4: 73.6}
 TRAIN_N, TEST_N, EPOCHS = 60000, 10000, 20
+_FAIL_KEY = "bench/fail"
 
 
-def _broadcast_params(tr, comm) -> None:
-    if comm is not None:
-        tr.engine.broadcast_params(0)            # framework RCCL communicator (+ shadow refresh)
-    else:
-        broadcast_(tr.ms.param, 0)               # torch.distributed (host-staged on gloo)
-        tr.engine.refresh_shadows()
-
-
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 600; --cpu: 200)")
@@ -188,8 +187,8 @@ def main() -> int:
     ap.add_argument("--force-comm", action="store_true",
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
     ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
-                    help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernel, or "
-                         "auto (time both at startup, keep the faster)")
+                    help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernels, or "
+                         "auto (validate and time both production schedules at startup, keep the faster)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (gloo + --allreduce xgmi: no RCCL, e.g. MNIST_AMD_ONE_GPU=1 rehearsals)")
     ap.add_argument("--cpu", action="store_true", help="reference CPU config (mnist.py --no-cuda, batch 64)")
@@ -197,33 +196,134 @@ def main() -> int:
                     help="skip the mnist_ddp.py child job (total_cost_time_s)")
     ap.add_argument("--no-warm-replay", dest="warm_replay", action="store_false",
                     help="do not replay the timed region's graphs once (state restored) before the warmup")
-    args = ap.parse_args()
-    if args.cpu:
-        return cpu_bench(200 if args.steps is None else args.steps, 10 if args.warmup is None else args.warmup)
-    args.steps = 600 if args.steps is None else args.steps
-    args.warmup = 50 if args.warmup is None else args.warmup
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus is not None and args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run with {args.gpus} procs",
-                  file=sys.stderr)
-            return 2
-    if os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
-        local = 0                      # one-GPU multi-rank rehearsal (gloo + xgmi only)
-    phases = PhaseTimes()              # host seconds per setup phase (JSON "setup_phases_s")
+
+# ----------------------------------------------------------------------------- self-launch
+def self_launch(args, argv) -> int:
+    """``--gpus N > 1`` without a launcher: start N ranks as a ``torch.distributed.run`` child job
+    (this process never touches a GPU - no HIP context to inherit or exec away from), forward the
+    child's output, and re-print rank 0's single JSON line (with ``launcher`` added)."""
+    n = args.gpus
+    one_gpu = os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1"
+    have = torch.cuda.device_count()          # (does not initialise HIP on this image)
+    if not one_gpu and have < n:
+        msg = (f"bench.py: --gpus {n} needs {n} visible GPUs, this node shows {have} "
+               f"(HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES); one-GPU rehearsal: MNIST_AMD_ONE_GPU=1 "
+               f"--dist-backend gloo --allreduce xgmi")
+        print(msg, file=sys.stderr, flush=True)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": n, "steps": args.steps,
+                          "warmup": args.warmup, "higher_is_better": True, "error": msg}), flush=True)
+        return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes", "1", "--nproc-per-node", str(n), os.path.abspath(__file__)] + list(argv)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+    t0 = time.perf_counter()
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env, cwd=ROOT)
+    lines = []
+    for ln in proc.stdout:                       # forwarded as it arrives (progress for long runs)
+        if ln.lstrip().startswith("{") and '"metric"' in ln:
+            lines.append(ln.strip())
+        else:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+    rc = proc.wait()
+    wall = time.perf_counter() - t0
+    out = None
+    for ln in lines:
+        try:
+            out = json.loads(ln)
+        except ValueError:
+            continue
+    if out is None:
+        out = {"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": n, "steps": args.steps,
+               "warmup": args.warmup, "higher_is_better": True,
+               "error": f"the {n}-rank child job exited with {rc} without a result line"}
+    out["launcher"] = {"kind": "bench.py self-launch (torch.distributed.run --standalone child)",
+                       "child_rc": rc, "child_wall_s": round(wall, 2)}
+    print(json.dumps(out), flush=True)
+    return rc if rc != 0 else (0 if out.get("value") is not None else 1)
+
+
+# ----------------------------------------------------------------------------- failure records
+class Diag:
+    """What a rank knows when it fails: the phase it was in, the transport, the setup seconds."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.phase = "start"
+        self.phases = PhaseTimes()
+        self.tr = None
+
+    def record(self, exc: BaseException) -> dict:
+        if getattr(exc, "setup", None) is not None:       # the trainer's phases up to the failure
+            self.phases.update(exc.setup, prefix="trainer.")
+        rec = {"rank": self.rank, "phase": self.phase, "error": f"{type(exc).__name__}: {exc}"[:4000],
+               "setup_phases_s": self.phases.rounded(3)}
+        if getattr(exc, "transport_report", None) is not None:
+            rec["transport_report"] = exc.transport_report
+        tr = self.tr
+        if tr is not None:
+            rec.update(allreduce=tr.allreduce, transport_report=tr.transport_report or None)
+            try:
+                e = tr.engine.errors()
+                rec["device_errors"] = {"handoff_timeout": bool(e[0]),
+                                        "xgmi": tr.C.Engine.describe_xgmi_error(e[1]) if e[1] else None}
+            except Exception:  # noqa: BLE001 - the device may be unusable
+                pass
+        return rec
+
+
+def _publish_failure(rec: dict, use_pg: bool) -> None:
+    if not use_pg:
+        return
+    try:
+        store = dist.distributed_c10d._get_default_store()
+        store.set(f"{_FAIL_KEY}/{rec['rank']}", json.dumps(rec))
+        from pytorch_mnist_ddp_amd.parallel.hostcomm import get_hostcomm
+        get_hostcomm().abort(f"rank {rec['rank']} failed in {rec['phase']}: {rec['error'][:300]}")
+    except Exception:  # noqa: BLE001
+        pass
+
+
+def _collect_failures(world: int, wait_s: float = 5.0) -> dict:
+    """Rank 0: every rank's published failure record (waits briefly for the others')."""
+    out = {}
+    try:
+        store = dist.distributed_c10d._get_default_store()
+    except Exception:  # noqa: BLE001
+        return out
+    t0 = time.perf_counter()
+    while True:
+        for q in range(world):
+            k = f"{_FAIL_KEY}/{q}"
+            if q not in out and store.check([k]):
+                out[q] = json.loads(store.get(k))
+        if len(out) == world or time.perf_counter() - t0 > wait_s:
+            return out
+        time.sleep(0.1)
+
+
+# ----------------------------------------------------------------------------- the rank's run
+def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None:
+    phases = diag.phases             # host seconds per setup phase (JSON "setup_phases_s")
     t_setup = time.perf_counter()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
+    pending = None
     if use_pg:
-        kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
+        diag.phase = "pg_init"
         with phases.phase("pg_init"):
-            dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank, **kw)
+            # lazy (no device_id): ProcessGroupNCCL never builds a communicator - the engine's all-reduce
+            # runs on its own RCCL communicator or the xGMI kernels, verdicts over the TCPStore
+            dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank)
+        if args.allreduce != "xgmi":       # the RCCL communicator initialises while data / model build
+            with phases.phase("rccl_comm_start"):
+                pending = start_rccl_comm(world, rank, local)
 
     B = args.batch_size
+    diag.phase = "data_model"
     with phases.phase("data_model"):
         torch.manual_seed(args.seed)
         net = Net()
@@ -234,23 +334,22 @@ def main() -> int:
         steps_per_epoch = math.ceil(len(sampler) / B)
         num_samples = max(total * B, steps_per_epoch * B)
         ms = ModelState(net, dev, lr=1.0)
-    # the RCCL communicator for the gradient all-reduce / its probe (none when the xGMI kernels are
-    # forced); a second one only on opt-in (MNIST_AMD_RCCL_COMMS=2)
-    rccl = use_pg and args.allreduce != "xgmi"
-    comm, comm2 = (None, None)
-    if rccl:
-        with phases.phase("rccl_comms"):
-            comm, comm2 = create_rccl_comms(world, rank, local)
+    comm = None
+    if pending is not None:
+        diag.phase = "rccl_comm"
+        with phases.phase("rccl_comm_wait"):
+            comm = pending.result()
+        phases.add_info("rccl_comm_init_thread_s", pending.seconds)
+    diag.phase = "trainer"
     t_tr = time.perf_counter()
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                      two_buckets=not args.single_bucket, comm2=comm2, allreduce=args.allreduce)
+                      two_buckets=not args.single_bucket, allreduce=args.allreduce)
+    diag.tr = tr
     phases.add("trainer", time.perf_counter() - t_tr)
-    if use_pg:                        # DDP construction semantics: rank-0 weights everywhere
-        with phases.phase("broadcast"):
-            _broadcast_params(tr, comm)
 
     # flat index stream = consecutive DistributedSampler epochs, full batches only
+    diag.phase = "capture"
     parts, ep = [], 1
     while sum(p.numel() for p in parts) < total * B:
         sampler.set_epoch(ep)
@@ -267,18 +366,19 @@ def main() -> int:
         # every graph the timed region replays has run once before t0 (model, optimizer and step
         # state restored bit for bit): the first timed replay pays no first-launch cost, and exactly
         # --steps steps are timed after exactly --warmup warmup steps
+        diag.phase = "warm_replay"
         with phases.phase("warm_replay"):
             first = sum(set(tr._chunks(args.steps))) if tr.use_graphs else 0   # rows the replays read
             tr.engine.gather_rows(0, min(total, max(first, args.warmup)) * B)
             tr.warm_graphs(args.steps)
-    if comm is not None:   # RCCL lazily sets up its channels on the first collective: do it untimed
-        tr.synchronize()
+    diag.phase = "warmup"
     tr.engine.gather_rows(0, args.warmup * B)
     tr.run_steps(args.warmup)
     tr.synchronize()
     if use_pg:
-        dist.barrier()
+        barrier()
     torch.cuda.synchronize()
+    diag.phase = "timed"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(tr.compute)                                   # device-side view of the same window
@@ -289,48 +389,51 @@ def main() -> int:
     tr.engine.sync_streams()
     torch.cuda.synchronize()
     if use_pg:
-        dist.barrier()
+        barrier()
     t1 = time.perf_counter()
     tr.check_errors()          # device hand-off / xGMI error flags of the timed steps (after the clock)
     elapsed = t1 - t0
-    elapsed = _max_over_ranks(elapsed, dev)
+    elapsed = _max_over_ranks(elapsed)
     final_loss = float(tr.loss_log[(total - 1) % tr.loss_log.numel()].item()) if tr.loss_log.numel() else float("nan")
     img_s = world * B * args.steps / elapsed
     # DDP correctness of the timed run: every rank must hold bitwise identical parameters
+    diag.phase = "params_in_sync"
     in_sync = True
     if use_pg:
-        in_sync = params_fingerprint_equal(ms.param, dev)
-    comm_info = {"allreduce": tr.allreduce if world > 1 or comm is not None else None,
+        in_sync = params_fingerprint_equal(ms.param)
+    comm_info = {"allreduce": tr.allreduce,
                  "rccl_world": comm.world_size if comm is not None else None,
-                 "rccl_comms": (1 if comm is not None else 0) + (1 if comm2 is not None else 0),
-                 "allreduce_probe_us": tr.allreduce_timings or None,
+                 "rccl_comms": 1 if comm is not None else 0,
+                 "allreduce_schedule_us": tr.allreduce_timings or None,
+                 "transport_report": tr.transport_report or None,
                  "xgmi_validation": tr.xgmi_validation,
                  "xgmi_ordering": tr.xgmi.ordering if tr.xgmi is not None else None,
-                 "conv_bucket_split": tr.conv_split,
                  "xgmi_grids": ({k: v for k, v in tr.xgmi.grids.items() if not k.startswith("cap")}
-                                if tr.xgmi is not None else None)}
+                                if tr.xgmi is not None else None),
+                 "schedule": ["serial", "overlap", "rccl", "xgmi"][tr.engine.schedule]}
     phases.update(tr.setup, prefix="trainer.")
 
     # ---- the README workload end to end: 20 epochs train + rank-0 eval, fresh model, on the SAME
-    # trainer (engine, graphs, communicators, all-reduce choice and validation reused, state reset)
+    # trainer (engine, graphs, communicators, transport choice and validation reused, state reset)
     wall = None
     acc = None
     desync_epoch = None
     if args.full_run and rank == 0:
         tr.evaluate()         # untimed, like the training kernels above: load the eval kernels' code
     if args.full_run:
+        diag.phase = "full_run"
         from pytorch_mnist_ddp_amd.parallel.ddp import params_fingerprint
         torch.manual_seed(args.seed)
         tr.reset_model(Net())
         if use_pg:
-            _broadcast_params(tr, comm)
+            tr.broadcast_params()
         fps = []
         if use_pg:
             with torch.cuda.stream(tr.compute):
                 params_fingerprint([ms.param])      # load its kernels' code outside the timed window
         tr.synchronize()
         if use_pg:
-            dist.barrier()
+            barrier()
         torch.cuda.synchronize()
         w0 = time.perf_counter()
         sampler.set_epoch(1)
@@ -349,19 +452,17 @@ def main() -> int:
                 acc = correct / max(1, n)
         tr.synchronize()
         if use_pg:
-            dist.barrier()
+            barrier()
         w1 = time.perf_counter()
         wall = w1 - w0
-        wall = _max_over_ranks(wall, dev)
+        wall = _max_over_ranks(wall)
         if use_pg:                                       # which epoch (if any) first desynced
-            mine = torch.stack(fps)
-            allv = [torch.zeros_like(mine) for _ in range(world)]
-            if dist.get_backend() != "nccl":
-                mine = mine.cpu()
-                allv = [v.cpu() for v in allv]
-            dist.all_gather(allv, mine)
+            from pytorch_mnist_ddp_amd.parallel.hostcomm import get_hostcomm
+            mine = torch.stack(fps).cpu()
+            allv = get_hostcomm().all_gather_bytes(mine.numpy().tobytes())
+            per = [torch.frombuffer(bytearray(b), dtype=torch.int64).view(mine.shape) for b in allv]
             for e in range(len(fps)):
-                if any(not torch.equal(v[e], allv[0][e]) for v in allv):
+                if any(not torch.equal(v[e], per[0][e]) for v in per):
                     desync_epoch = e + 1
                     in_sync = False
                     break
@@ -369,9 +470,10 @@ def main() -> int:
     # ---- the reference's own metric, measured the reference's way (child job at the same N)
     script = None
     if args.full_run and args.script_run:
+        diag.phase = "reference_script"
         torch.cuda.synchronize()
         if use_pg:
-            dist.barrier()
+            barrier()
         if rank == 0:
             try:
                 extra = []     # non-default transport choices carry over to the child job
@@ -391,6 +493,7 @@ def main() -> int:
 
     base = BASELINE_WALLCLOCK.get(world)
     base_img_s = (EPOCHS * TRAIN_N / base) if base else None
+    out = None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -427,16 +530,66 @@ def main() -> int:
             "timed_enqueue_ms": round(1000.0 * (t_enq - t0), 3),
             "timed_device_ms": round(ev0.elapsed_time(ev1), 3),
             "setup_phases_s": phases.rounded(3),
+            "setup_info_s": phases.info or None,
         }
-        print(json.dumps(out), flush=True)
-    if use_pg:
-        dist.barrier()
-        dist.destroy_process_group()
+    diag.phase = "done"
     if not in_sync:
         where = f" (first differing epoch of the 20-epoch run: {desync_epoch})" if desync_epoch else ""
-        print(f"bench.py: DDP desync - ranks hold different parameters{where}", file=sys.stderr)
-        return 1
-    return 0
+        raise RuntimeError(f"DDP desync - ranks hold different parameters{where}")
+    return out
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.cpu:
+        return cpu_bench(200 if args.steps is None else args.steps, 10 if args.warmup is None else args.warmup)
+    args.steps = 600 if args.steps is None else args.steps
+    args.warmup = 50 if args.warmup is None else args.warmup
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
+        return 2
+    if os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
+        local = 0                      # one-GPU multi-rank rehearsal (gloo + xgmi only)
+    use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
+    diag = Diag(rank, world)
+    rc = 0
+    try:
+        out = run_rank(args, world, rank, local, diag)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+    except BaseException as e:  # noqa: BLE001 - every failure ends in one JSON line + non-zero rc
+        rec = diag.record(e)
+        print(f"bench.py rank {rank}: FAILED in {rec['phase']}: {rec['error']}", file=sys.stderr, flush=True)
+        _publish_failure(rec, use_pg and dist.is_initialized())
+        if rank == 0:
+            recs = _collect_failures(world) if (use_pg and dist.is_initialized()) else {}
+            recs[0] = rec
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                              "error": rec["error"], "failed_phase": rec["phase"],
+                              "rank_failures": {str(q): recs[q] for q in sorted(recs)}}), flush=True)
+        if getattr(e, "fatal", False):
+            # a collective stuck on the device cannot be cancelled: leave without the runtime's
+            # teardown (which would wait for it), the driver sees the exit code
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(3)
+        rc = 1
+    if use_pg and dist.is_initialized():
+        try:
+            if rc == 0:
+                barrier()
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+    return rc
 
 
 if __name__ == "__main__":

@@ -114,6 +114,12 @@ PYBIND11_MODULE(_C, m) {
   m.attr("PARAM_OFFSETS") = offs;
   m.attr("BUCKET_SPLIT") = OFF_CONV1_W;
   m.def("conv_wgrad_groups", &conv_wgrad_groups);
+  m.def("set_dgrad_grid", &set_dgrad_grid, "persistent dgrad grid override (0 = 2 x CUs; tests)");
+  m.def("set_wgrad_form", &set_wgrad_form, "wgrad form override (-1 = by batch, 0 lean, 1 staggered; tests)");
+  m.attr("SCHED_SERIAL") = (int)Engine::SERIAL;
+  m.attr("SCHED_OVERLAP") = (int)Engine::OVERLAP;
+  m.attr("SCHED_RCCL") = (int)Engine::RCCL;
+  m.attr("SCHED_XGMI") = (int)Engine::XGMI;
 
   // ---------------- per-kernel entry points ----------------
   m.def("trunk_fwd", [](uintptr_t data_u8, uintptr_t idx, int64_t idx_stride, uintptr_t state, uintptr_t w1c,
@@ -211,7 +217,14 @@ PYBIND11_MODULE(_C, m) {
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int world, int rank, int device) {
              std::string s = uid;
-             return std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device);
+             std::shared_ptr<RcclComm> c;
+             {
+               // ncclCommInitRank blocks for its bootstrap: let other Python threads run meanwhile
+               // (distributed.PendingRcclComm overlaps it with data / model / trainer setup)
+               py::gil_scoped_release nogil;
+               c = std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device);
+             }
+             return c;
            }),
            py::arg("unique_id"), py::arg("world_size"), py::arg("rank"), py::arg("device"))
       .def_static("available", &RcclComm::available)
@@ -270,6 +283,20 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("channel"), py::arg("offset"), py::arg("count"), py::arg("stream"))
       .def("error", &XgmiComm::error)
       .def("set_timeout_seconds", &XgmiComm::set_timeout_seconds)
+      .def("set_fences", &XgmiComm::set_fences)
+      .def_property_readonly("fences", &XgmiComm::fences)
+      .def("close_peers", &XgmiComm::close_peers, py::call_guard<py::gil_scoped_release>())
+      .def("mark_recyclable", &XgmiComm::mark_recyclable)
+      // rank `root`'s parameters to every rank through the IPC-mapped output buffers (DDP construction
+      // broadcast without RCCL): root stages `count` floats of `buf` into its output buffer, then -
+      // after the caller's barrier - every other rank copies them out of root's; the caller barriers
+      // again before the buffers are reused
+      .def("stage_out", [](XgmiComm& c, uintptr_t buf, int64_t count, uintptr_t stream) {
+        c.stage_out(P<const float>(buf), count, S(stream));
+      })
+      .def("read_peer_out", [](XgmiComm& c, int peer, uintptr_t buf, int64_t count, uintptr_t stream) {
+        c.read_peer_out(peer, P<float>(buf), count, S(stream));
+      })
       .def_property_readonly("connected", &XgmiComm::connected)
       .def_property_readonly("world_size", &XgmiComm::world_size)
       .def_property_readonly("rank", &XgmiComm::rank);
@@ -300,20 +327,14 @@ PYBIND11_MODULE(_C, m) {
            py::arg("buffers"), py::arg("max_batch"), py::arg("max_test_batch"), py::arg("compute_stream"),
            py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
       .def("attach_comm", &Engine::attach_comm)
-      .def("attach_comm2", &Engine::attach_comm2)
       .def("attach_xgmi", &Engine::attach_xgmi)
       .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)
       .def("set_bucket_split", &Engine::set_bucket_split)
-      .def("set_concurrent", &Engine::set_concurrent)
-      .def("set_dist_schedule", &Engine::set_dist_schedule)
+      .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("schedule", &Engine::schedule)
+      .def("reset_counters", &Engine::reset_counters, py::call_guard<py::gil_scoped_release>())
       .def("probe_stream_handoff", &Engine::probe_stream_handoff, py::arg("timeout_s") = 2.0,
            py::call_guard<py::gil_scoped_release>())
-      .def("set_fuse_fc_update", &Engine::set_fuse_fc_update)
-      .def("set_overlap_fc_update", &Engine::set_overlap_fc_update)
-      .def("set_conv_split", &Engine::set_conv_split)
-      .def("set_dgrad_update", &Engine::set_dgrad_update)
-      .def("set_side_first", &Engine::set_side_first)
-      .def("set_side_conv2", &Engine::set_side_conv2)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

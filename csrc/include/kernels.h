@@ -59,12 +59,6 @@ struct HeadArgs {
   const float* dlogp;         // module API backward: upstream grad wrt log-probs [B][10] (replaces NLL)
 };
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s);
-// fc1 + training head in one launch (B < FC1_BIG_MIN_B, fc1 MR = 2; opt-in MNIST_AMD_FUSE_HEAD=1, slower):
-// ctr / hdone = FC1_HEAD_MAX_TILES zero-initialised ints each (self re-arming), err = error flag
-constexpr int FC1_HEAD_MAX_TILES = (FC1_BIG_MIN_B + 31) / 32;   // 16
-bool fc1_head_fusable(int B);
-void launch_fc1_head_train(const uint16_t* p, const uint16_t* w1, const HeadArgs& a, int B, int Bp, int* ctr,
-                           int* hdone, int* err, hipStream_t s);
 void launch_head_eval(const HeadArgs& a, int B, hipStream_t s);
 // module API forward: log-probs with (train) or without (eval) dropout-2
 void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
@@ -75,22 +69,6 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
 // 64 argmax codes (2x2 window position, 0..3).  Dense dy[y][x][c] = (code == 2(y&1)+(x&1)) ? g : 0.
 constexpr int DYC_REC = 192, DYC_ROUTE = 128;
 constexpr int64_t DYC_BYTES_PER_IMAGE = (int64_t)NPOOL * DYC_REC;   // 27648
-
-// Single-GPU fused fc update: with param != nullptr (and an unsplit batch, B <= FC_BWD_SPLIT_ROWS)
-// the role A / C epilogues apply the Adadelta step to fc1 / fc2 the moment each gradient is final
-// (same Ada math as the optimizer kernels -> bitwise equal), so the memory-bound fc update
-// (98.4 % of the parameters) runs under role B instead of in the step tail.  w1 is rewritten in
-// place (only the next step's fc1_fwd reads it); the transposed shadow goes to w1t_out, which
-// must not be the w1t buffer role B of the same launch is reading.
-struct FcUpdate {
-  float* param;
-  float* square_avg;
-  float* acc_delta;
-  const float* lr;
-  float rho, eps, weight_decay;
-  uint16_t* w1;               // bf16 [128][9216]
-  uint16_t* w1t_out;          // bf16 [9216][128]
-};
 
 struct FcBwdArgs {
   const uint16_t* dz1;        // bf16 [Bp][128]
@@ -109,7 +87,6 @@ struct FcBwdArgs {
                               // that leaves inv_batch at 1/B would pass 1/world_size here
   float inv_batch;
   float* part;                // B > FC_BWD_SPLIT_ROWS: [fc_bwd_splits(B)][FCB_PART_STRIDE] partial fc grads
-  FcUpdate upd;               // optional fused fc Adadelta (zero-initialised = off)
   int* signal_ctr;            // optional: the launch's first workgroup adds 1 at its start (schedule-3 hand-off)
 };
 // Large batches split the batch (= K of the fc weight gradients) over fc_bwd_splits(B) groups of
@@ -124,9 +101,6 @@ constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_P
                   FCB_PART_STRIDE = (FCB_PART_LOSS + 1 + 63) / 64 * 64;
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s);   // profiling aid
-// two-stream form (B <= FC_BWD_SPLIT_ROWS): part 0 = roles C + B (dW2 / loss and the dy records the conv
-// backward needs), part 1 = role A (dW1, only the optimizer / all-reduce needs it)
-void launch_fc_bwd_part(const FcBwdArgs& a, int B, int Bp, int part, hipStream_t s);
 
 struct ConvBwdArgs {
   const uint8_t* dyc;         // compact un-pooled gradient (written by fc_bwd role B)
@@ -145,16 +119,18 @@ struct ConvBwdArgs {
   int wgrad_groups;           // G
   const float* xin;           // optional fp32 [B][784] input (module API), replaces data_u8/idx
   int* signal_ctr;            // optional: conv2_wgrad / conv2_dgrad add 1 at kernel start (schedule-3 hand-offs)
-  // optional [C1_PRE_SLABS][320]: when set, launch_conv_dgrad(_update) pre-reduces the 4B conv1
+  // optional [C1_PRE_SLABS][320]: when set, launch_conv_dgrad pre-reduces the 4B conv1
   // partials into C1_PRE_SLABS fixed-order group sums and the conv reduce reads those (large B:
   // 20 reduce workgroups walking 4B slabs is a dependent-load chain, 81 us at B = 8192)
   float* c1red;
   int c1_rows;                // conv1 partial rows the dgrad launch writes: conv_dgrad_c1_rows(B)
 };
-// 4B (4 strips of 7 rows per image, 2 workgroups per CU) or 3B (3 strips of 9/9/8 rows, conv2
-// weights read from L2 instead of LDS: 3 workgroups per CU, one round at B <= 256; opt-in
-// MNIST_AMD_DGRAD3=1, slower: see docs/PERF_NOTES.md)
+// 4B: 4 strips of 7 rows per image, items of the persistent dgrad (2 workgroups per CU)
 int conv_dgrad_c1_rows(int B);
+// test / tuning hooks (host globals, read at enqueue): persistent dgrad grid (0 = 2 x CUs) and the
+// wgrad form (-1 = by batch, 0 = lean lockstep halves, 1 = staggered halves)
+void set_dgrad_grid(int n);
+void set_wgrad_form(int f);
 constexpr int C1_PRE_SLABS = 256;
 constexpr int C1_PRE_MIN_SLABS = 1024;    // engine: pre-reduce when c1_rows exceeds this
 int conv_wgrad_groups(int B);
@@ -162,11 +138,6 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 wgrad + bias partials
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s);
-struct AdadeltaArgs;
-// single-GPU step: conv2_dgrad's 4B workgroups followed, in the same launch, by the conv2 slab reduce
-// + conv2 Adadelta update (RED_W2_PARTS workgroups filling the slots dgrad's last partial round
-// leaves idle).  u.w2d must not alias c.w2d (dgrad reads the step's shadow while the update writes)
-void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s);
 
 // ---------------- optimizer ----------------
 struct AdadeltaArgs {
@@ -189,9 +160,8 @@ struct AdadeltaArgs {
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
 void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
-// conv gradient slab reduce + the whole Adadelta update in one launch (single-GPU step tail);
-// conv_only when fc_bwd already applied the fc update (FcBwdArgs::upd)
-void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s);
+// conv gradient slab reduce + the whole Adadelta update in one launch (serial single-GPU step tail)
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 // conv-only form restricted to reduce parts [lo, hi) (conv_grad_reduce.h partition)
 void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s);
 // Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
@@ -223,7 +193,7 @@ struct XgmiArgs {
   int* err;                          // local error flag (timeout)
   int world, rank;
   int64_t nvec;                      // bucket length in float4s
-  uint64_t timeout_ticks;            // s_memrealtime ticks (100 MHz)
+  const uint64_t* timeout_ticks;     // device: stage-wait timeout, s_memrealtime ticks (100 MHz)
   // optional fused Adadelta (conv bucket): with fuse_ada, phase 2 applies the update to every element
   // it gathers (flat index ada_base + bucket index; grad = the reduced values), refreshes the conv2
   // bf16 shadows and advances ada.state_inc->step - the bucket's separate update launch disappears

@@ -118,9 +118,8 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
 // conv-gradient slab reduction, whose workgroups apply the update to each conv parameter as soon as
 // its gradient is final (no grad round trip, no extra kernel boundary; both halves are memory-
 // bound and overlap).  Same per-element math as the two-kernel path, so results are bitwise equal.
-// conv_only: the fc parameters were already updated by fc_bwd's fused epilogue (FcBwdArgs::upd).
-// conv_only: reduce parts [bid0, bid0 + grid) only (the conv2 parts may already have run inside the
-// dgrad launch, launch_conv_dgrad_update)
+// conv_only: reduce + update parts [bid0, bid0 + grid) of the conv bucket only (the overlapped
+// single-GPU schedule updates the fc parameters on the comm stream and splits conv2 / conv1)
 __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int conv_only,
                                                               int bid0) {
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
@@ -141,9 +140,8 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
     spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hold_err);
 }
 
-void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, bool conv_only, hipStream_t s) {
-  const int grid = (conv_only ? 0 : FC1_TILES + 1) + RED_WGS;
-  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(grid), dim3(256), 0, s, a, c, B, conv_only ? 1 : 0, 0);
+void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(FC1_TILES + 1 + RED_WGS), dim3(256), 0, s, a, c, B, 0, 0);
 }
 
 void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s) {

@@ -3,14 +3,14 @@
 // Replaces the autograd backward of reference mnist_ddp.py:50-55 (dropout1, max_pool2d, relu, conv2,
 // relu, conv1): max_pool2d_with_indices_backward, threshold_backward x2, convolution_backward x2.
 //
-//  * conv2_dgrad_kernel  (WG = image x strip of 7 conv1 rows): expands the compact un-pooled gradient
+//  * conv2_dgrad_persist_kernel (items = image x strip of 7 conv1 rows): expands the compact un-pooled gradient
 //    (pooled grads + argmax codes written by fc_bwd) into a zero-padded NHWC LDS tile, runs the transposed
 //    convolution as an MFMA implicit GEMM (M = pixels, N = 32 ci, K = 9 taps x 64 co), applies the
 //    conv1 ReLU mask (stored bf16 a1 > 0, prefetched under the MFMA loop), and folds
 //    the conv1 weight/bias gradient into the epilogue as a second 16x16x16 MFMA fed straight
 //    from the masked accumulators (per-workgroup partials).
-//  * conv2_wgrad_kernel  (G <= 256 WGs, each a contiguous range of dy rows of the whole batch, in
-//    8-row chunks through a double-buffered LDS pipeline): dW2 = dy^T (x) im2col(a1), contraction
+//  * conv2_wgrad_lean_kernel / _lstag_kernel (G <= 256 WGs, each a contiguous range of dy rows of
+//    the whole batch, in 8-row chunks through a double-buffered LDS pipeline): dW2 = dy^T (x) im2col(a1), contraction
 //    over pixels.  Both operands are pixel-major NHWC tiles in LDS; fragments come
 //    from ds_read_b64_tr_b16 with per-lane row addresses, so the im2col gather is free.
 //  * conv_grad_reduce_kernel: fixed-order (deterministic) sum of the partial slabs into the flat
@@ -25,19 +25,18 @@
 
 namespace mnist {
 
-// Phase timing of the per-item dgrad (tools/dgrad_phase.hip compiles this file with
+// Phase timing of the dgrad item (tools/dgrad_phase.hip compiles a copy of this file with
 // MNIST_DGRAD_PHASE_TIMING): thread 0 of every workgroup records s_memtime at each phase boundary.
 #ifdef MNIST_DGRAD_PHASE_TIMING
 constexpr int kDgPhaseMaxWG = 32768;
 __device__ uint64_t g_dg_phase[kDgPhaseMaxWG * 8];
-__device__ int g_dg_stagger;                     // persistent form: ticks the second half of the grid waits
 #define DG_MARK(i)                                                                             \
   if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < kDgPhaseMaxWG)                 \
     g_dg_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime();
 #else
 #define DG_MARK(i)
 #endif
-// Phase timing of conv2_wgrad_kernel (tools/wgrad_phase.hip: MNIST_WGRAD_PHASE_TIMING).
+// Phase timing of the wgrad kernels (tools/wgrad_phase.hip: MNIST_WGRAD_PHASE_TIMING).
 #ifdef MNIST_WGRAD_PHASE_TIMING
 constexpr int kWgPhaseMaxWG = 1024;
 __device__ uint64_t g_wg_phase[kWgPhaseMaxWG * 8];
@@ -444,50 +443,13 @@ __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, i
   dgrad_compute_p<XM, false, PRE>(a, strip, b, dys, w2ds, xs, red, threadIdx.x >> 6, threadIdx.x, xv, pre, prefetch);
 }
 
-template <int XM>
-__device__ __forceinline__ void dgrad_body(const ConvBwdArgs& a, int B, int strip, int b, unsigned char* smem) {
-  const int tid = threadIdx.x;
-  // schedule-3 conv bucket split: dgrad's start = conv2_wgrad done (stream order), i.e. the conv2
-  // gradient slabs are final; one lane tells the comm stream (release: wgrad's writes happen-before)
-  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const StepState* st = a.state ? a.state : &g_zero_state;
-  const int step = st->step;                      // oldest load: the input-row chain hangs off it
-  DG_MARK(0);
-  uint4 w[9];
-  dgrad_w2d_load(a, tid, w);
-  DgLoad L;
-  dgrad_fetch<XM>(a, strip, b, step, tid, L);
-#ifndef MNIST_DGRAD_LATE_MASK
-  DgMask mk;                                      // issued last: first needed in the epilogue
-  dgrad_mask_load(a, strip, b, tid >> 6, mk);
-  constexpr bool kPre = true;
-#else
-  const DgMask mk{};                              // A/B (tools/dgrad_phase.hip): issue under the MFMA loop
-  constexpr bool kPre = false;
-#endif
-  dgrad_w2d_store(smem, tid, w);
-  DG_MARK(1);
-  dgrad_dy_store(smem, strip, tid, L);
-  lds_barrier();        // LDS-only barriers in the dgrad item: the mask loads / the persistent form's
-  DG_MARK(2);           // next-item prefetch and the c1part stores stay in flight across them
-  dgrad_compute<XM, kPre>(a, strip, b, smem, L.xv, mk, [] {});
-  DG_MARK(4);
-}
-
-template <int XM>
-__global__ __launch_bounds__(256) void conv2_dgrad_kernel(ConvBwdArgs a, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
-  dgrad_body<XM>(a, B, blockIdx.x, blockIdx.y, smem);
-}
-
-// Persistent form (default): G <= 2 x CUs workgroups (two fit a CU by LDS), each staging the
+// Persistent dgrad: G <= 2 x CUs workgroups (two fit a CU by LDS), each staging the
 // conv2 weights (36.9 KB) into LDS ONCE and then walking items it = blockIdx.x, +G, ... of the 4B
-// (image, strip) items (strip = it & 3, image = it >> 2: the dgrad_update grid's order).  The next
-// item's dy / input loads are issued right after the current tile's barrier, so they are in flight
-// under the MFMA loop; the co-resident workgroup of the CU overlaps the LDS stores.  Per item the
-// math (K order, masks, conv1-gradient MFMA, c1part row) is the per-item kernel's, bit for bit.
-template <int XM, bool PF>
+// (image, strip) items (strip = it & 3, image = it >> 2).  The next item's dy / input loads are
+// issued right after the current tile's barrier, so they are in flight under the MFMA loop; the
+// co-resident workgroup of the CU overlaps the LDS stores.  Per item the math (K order, masks,
+// conv1-gradient MFMA, c1part row) does not depend on the grid: any G gives the same bits.
+template <int XM>
 __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs a, int B) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
   const int tid = threadIdx.x, n = 4 * B, G = gridDim.x;
@@ -496,230 +458,31 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const StepState* st = a.state ? a.state : &g_zero_state;
   const int step = st->step;
-#ifdef MNIST_DGRAD_PHASE_TIMING
-  if (2 * it >= G && g_dg_stagger > 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)g_dg_stagger) __builtin_amdgcn_s_sleep(2);
-  }
-#endif
   uint4 w[9];
   dgrad_w2d_load(a, tid, w);
   DgLoad L;
   dgrad_fetch<XM>(a, it & 3, it >> 2, step, tid, L);
   dgrad_w2d_store(smem, tid, w);
   for (; it < n; it += G) {
-    if (!PF && it != (int)blockIdx.x) dgrad_fetch<XM>(a, it & 3, it >> 2, step, tid, L);
     dgrad_dy_store(smem, it & 3, tid, L);
     const float xv = L.xv;
     lds_barrier();
     const int nx = (it + G < n) ? it + G : it;   // clamped: the last item's prefetch is a re-read
-    if constexpr (PF)
-      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
-    else
-      dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [] {});
+    dgrad_compute<XM>(a, it & 3, it >> 2, smem, xv, DgMask{}, [&] { dgrad_fetch<XM>(a, nx & 3, nx >> 2, step, tid, L); });
     lds_barrier();                              // the next dy store must not overtake the red reads
   }
 }
 
-// --------------------------------------------------------------------------------------------
-// conv2_dgrad, 3-strip form (opt-in MNIST_AMD_DGRAD3=1): WG = image x strip of 9/9/8 conv1 rows.  The conv2 weights' B fragments
-// come straight from L2 (w2d is 36.9 KB, L2-resident; each wave streams it once per strip with a
-// 4-k-step register prefetch) instead of an LDS copy, so a workgroup needs only the dy tile (11 x 28
-// pixels x 64 ch) + input rows + the reduction scratch: 45.8 KB -> 3 workgroups per CU, and the 3B
-// workgroups of B <= 256 run in one round (the 4-strip form: 4B workgroups, 2 per CU, 1.56 rounds
-// at B = 200).  Same math per pixel as conv2_dgrad_kernel (K order, masks, conv1-gradient MFMA);
-// the conv1 partials are per (image, strip of 3).
-namespace {
-constexpr int D3_ROWS = 9;
-constexpr int D3_TROWS = D3_ROWS + 2;                        // 11 dy rows incl. halo, 11 input rows
-constexpr int D3_DYS = D3_TROWS * DG_TCOLS * C2 * 2;         // 39424
-constexpr int D3_XS = 1280;                                  // 11 * 28 floats (1232 B)
-constexpr int D3_RED = 4 * 32 * 10 * 4;                      // 5120
-constexpr int D3_LDS = D3_DYS + D3_XS + D3_RED;              // 45824
-constexpr int D3_MT = 4;                                     // M-tiles per wave (<= 15 per strip)
-constexpr int D3_PF = 4;                                     // B-fragment prefetch depth (k-steps)
-static_assert(3 * D3_LDS <= 160 * 1024, "three dgrad workgroups per CU");
-static_assert(D3_TROWS * IMG <= 2 * 256, "input rows: two per thread");
-}  // namespace
+int conv_dgrad_c1_rows(int B) { return 4 * B; }
 
-__global__ __launch_bounds__(256, 3) void conv2_dgrad3_kernel(ConvBwdArgs a, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[D3_LDS];
-  uint16_t* dys = reinterpret_cast<uint16_t*>(smem);
-  float* xs = reinterpret_cast<float*>(smem + D3_DYS);
-  float* red = reinterpret_cast<float*>(smem + D3_DYS + D3_XS);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int strip = blockIdx.x, b = blockIdx.y;
-  if (a.signal_ctr && strip == 0 && b == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const int r0 = strip * D3_ROWS;
-  const int npix = ((strip == 2) ? (H1 - 2 * D3_ROWS) : D3_ROWS) * H1;   // 9, 9, 8 rows
-  const int step = a.state ? a.state->step : 0;
-
-  // ---- stage the padded dy tile (rows r0-2..r0+8, cols -2..25) and the input rows
-  {
-    constexpr int NCH = D3_TROWS * DG_TCOLS * 8;   // 2464 16-B chunks
-    constexpr int KV = (NCH + 255) / 256;          // 10
-    uint4 v[KV];
-    uint2 rt[KV];
-    uint32_t okm = 0;
-#pragma unroll
-    for (int k = 0; k < KV; ++k) {
-      const int c = tid + 256 * k;
-      const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3, c8 = rem & 7;
-      const int y = r0 - 2 + ly, x = col - 2;
-      const bool ok = c < NCH && y >= 0 && y < H2 && x >= 0 && x < H2;
-      okm |= (ok ? 1u : 0u) << k;
-      const uint8_t* rec = dyc_record(a.dyc, b, ok ? y : 0, ok ? x : 0);
-      v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
-      rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
-    }
-    float xv[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int e = tid + 256 * j;
-      const bool okx = e < D3_TROWS * IMG && r0 + e / IMG < IMG;
-      const int off = r0 * IMG + (okx ? e : 0);
-      if (a.xin) {
-        xv[j] = a.xin[(int64_t)b * (IMG * IMG) + off];
-      } else {
-        const int64_t row = (int64_t)step * a.idx_step_stride + b;
-        const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
-        xv[j] = normalize_u8(a.data_u8[img * (IMG * IMG) + off]);
-      }
-      if (!okx) xv[j] = 0.0f;
-    }
-    const uint4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < KV; ++k) {
-      const int c = tid + 256 * k;
-      if (c < NCH) {
-        const int ly = c / (DG_TCOLS * 8), rem = c - ly * (DG_TCOLS * 8), col = rem >> 3;
-        const int y = r0 - 2 + ly, x = col - 2;
-        const int row = c >> 3, c8 = c & 7;
-        const uint4 d = ((okm >> k) & 1u) ? dyc_expand(v[k], rt[k], ((y & 1) << 1) | (x & 1)) : z;
-        reinterpret_cast<uint4*>(dys)[row * 8 + (c8 ^ swz8(row))] = d;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      if (tid + 256 * j < D3_TROWS * IMG) xs[tid + 256 * j] = xv[j];
-  }
-  __syncthreads();
-
-  // ---- transposed conv on MFMA: wave w owns M-tiles w, w+4, w+8, w+12 (16 pixels each)
-  const int m = lane & 15, kg = lane >> 4;
-  int qbase[D3_MT];
-#pragma unroll
-  for (int i = 0; i < D3_MT; ++i) {
-    int q = 16 * (wave + 4 * i) + m;
-    if (q >= npix) q = 0;
-    const int qy = q / H1, qx = q - qy * H1;
-    qbase[i] = (qy + 2) * DG_TCOLS + qx + 2;
-  }
-  floatx4 acc[D3_MT][2];
-#pragma unroll
-  for (int i = 0; i < D3_MT; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // conv1 ReLU mask (a1 > 0), two bf16 per VGPR, loaded before the B stream (vmcnt is in order)
-  uint32_t a1v[D3_MT][4];
-#pragma unroll
-  for (int i = 0; i < D3_MT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int q = 16 * (wave + 4 * i) + 4 * kg + r;
-      q = q < npix ? q : npix - 1;
-      const uint16_t* src = a.a1 + ((int64_t)b * H1 * H1 + r0 * H1 + q) * C1 + m;
-      a1v[i][r] = (uint32_t)src[0] | ((uint32_t)src[16] << 16);
-    }
-  // B fragment (tap t, ci tile nt, co chunk) of w2d [9][32][64]: 16 contiguous bytes per lane
-  const uint16_t* wb = a.w2d + (int64_t)m * C2 + 8 * kg;
-  bf16x8 Bq[18][2];
-#pragma unroll
-  for (int ks = 0; ks < D3_PF; ++ks)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) Bq[ks][nt] = ld16(wb + ((ks >> 1) * C1 + nt * 16) * C2 + 32 * (ks & 1));
-#pragma unroll
-  for (int ks = 0; ks < 18; ++ks) {
-    if (ks + D3_PF < 18) {
-      const int kn = ks + D3_PF;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) Bq[kn][nt] = ld16(wb + ((kn >> 1) * C1 + nt * 16) * C2 + 32 * (kn & 1));
-    }
-    const int t = ks >> 1, co0 = 32 * (ks & 1);
-    const int toff = (t / 3) * DG_TCOLS + (t % 3);
-    const int ch = (co0 >> 3) + kg;
-    bf16x8 A[D3_MT];
-#pragma unroll
-    for (int i = 0; i < D3_MT; ++i) {
-      const int row = qbase[i] - toff;
-      A[i] = ld16(dys + row * C2 + ((ch ^ swz8(row)) << 3));
-    }
-#pragma unroll
-    for (int i = 0; i < D3_MT; ++i)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[i][nt] = mfma16x16x32(A[i], Bq[ks][nt], acc[i][nt]);
-  }
-
-  // ---- conv1 ReLU mask + conv1 weight/bias gradient MFMA (as conv2_dgrad_kernel)
-  floatx4 dw[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
-  {
-    const int tap = lane & 15, ty = tap / 3, tx = tap - 3 * ty;
-#pragma unroll
-    for (int i = 0; i < D3_MT; ++i) {
-      short4_t ax, bd[2];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = 16 * (wave + 4 * i) + 4 * kg + j;
-        const int qc = q < npix ? q : npix - 1;
-        const int py = qc / H1, px = qc - py * H1;
-        const float xv = (tap < 9) ? xs[(py + ty) * IMG + px + tx] : ((tap == 9) ? 1.0f : 0.0f);
-        ax[j] = (short)f2bf(xv);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const uint16_t av = (uint16_t)(a1v[i][j] >> (16 * nt));
-          const float d = (q < npix && av != 0 && !(av & 0x8000)) ? acc[i][nt][j] : 0.0f;
-          bd[nt][j] = (short)f2bf(d);
-        }
-      }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) dw[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ax, bd[nt], dw[nt], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 4 * kg + r;
-      if (t < 10) red[(wave * 32 + nt * 16 + m) * 10 + t] = dw[nt][r];
-    }
-  __syncthreads();
-  for (int e = tid; e < 320; e += 256) {
-    const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
-    a.c1part[((int64_t)b * 3 + strip) * 320 + e] = s;
-  }
-}
-
-// read per call (host, at enqueue / capture time) so a process can compare both forms.  Default: the
-// 4-strip LDS form (measured B = 200: 81.2-81.5 vs 84.6-84.8 us/step, B = 8192: 1326 vs 1377 us):
-// streaming w2d through L1 (32 KB, smaller than w2d) costs more than the occupancy it buys.
-static int dgrad_strips() {
-  const char* e = getenv("MNIST_AMD_DGRAD3");
-  return (e && e[0] == '1') ? 3 : 4;
-}
-int conv_dgrad_c1_rows(int B) { return dgrad_strips() * B; }
-
-// Grid of the persistent 4-strip dgrad: MNIST_AMD_DGRAD_PERSIST = 0 -> per-item kernel (returns 0),
-// unset / 1 -> 2 x CUs workgroups (measured B = 200: 80.4 vs 82.6 us/step; B = 8192, since the
-// branch-free conv1-gradient epilogue: 0.980 vs 1.062 ms/step - the item loop stages the conv2
-// weights once and hides the next item's record / input-row chain under the MFMA loop, where the
-// per-item kernel waits out that chain in every workgroup; round 2 measured the per-item kernel
-// faster at 8192, 1.35 vs 1.44, with the old epilogue); N > 1 -> min(4B, N) workgroups.  Read per
-// call (host).
+// Grid of the persistent dgrad: 2 x CUs workgroups, or fewer when 4B items are fewer (measured
+// B = 200: 80.4 vs 82.6 us/step against the per-item grid; B = 8192, with the branch-free conv1-gradient
+// epilogue, 0.980 vs 1.062 ms/step).  set_dgrad_grid(n > 0) overrides it (tests: ragged item rounds).
+static int g_dgrad_grid_override = 0;
+void set_dgrad_grid(int n) { g_dgrad_grid_override = n > 0 ? n : 0; }
 static int dgrad_persist_grid(int B) {
-  const char* e = getenv("MNIST_AMD_DGRAD_PERSIST");
-  const int v = e ? atoi(e) : 1;
-  if (v == 0) return 0;
-  int g = v;
-  if (v == 1) {
+  int g = g_dgrad_grid_override;
+  if (g <= 0) {
     static int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -731,211 +494,19 @@ static int dgrad_persist_grid(int B) {
   return g < 4 * B ? g : 4 * B;
 }
 
-// dgrad (workgroups [0, 4B), same order as conv2_dgrad_kernel's (strip, b) grid) + the conv2 slab
-// reduce and Adadelta step (workgroups [4B, 4B + RED_W2_PARTS)).  Workgroups are dispatched in id
-// order, so the reduce parts take the slots of dgrad's last partial round (800 WGs on 512 slots at
-// B = 200) instead of a launch of their own after dgrad.  Reads only wgrad's slabs (complete at
-// launch); writes conv2 params / state / grads and the shadows u.w2f, u.w2d (!= a.w2d, which the
-// dgrad workgroups read).
-template <int XM>
-__global__ __launch_bounds__(256) void conv2_dgrad_update_kernel(ConvBwdArgs a, AdadeltaArgs u, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
-  const int bid = blockIdx.x;
-  if (bid < 4 * B) {
-    dgrad_body<XM>(a, B, bid & 3, bid >> 2, smem);
-    return;
-  }
-  conv_reduce_update(u, a, B, bid - 4 * B, reinterpret_cast<float4*>(smem));
-}
-
 // --------------------------------------------------------------------------------------------
 namespace {
 // first a1 row (global, [B*26]) under dy row R (global, [B*24])
 __device__ __forceinline__ int a1_row_of(int R) { return R + 2 * (R / H2); }
 
-template <int NTH>
-struct WgradChunkT {
-  static constexpr int VD = WDY_BYTES / 16 / NTH, VA = (WA1_BYTES / 16 + NTH - 1) / NTH;
-  uint4 vd[VD], va[VA];
-  uint2 rt[VD];
-  uint32_t okd, oka;          // validity bits, applied at the LDS store (not on the loaded values)
-};
-using WgradChunk = WgradChunkT<WG_THREADS>;
-static_assert(WDY_BYTES % (16 * 256) == 0, "dy chunk staging by 256 threads");
-
-// Issue the global loads of chunk [c0, c1) into registers (zeros past the valid rows, so every LDS
-// byte of the buffer is rewritten and finite).  The loads are unconditional (clamped to the chunk's
-// first element, the value masked after): loads under a branch make the waitcnt pass fall back to
-// vmcnt(0), which pulled the wait for this prefetch up into the middle of the MFMA loop.
-template <int NTH>
-__device__ __forceinline__ void wgrad_fetch(const ConvBwdArgs& a, int c0, int c1, int tid, WgradChunkT<NTH>& k) {
-  constexpr int VD = WgradChunkT<NTH>::VD, VA = WgradChunkT<NTH>::VA;
-  const int ndy = (c1 - c0) * H2 * 8;                               // valid 16-B chunks of dy
-  const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
-  const int na1 = (A1 - A0) * H1 * 4;                               // valid 16-B chunks of a1
-  const uint4* asrc = reinterpret_cast<const uint4*>(a.a1 + (int64_t)A0 * H1 * C1);
-  k.okd = k.oka = 0;
-#pragma unroll
-  for (int i = 0; i < VD; ++i) {
-    const int c0i = tid + NTH * i;
-    const bool ok = c0i < ndy;
-    k.okd |= (ok ? 1u : 0u) << i;
-    const int c = ok ? c0i : 0;                     // dense chunk (pixel c>>3, channels 8(c&7)..)
-    const int pix = c >> 3, R = c0 + pix / H2, x = pix - (pix / H2) * H2;
-    const int bimg = R / H2, y = R - bimg * H2;
-    const uint8_t* rec = dyc_record(a.dyc, bimg, y, x);
-    k.vd[i] = *reinterpret_cast<const uint4*>(rec + (c & 7) * 16);
-    k.rt[i] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + (c & 7) * 8);
-  }
-#pragma unroll
-  for (int i = 0; i < VA; ++i) {
-    const int c = tid + NTH * i;
-    k.oka |= (c < na1 ? 1u : 0u) << i;
-    k.va[i] = asrc[c < na1 ? c : 0];
-  }
-}
-
-template <int NTH>
-__device__ __forceinline__ void wgrad_store(unsigned char* buf, int tid, int c0, const WgradChunkT<NTH>& k, float* bsum) {
-  constexpr int VD = WgradChunkT<NTH>::VD, VA = WgradChunkT<NTH>::VA;
-  uint4* dys = reinterpret_cast<uint4*>(buf);
-  uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
-#pragma unroll
-  for (int i = 0; i < VD; ++i) {
-    const int c = tid + NTH * i, pix = c >> 3;
-    const int R = c0 + pix / H2, x = pix - (pix / H2) * H2;
-    const uint4 d = ((k.okd >> i) & 1u) ? dyc_expand(k.vd[i], k.rt[i], ((R & 1) << 1) | (x & 1))   // H2 even: y&1 == R&1
-                                        : uint4{0u, 0u, 0u, 0u};
-    dys[pix * 8 + ((c & 7) ^ swz_dy(pix))] = d;
-    const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {          // conv2 bias gradient: this thread always holds channels 8*(tid&7)..
-      bsum[2 * j] += bf2f((uint16_t)(w4[j] & 0xFFFF));
-      bsum[2 * j + 1] += bf2f((uint16_t)(w4[j] >> 16));
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < VA; ++i) {
-    const int c = tid + NTH * i;
-    if (c < WA1_BYTES / 16) a1s[c] = ((k.oka >> i) & 1u) ? k.va[i] : uint4{0u, 0u, 0u, 0u};
-  }
-}
 }  // namespace
 
-__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  // 8 waves = 2 co-tile pairs x 4 groups of the 18 (tap, ci-half) n-tiles (5, 5, 4, 4)
-  const int mt0 = 2 * (wave & 1), ng = wave >> 1;
-  const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
-  const int G = gridDim.x, g = blockIdx.x;
-  // DDP schedule 3: announce "this step's fc gradients are final" to the comm stream.  fc_bwd, the
-  // previous kernel on this stream, has completed and released its writes, so one lane's add at
-  // kernel start is the signal - no separate signal launch on the critical path.
-  if (a.signal_ctr && g == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const int rows = H2 * B;
-  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
-  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
-
-  floatx4 acc[2][5];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float bsum[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-  // per-lane A (dy) fragment offsets: pixel rows 32ks + clo / + chi, swizzle independent of ks
-  const int clo = 8 * gq + q, chi = clo + 4;
-  int aoff_lo[2], aoff_hi[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int cb = 16 * (mt0 + i) + 4 * pp;
-    aoff_lo[i] = clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7));
-    aoff_hi[i] = chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7));
-  }
-  // per-lane B (a1) tap offsets of this wave's n-tiles
-  int toffs[5];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int nt = nt0 + (j < nn ? j : 0), t = nt >> 1, ci0 = 16 * (nt & 1);
-    toffs[j] = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
-  }
-
-  WgradChunk k;
-  WG_MARK(0);
-  if (nchunks > 0) {
-    wgrad_fetch(a, r0, min(r0 + WG_CH, r1), tid, k);
-    wgrad_store(smem, tid, r0, k, bsum);
-  }
-  __syncthreads();
-  WG_MARK(1);
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int c0 = r0 + ch * WG_CH, c1 = min(c0 + WG_CH, r1);
-    const bool more = ch + 1 < nchunks;
-    if (more) wgrad_fetch(a, c1, min(c1 + WG_CH, r1), tid, k);     // in flight under the MFMAs
-    const unsigned char* buf = smem + (ch & 1) * WBUF_BYTES;
-    const uint16_t* dys = reinterpret_cast<const uint16_t*>(buf);
-    const uint16_t* a1s = reinterpret_cast<const uint16_t*>(buf + WDY_BYTES);
-    const int A0 = a1_row_of(c0);
-    const int nks = ((c1 - c0) * H2 + 31) / 32;
-#pragma unroll 1
-    for (int ks = 0; ks < nks; ++ks) {
-      bf16x8 A[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) A[i] = tr_frag(dys + ks * 32 * C2 + aoff_lo[i], dys + ks * 32 * C2 + aoff_hi[i]);
-      // B: a1 pixel under dy pixel p of the chunk (row c0 + p/24, col p%24), shifted by the tap
-      const int plo = 32 * ks + clo, phi = plo + 4;
-      const int rlo = plo / H2, rhi = phi / H2;
-      const int blo_px = (a1_row_of(c0 + rlo) - A0) * H1 + (plo - rlo * H2);
-      const int bhi_px = (a1_row_of(c0 + rhi) - A0) * H1 + (phi - rhi * H2);
-      const uint16_t* blo = a1s + blo_px * C1 + 4 * pp;
-      const uint16_t* bhi = a1s + bhi_px * C1 + 4 * pp;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        if (j < nn) {                                               // wave-uniform
-          const bf16x8 Bf = tr_frag(blo + toffs[j], bhi + toffs[j]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
-        }
-      }
-    }
-    if (ch == 0) { WG_MARK(2); }             // chunk 0's MFMAs issued (wave 0)
-    if (more) wgrad_store(smem + ((ch + 1) & 1) * WBUF_BYTES, tid, c1, k, bsum);
-    __syncthreads();
-    if (ch == 0) { WG_MARK(3); }             // chunk 1 staged (barrier)
-  }
-  WG_MARK(4);
-  // slab layout = MFMA-native [co-tile 4][n-tile 18][lane 64][4]: one coalesced float4 per tile
-  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-      if (j < nn) {
-        const int tile = (mt0 + i) * 18 + nt0 + j;
-        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
-      }
-  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 64 such threads via LDS
-  float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[j * WG_THREADS + tid] = bsum[j];
-  __syncthreads();
-  if (tid < 64) {
-    const int c8 = tid >> 3, j = tid & 7;     // channel = 8*c8 + j
-    float s = 0.f;
-    for (int kk = 0; kk < WG_THREADS / 8; ++kk) s += red[j * WG_THREADS + kk * 8 + c8];
-    out[18432 + 8 * c8 + j] = s;
-  }
-  WG_MARK(5);
-}
-
 // --------------------------------------------------------------------------------------------
-// conv2_wgrad, VALU-lean form (default below the staggered threshold).  Same workgroup geometry,
-// chunk pipeline, wave tiling and slab layout as conv2_wgrad_kernel, with the VALU work that made
-// it issue-bound taken out (PMC at B = 200: ~1570 VALU instructions per wave against 133 MFMAs; a
+// conv2_wgrad, VALU-lean form (below the staggered threshold).  G <= 256 workgroups, each a
+// contiguous range of dy rows of the whole batch in 8-row chunks through a double-buffered LDS
+// pipeline; 8 waves = 2 co-tile pairs x 4 groups of the 18 (tap, ci-half) n-tiles.  The round-2
+// lockstep kernel of the same geometry had the VALU work that made it issue-bound (removed; numbers
+// in docs/PERF_NOTES.md) (PMC at B = 200: ~1570 VALU instructions per wave against 133 MFMAs; a
 // wave64 VALU instruction holds its SIMD for 2-4 cycles, so VALU issue - not the MFMA pipe or the
 // LDS - set the kernel's time; tools/wgrad_phase.hip):
 //  * staging: every chunk-invariant part of a thread's three dense dy chunks (row / column inside
@@ -949,7 +520,6 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_kernel(ConvBwdArgs a, 
 //  * MFMA loop: k-steps unrolled, the n-group a template parameter, so every fragment read is a
 //    base register + an immediate; the B-row base of each (k-step, lo/hi) lane row is precomputed
 //    once per kernel and only the image-boundary shift (52 a1 pixels) is selected per chunk.
-// The sums differ from conv2_wgrad_kernel's only in the bias (MFMA accumulation order).
 namespace {
 constexpr int WL_KS = WG_CHPX / 32;                         // 6 k-steps per full chunk
 // a1 tile planar by channel half ([ci / 16][pixel][16 ci], 32 B per pixel): with the k -> pixel map
@@ -1279,135 +849,6 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
 }
 
 // --------------------------------------------------------------------------------------------
-// conv2_wgrad, staggered halves (large batches, see wgrad_staggered).  The
-// 8 waves form two independent halves of 4 (waves 0-3 / 4-7: one wave of each half per SIMD), each
-// owning one of the two LDS chunk buffers and the alternate chunks of the workgroup's row range
-// (half h: chunks h, h+2, ...).  In phase p half (p & 1) runs the MFMAs of chunk p while the other
-// half stores its prefetched chunk p+1 into its buffer and issues the global loads of chunk p+3 - so
-// every SIMD pairs one MFMA wave with one staging wave instead of all 8 waves alternating between
-// an MFMA phase and a VALU/LDS-store phase in lockstep (cdna4 "stagger": matrix beside memory).
-// Each wave of a half covers 2 co-tiles x 9 (tap, ci-half) n-tiles; at the end half 1 hands its
-// accumulators to half 0 through LDS (fixed order: half 0 + half 1) and the workgroup writes one
-// slab, so the reduce sees the same G slabs.  The conv2 bias sum is per thread as before.
-__global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_stag_kernel(ConvBwdArgs a, int B) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int half = wave >> 2, hw = wave & 3, htid = tid & 255;
-  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int mt0 = 2 * (hw & 1), nt0 = 9 * (hw >> 1);
-  const int G = gridDim.x, g = blockIdx.x;
-  if (a.signal_ctr && g == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const int rows = H2 * B;
-  const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
-  const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
-
-  floatx4 acc[2][9];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float bsum[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-  const int clo = 8 * gq + q, chi = clo + 4;
-  int aoff_lo[2], aoff_hi[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int cb = 16 * (mt0 + i) + 4 * pp;
-    aoff_lo[i] = clo * C2 + ((((cb >> 3) ^ swz_dy(clo)) << 3) | (cb & 7));
-    aoff_hi[i] = chi * C2 + ((((cb >> 3) ^ swz_dy(chi)) << 3) | (cb & 7));
-  }
-  int toffs[9];
-#pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    const int nt = nt0 + j, t = nt >> 1, ci0 = 16 * (nt & 1);
-    toffs[j] = ((t / 3) * H1 + (t % 3)) * C1 + ci0;
-  }
-  auto chunk_lo = [&](int ch) { return r0 + ch * WG_CH; };
-  auto chunk_hi = [&](int ch) { return min(r0 + (ch + 1) * WG_CH, r1); };
-  unsigned char* mybuf = smem + half * WBUF_BYTES;
-
-  // prologue: half 0 stages chunk 0 and prefetches chunk 2; half 1 prefetches chunk 1
-  WgradChunkT<256> k;
-  if (half == 0) {
-    if (nchunks > 0) {
-      wgrad_fetch<256>(a, chunk_lo(0), chunk_hi(0), htid, k);
-      wgrad_store<256>(mybuf, htid, chunk_lo(0), k, bsum);
-    }
-    if (nchunks > 2) wgrad_fetch<256>(a, chunk_lo(2), chunk_hi(2), htid, k);
-  } else if (nchunks > 1) {
-    wgrad_fetch<256>(a, chunk_lo(1), chunk_hi(1), htid, k);
-  }
-  __syncthreads();
-  for (int ph = 0; ph < nchunks; ++ph) {
-    if ((ph & 1) == half) {                             // MFMAs of chunk ph (half-uniform)
-      const int c0 = chunk_lo(ph), c1 = chunk_hi(ph);
-      const uint16_t* dys = reinterpret_cast<const uint16_t*>(mybuf);
-      const uint16_t* a1s = reinterpret_cast<const uint16_t*>(mybuf + WDY_BYTES);
-      const int A0 = a1_row_of(c0);
-      const int nks = ((c1 - c0) * H2 + 31) / 32;
-#pragma unroll 1
-      for (int ks = 0; ks < nks; ++ks) {
-        bf16x8 A[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) A[i] = tr_frag(dys + ks * 32 * C2 + aoff_lo[i], dys + ks * 32 * C2 + aoff_hi[i]);
-        const int plo = 32 * ks + clo, phi = plo + 4;
-        const int rlo = plo / H2, rhi = phi / H2;
-        const int blo_px = (a1_row_of(c0 + rlo) - A0) * H1 + (plo - rlo * H2);
-        const int bhi_px = (a1_row_of(c0 + rhi) - A0) * H1 + (phi - rhi * H2);
-        const uint16_t* blo = a1s + blo_px * C1 + 4 * pp;
-        const uint16_t* bhi = a1s + bhi_px * C1 + 4 * pp;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          const bf16x8 Bf = tr_frag(blo + toffs[j], bhi + toffs[j]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) acc[i][j] = mfma16x16x32(A[i], Bf, acc[i][j]);
-        }
-      }
-    } else if (ph + 1 < nchunks) {                      // stage chunk ph+1, prefetch chunk ph+3
-      wgrad_store<256>(mybuf, htid, chunk_lo(ph + 1), k, bsum);
-      if (ph + 3 < nchunks) wgrad_fetch<256>(a, chunk_lo(ph + 3), chunk_hi(ph + 3), htid, k);
-    }
-    __syncthreads();
-  }
-  // half 1 -> half 0 through LDS ([hw][i][j][lane] float4, 73.7 KB), half 0 adds in fixed order
-  floatx4* xch = reinterpret_cast<floatx4*>(smem);
-  static_assert(4 * 18 * 64 * 16 <= WG_LDS, "accumulator exchange fits the chunk buffers");
-  if (half == 1) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 9; ++j) xch[((hw * 2 + i) * 9 + j) * 64 + lane] = acc[i][j];
-  }
-  __syncthreads();
-  float* out = a.w2part + (int64_t)g * W2PART_STRIDE;
-  if (half == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const floatx4 o = xch[((hw * 2 + i) * 9 + j) * 64 + lane];
-        const floatx4 v = {acc[i][j][0] + o[0], acc[i][j][1] + o[1], acc[i][j][2] + o[2], acc[i][j][3] + o[3]};
-        const int tile = (mt0 + i) * 18 + nt0 + j;
-        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = v;
-      }
-  }
-  __syncthreads();
-  // bias: threads with equal tid&7 hold the same 8 channels -> reduce 64 such threads via LDS
-  float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[j * WG_THREADS + tid] = bsum[j];
-  __syncthreads();
-  if (tid < 64) {
-    const int c8 = tid >> 3, j = tid & 7;     // channel = 8*c8 + j
-    float sm = 0.f;
-    for (int kk = 0; kk < WG_THREADS / 8; ++kk) sm += red[j * WG_THREADS + kk * 8 + c8];
-    out[18432 + 8 * c8 + j] = sm;
-  }
-}
-
-// --------------------------------------------------------------------------------------------
 // Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
   __shared__ float4 red[256];
@@ -1416,15 +857,6 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, in
 }
 
 static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
-
-void launch_conv_dgrad_update(const ConvBwdArgs& c, const AdadeltaArgs& u, int B, hipStream_t s) {
-  if (c.c1_rows != 4 * B) throw std::runtime_error("conv_dgrad_update: needs the 4-strip dgrad (c1_rows = 4B)");
-  if (c.idx)
-    hipLaunchKernelGGL(conv2_dgrad_update_kernel<DGX_IDX>, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
-  else
-    hipLaunchKernelGGL(conv2_dgrad_update_kernel<DGX_PRE>, dim3(4 * B + RED_W2_WGS), dim3(256), 0, s, c, u, B);
-  launch_c1_prereduce(c, B, s);
-}
 
 // c1red[j] = sum of the conv1 partial rows [j*R, (j+1)*R) (R = ceil(4B / C1_PRE_SLABS)) in fixed
 // order: thread (column, slice) sums rows slice, slice+3, ... in batches of 16 independent loads,
@@ -1464,55 +896,31 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
 }
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  if (a.c1_rows == 3 * B)
-    hipLaunchKernelGGL(conv2_dgrad3_kernel, dim3(3, B), dim3(256), 0, s, a, B);
-  else if (a.c1_rows == 4 * B && dgrad_persist_grid(B) > 0) {
-    const dim3 g(dgrad_persist_grid(B));
-    const char* pe = getenv("MNIST_AMD_DGRAD_PF");
-    const bool pf = !(pe && pe[0] == '0');
-    if (a.xin)
-      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_XIN, true>), g, dim3(256), 0, s, a, B);
-    else if (a.idx && pf)
-      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_IDX, true>), g, dim3(256), 0, s, a, B);
-    else if (a.idx)
-      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_IDX, false>), g, dim3(256), 0, s, a, B);
-    else if (pf)
-      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_PRE, true>), g, dim3(256), 0, s, a, B);
-    else
-      hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_PRE, false>), g, dim3(256), 0, s, a, B);
-  } else if (a.c1_rows == 4 * B && a.xin)
-    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_XIN>, dim3(4, B), dim3(256), 0, s, a, B);
-  else if (a.c1_rows == 4 * B && a.idx)
-    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_IDX>, dim3(4, B), dim3(256), 0, s, a, B);
-  else if (a.c1_rows == 4 * B)
-    hipLaunchKernelGGL(conv2_dgrad_kernel<DGX_PRE>, dim3(4, B), dim3(256), 0, s, a, B);
+  if (a.c1_rows != 4 * B) throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
+  const dim3 g(dgrad_persist_grid(B));
+  if (a.xin)
+    hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_XIN>), g, dim3(256), 0, s, a, B);
+  else if (a.idx)
+    hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_IDX>), g, dim3(256), 0, s, a, B);
   else
-    throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
+    hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_PRE>), g, dim3(256), 0, s, a, B);
   launch_c1_prereduce(a, B, s);
 }
 // Staggered halves pay once every half has >= 2 chunks of its own (rows per workgroup >= 32, i.e.
 // B >= 342 at 256 groups): measured B = 8192 1263-1266 -> 1214-1216 us/step, B = 2048 367-370 ->
-// 355-363; at B = 200 (2-3 chunks per workgroup) the plain kernel stays (78.5-78.9 vs 80.3-80.8).
-// MNIST_AMD_WGRAD_STAG=0 / 1 forces either form (read per call, host).
+// 355-363; at B = 200 (2-3 chunks per workgroup) the single-buffer-pair form stays (78.5-78.9 vs
+// 80.3-80.8).  set_wgrad_form(0 / 1) forces either form (tests: the two forms agree), -1 = by batch.
+static int g_wgrad_form = -1;
+void set_wgrad_form(int f) { g_wgrad_form = (f == 0 || f == 1) ? f : -1; }
 static bool wgrad_staggered(const ConvBwdArgs& a, int B) {
-  const char* e = getenv("MNIST_AMD_WGRAD_STAG");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  if (g_wgrad_form >= 0) return g_wgrad_form == 1;
   return (int64_t)H2 * B >= (int64_t)4 * WG_CH * a.wgrad_groups;
 }
-// MNIST_AMD_WGRAD_LEAN=0: the previous lockstep / staggered kernels instead of the VALU-lean ones
-static bool wgrad_lean() {
-  const char* e = getenv("MNIST_AMD_WGRAD_LEAN");
-  return !(e && e[0] == '0');
-}
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
-  if (!wgrad_staggered(a, B) && wgrad_lean())
-    hipLaunchKernelGGL(conv2_wgrad_lean_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
-  else if (wgrad_lean())
+  if (wgrad_staggered(a, B))
     hipLaunchKernelGGL(conv2_wgrad_lstag_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
-  else if (!wgrad_staggered(a, B))
-    hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
   else
-    hipLaunchKernelGGL(conv2_wgrad_stag_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
+    hipLaunchKernelGGL(conv2_wgrad_lean_kernel, dim3(a.wgrad_groups), dim3(WG_THREADS), 0, s, a, B);
 }
 void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
   launch_conv_dgrad(a, B, s);

@@ -20,10 +20,9 @@ namespace mnist {
 // ============================================================================================
 // MR = 16-row M-tiles per workgroup: MR = 2 (default) halves the w1 fragment traffic per output
 // (each wave's B fragments feed two M-tiles) at half the workgroups; bitwise the MR = 1 result.
-// One fc1 workgroup (row tile x K-chunk) of the R x 32 grid, linear id `lin`; returns the row tile.
-// SC1: z1part written with sc1 (write-through) stores, for the fused head consumers below.
-template <int MR, bool SC1>
-__device__ __forceinline__ int fc1_tile(const uint16_t* __restrict__ p, const uint16_t* __restrict__ w1,
+// One fc1 workgroup (row tile x K-chunk) of the R x 32 grid, linear id `lin`.
+template <int MR>
+__device__ __forceinline__ void fc1_tile(const uint16_t* __restrict__ p, const uint16_t* __restrict__ w1,
                                         float* __restrict__ z1part, int B, int R, int lin) {
   constexpr int KC = NFLAT / FC1_KSPLIT;   // 288
   constexpr int KS = KC / 32;              // 9
@@ -66,24 +65,18 @@ __device__ __forceinline__ int fc1_tile(const uint16_t* __restrict__ p, const ui
       const int b = (tile * MR + t) * 16 + 4 * kg + r;
       if (b < B) {
         float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
-        if constexpr (SC1) {
-          __hip_atomic_store(dst, acc0[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(dst + 16, acc1[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          dst[0] = acc0[r];
-          dst[16] = acc1[r];
-        }
+        dst[0] = acc0[r];
+        dst[16] = acc1[r];
       }
     }
   }
-  return tile;
 }
 
 template <int MR>
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
                                                       const uint16_t* __restrict__ w1,
                                                       float* __restrict__ z1part, int B) {
-  fc1_tile<MR, false>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
+  fc1_tile<MR>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
 }
 
 // Large batches: 64 rows x 128 columns per workgroup, K split 4 ways (2304 = 36 stages of 64),
@@ -197,17 +190,9 @@ void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B,
                        p, w1, z1part, B);
     return;
   }
-  // 16-row tiles per workgroup (MNIST_AMD_FC1_MR = 1 / 2 / 4, read per call; default 2: measured
-  // B = 200 75.6-77.0 -> 73.8-74.7 us/step with 2, B = 300 97.0-97.2 -> 95.6-96.3)
-  const char* e = getenv("MNIST_AMD_FC1_MR");
-  const int mr = e ? atoi(e) : 2;
-  if (mr == 4) {
-    hipLaunchKernelGGL(fc1_fwd_kernel<4>, dim3((B + 63) / 64, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
-  } else if (mr == 1) {
-    hipLaunchKernelGGL(fc1_fwd_kernel<1>, dim3((B + 15) / 16, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
-  } else {
-    hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3((B + 31) / 32, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
-  }
+  // two 16-row tiles per workgroup (MR = 2; measured B = 200 75.6-77.0 -> 73.8-74.7 us/step against
+  // MR = 1, B = 300 97.0-97.2 -> 95.6-96.3; MR = 4 was slower: docs/PERF_NOTES.md)
+  hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3((B + 31) / 32, FC1_KSPLIT), dim3(256), 0, s, p, w1, z1part, B);
 }
 
 // ============================================================================================
@@ -275,9 +260,8 @@ __device__ __forceinline__ void log_softmax10(const float* x, float* lp) {
 // a branch-guarded load ends in vmcnt(0), which used to finish the label + bias round trip before
 // the partial-sum loads even went out.  Arithmetic (order and expression forms) is that of
 // head_forward_row / the module head, so the results are bitwise unchanged.
-// One wave = one batch row b.  SC1: the split-K partials are read with sc1 loads (they were
-// published by other workgroups of the same launch: fc1_head_train_kernel).
-template <int KS, bool IDX, bool SC1>
+// One wave = one batch row b.
+template <int KS, bool IDX>
 __device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, int lane) {
   if (b >= B) {  // padding rows of the bf16 operands consumed by the backward GEMMs
     a.dz1[(int64_t)b * NH + lane] = 0;
@@ -300,11 +284,7 @@ __device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, 
 #pragma unroll
   for (int c = 0; c < KS; ++c)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float* src = a.z1part + ((int64_t)c * B + b) * NH + lane + 64 * j;
-      if constexpr (SC1) part[c][j] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else part[c][j] = *src;
-    }
+    for (int j = 0; j < 2; ++j) part[c][j] = a.z1part[((int64_t)c * B + b) * NH + lane + 64 * j];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bf1[j] = a.b_fc1[lane + 64 * j];
 #pragma unroll
@@ -376,71 +356,7 @@ __device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, 
 
 template <int KS, bool IDX>
 __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
-  head_train_row<KS, IDX, false>(a, B, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), threadIdx.x & 63);
-}
-
-// fc1 (B < FC1_BIG_MIN_B) and the training head in ONE launch.  Workgroups [0, 32R) are fc1's
-// (row tile of 32 rows x K-chunk, exactly fc1_fwd_kernel<2>'s), each publishing its sc1-stored
-// partials with one agent-scope counter add per row tile after every wave's vmcnt(0) + a barrier;
-// workgroups [32R, 32R + Bp/4) are the head's (4 rows each, exactly head_train_kernel's math), each
-// polling its tile's counter, then reading the partials with sc1 loads.  Dispatch is in grid order
-// on every XCD and producers never wait, so the consumers always make progress; the tile's last
-// head workgroup re-arms the two counters for the next launch (stream-ordered).  Saves the fc1 ->
-// head kernel boundary and lets the head's workgroups be resident before their data is.
-template <bool IDX>
-__global__ __launch_bounds__(256) void fc1_head_train_kernel(const uint16_t* __restrict__ p,
-                                                             const uint16_t* __restrict__ w1, HeadArgs a, int B,
-                                                             int R, int* ctr, int* hdone, int* err) {
-  const int nF = R * FC1_KSPLIT;
-  if ((int)blockIdx.x < nF) {
-    const int tile = fc1_tile<2, true>(p, w1, const_cast<float*>(a.z1part), B, R, blockIdx.x);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int h = blockIdx.x - nF;
-  const int tile = (4 * h) / 32;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(ctr + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < FC1_KSPLIT) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ull) {   // 60 s: report, do not hang
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
-  head_train_row<FC1_KSPLIT, IDX, true>(a, B, 4 * h + (threadIdx.x >> 6), threadIdx.x & 63);
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(hdone + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 32 / 4 - 1) {
-    __hip_atomic_store(ctr + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm (next launch)
-    __hip_atomic_store(hdone + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-bool fc1_head_fusable(int B) {
-  if (fc1_ksplit(B) != FC1_KSPLIT) return false;
-  const char* e = getenv("MNIST_AMD_FC1_MR");              // the fused form is fc1's MR = 2 tiling
-  if (e && atoi(e) != 2) return false;
-  // opt-in (MNIST_AMD_FUSE_HEAD=1): measured SLOWER at B = 200 - 600 steps 71.4 -> 76.4-77.3 us,
-  // the 20-step window 75.8-77.4 -> 82.3-83.3 (bitwise equal losses): the head workgroups wait for
-  // the LAST of their tile's 32 chunk workgroups and then read the partials with write-through
-  // visibility, which costs more than the kernel boundary it removes
-  const char* f = getenv("MNIST_AMD_FUSE_HEAD");
-  return f && f[0] == '1';
-}
-
-void launch_fc1_head_train(const uint16_t* p, const uint16_t* w1, const HeadArgs& a, int B, int Bp, int* ctr,
-                           int* hdone, int* err, hipStream_t s) {
-  const int R = (B + 31) / 32;
-  if (Bp != 32 * R || R > FC1_HEAD_MAX_TILES) throw std::runtime_error("fc1_head_train: bad batch");
-  const dim3 g(R * FC1_KSPLIT + Bp / 4), t(256);
-  if (a.idx) hipLaunchKernelGGL(fc1_head_train_kernel<true>, g, t, 0, s, p, w1, a, B, R, ctr, hdone, err);
-  else hipLaunchKernelGGL(fc1_head_train_kernel<false>, g, t, 0, s, p, w1, a, B, R, ctr, hdone, err);
+  head_train_row<KS, IDX>(a, B, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
 __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
@@ -491,21 +407,10 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B, train ? 1 : 0);
 }
 
-// rows (waves) per workgroup (MNIST_AMD_HEAD_WAVES, default 4).  Measured at B = 200: 1 row per
-// workgroup (224 WGs) 82.9 us/step, 2 rows 82.1, 4 rows 82.2 - spreading the rows over more CUs
-// does not pay; the head is bound by its per-row dependent latency chain.
-static int head_waves() {
-  static const int w = [] {
-    const char* e = getenv("MNIST_AMD_HEAD_WAVES");
-    const int v = e ? atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 4) ? v : 4;
-  }();
-  return w;
-}
-
+// 4 rows (waves) per workgroup: measured at B = 200 1 row per workgroup (224 WGs) 82.9 us/step,
+// 2 rows 82.1, 4 rows 82.2 - the head is bound by its per-row dependent latency chain
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {
-  const int w = Bp >= 2048 ? 4 : head_waves();   // (Bp is a multiple of 32)
-  const dim3 g(Bp / w), t(64 * w);
+  const dim3 g(Bp / 4), t(256);   // (Bp is a multiple of 32)
   if (fc1_ksplit(B) == FC1_KSPLIT) {
     if (a.idx) hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, true>), g, t, 0, s, a, B);
     else hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, false>), g, t, 0, s, a, B);
@@ -542,96 +447,6 @@ __device__ __forceinline__ int swz_row128(int row, int col) {   // 64 bf16 per r
   return (((col >> 4) ^ code) << 4) | (col & 15);
 }
 constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
-
-// Fused fc1 Adadelta (FcUpdate, single GPU, unsplit batch): the tile's final gradients are still in
-// the MFMA accumulators (lane: o = 32 wave + 16 mt + 4 g + r, i = i0 + 16 nt + (lane & 15)), so
-// the update reads p / sq / acc once, writes them back with the gradient, and the bf16 shadows
-// leave through two LDS transposes as whole 128-B (w1 rows) / 256-B (w1t rows) runs.
-__device__ __forceinline__ void fc_bwd_role_a_update(const FcBwdArgs& a, const floatx4 (&acc)[2][4], bool ones,
-                                                     int i0, unsigned char* smem) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
-  const FcUpdate& u = a.upd;
-  const Ada ad{u.rho, u.eps, u.weight_decay, *u.lr};
-  const float sc = a.grad_scale;
-  if (ones) {                                           // fc1.bias: column 0 of the ones-GEMM
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t e = OFF_FC1_B + 32 * wave + 16 * mt + 4 * g + r;
-          const float gv = acc[mt][0][r] * sc;
-          float p = u.param[e], sq = u.square_avg[e], ac = u.acc_delta[e];
-          ad.step(p, gv, sq, ac);
-          a.grad[e] = gv;
-          u.param[e] = p;
-          u.square_avg[e] = sq;
-          u.acc_delta[e] = ac;
-        }
-    }
-    return;
-  }
-  // The gradient tile goes through LDS once so that the update runs on whole 256-B row runs: thread
-  // (row group, c4) owns float4 column c4 of rows o = (tid >> 4) + 16 k (k = 0..7) - coalesced 16-B
-  // loads / stores of p, sq, acc, grad and 8-B bf16 w1 stores, instead of 4-B scattered accesses.
-  constexpr int GT_LD = 68, WTS_LD = 136;               // padded fp32 / bf16 rows (16-B aligned)
-  float* gt = reinterpret_cast<float*>(smem);                             // [128 o][64 i] fp32
-  uint16_t* wts = reinterpret_cast<uint16_t*>(smem);                      // [64 i][128 o] (after gt)
-  __syncthreads();                                      // the k-loop's LDS tiles are dead
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)                       // banks: 16 g + (lane & 15), conflict-free
-        gt[(32 * wave + 16 * mt + 4 * g + r) * GT_LD + 16 * nt + (lane & 15)] = acc[mt][nt][r] * sc;
-  __syncthreads();
-  const int c4 = tid & 15, orow = tid >> 4;
-  float4 pv[8];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {                         // 2 rounds of 12 x 16-B loads in flight
-    float4 sv[4], av[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t e = OFF_FC1_W + (int64_t)(orow + 16 * (4 * h + k)) * NFLAT + i0 + 4 * c4;
-      pv[4 * h + k] = *reinterpret_cast<const float4*>(u.param + e);
-      sv[k] = *reinterpret_cast<const float4*>(u.square_avg + e);
-      av[k] = *reinterpret_cast<const float4*>(u.acc_delta + e);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int o = orow + 16 * (4 * h + k);
-      const int64_t e = OFF_FC1_W + (int64_t)o * NFLAT + i0 + 4 * c4;
-      const float4 gv = *reinterpret_cast<const float4*>(gt + o * GT_LD + 4 * c4);
-      float4& p = pv[4 * h + k];
-      ad.step(p.x, gv.x, sv[k].x, av[k].x);
-      ad.step(p.y, gv.y, sv[k].y, av[k].y);
-      ad.step(p.z, gv.z, sv[k].z, av[k].z);
-      ad.step(p.w, gv.w, sv[k].w, av[k].w);
-      *reinterpret_cast<float4*>(a.grad + e) = gv;
-      *reinterpret_cast<float4*>(u.param + e) = p;
-      *reinterpret_cast<float4*>(u.square_avg + e) = sv[k];
-      *reinterpret_cast<float4*>(u.acc_delta + e) = av[k];
-      *reinterpret_cast<uint2*>(u.w1 + (int64_t)o * NFLAT + i0 + 4 * c4) = uint2{pack2bf(p.x, p.y), pack2bf(p.z, p.w)};
-    }
-  }
-  __syncthreads();                                      // gt is dead: the w1t transpose reuses it
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int o = orow + 16 * k;
-    wts[(4 * c4 + 0) * WTS_LD + o] = f2bf(pv[k].x);
-    wts[(4 * c4 + 1) * WTS_LD + o] = f2bf(pv[k].y);
-    wts[(4 * c4 + 2) * WTS_LD + o] = f2bf(pv[k].z);
-    wts[(4 * c4 + 3) * WTS_LD + o] = f2bf(pv[k].w);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {                         // w1t: 64 rows x 256 B (one 16 KB run)
-    const int c = tid + 256 * k, row = c >> 4, c16 = c & 15;
-    *reinterpret_cast<uint4*>(u.w1t_out + (int64_t)(i0 + row) * NH + c16 * 8) =
-        *reinterpret_cast<const uint4*>(wts + row * WTS_LD + c16 * 8);
-  }
-}
 
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
 // loaded into VGPRs while the current one (double-buffered LDS) feeds the MFMAs; one barrier per slab.
@@ -693,10 +508,6 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
         }
       }
     }
-  }
-  if (S == 1 && a.upd.param) {
-    fc_bwd_role_a_update(a, acc, ones, i0, smem);
-    return;
   }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -882,19 +693,7 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
     float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
     const float sc = (S == 1) ? a.grad_scale : 1.0f;
     const int64_t k = (c >= NCLS) ? -1 : (nt < 8) ? OFF_FC2_W + c * NH + 16 * nt + col : (col == 0) ? OFF_FC2_B + c : -1;
-    if (k >= 0) {
-      const float gv = s * sc;
-      dst[k] = gv;
-      if (S == 1 && a.upd.param) {                     // fused fc2 Adadelta (FcUpdate)
-        const FcUpdate& u = a.upd;
-        const Ada ad{u.rho, u.eps, u.weight_decay, *u.lr};
-        float p = u.param[k], sq = u.square_avg[k], ac = u.acc_delta[k];
-        ad.step(p, gv, sq, ac);
-        u.param[k] = p;
-        u.square_avg[k] = sq;
-        u.acc_delta[k] = ac;
-      }
-    }
+    if (k >= 0) dst[k] = s * sc;
   }
   if (wave == 0) {
     const int b_lo = sp * FC_BWD_SPLIT_ROWS, b_hi = min(B, b_lo + FC_BWD_SPLIT_ROWS);
@@ -917,24 +716,23 @@ __host__ __device__ inline int fc_bwd_role_b_wgs(int B) {
   return ((rows16 + mr - 1) / mr) * ROLE_B_SBLOCKS;
 }
 
-// order 0: [C | A | B] (one launch); order 1: [C | B | A] (two launches: C + B on the compute stream,
-// A on the comm stream)
+// workgroups [C | A | B]; bid0 offsets a partial grid (launch_fc_bwd_role)
 template <bool BIG>
-__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0, int order) {
+__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const int bid = blockIdx.x + bid0;
   const int S = fc_bwd_splits(B);
-  const int nA = S * ROLE_A_WGS, nB = fc_bwd_role_b_wgs(B);
+  const int nA = S * ROLE_A_WGS;
   // role C (long-running, one per split) first so it is dispatched before the short role-B tiles
   if (bid < S) {
     fc_bwd_role_c(a, B, Bp, bid, S, smem);
-  } else if (order == 0 ? bid < S + nA : bid >= S + nB) {
-    const int r = bid - S - (order == 0 ? 0 : nB);
+  } else if (bid < S + nA) {
+    const int r = bid - S;
     fc_bwd_role_a(a, B, Bp, r % ROLE_A_WGS, r / ROLE_A_WGS, S, smem);
   } else {
-    fc_bwd_role_b<BIG>(a, B, Bp, bid - S - (order == 0 ? nA : 0), fcb_mr(B), smem);
+    fc_bwd_role_b<BIG>(a, B, Bp, bid - S - nA, fcb_mr(B), smem);
   }
 }
 
@@ -970,8 +768,8 @@ void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
   const int S = fc_bwd_splits(B);
   if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
   const int grid = S + S * ROLE_A_WGS + fc_bwd_role_b_wgs(B);
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, 0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, 0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
   if (S > 1) {
     constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;
     hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
@@ -984,17 +782,8 @@ void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t
   const int nb = fc_bwd_role_b_wgs(B);
   const int grid = role == 0 ? S : role == 1 ? S * ROLE_A_WGS : nb;
   const int bid0 = role == 0 ? 0 : role == 1 ? S : S + S * ROLE_A_WGS;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
-}
-
-void launch_fc_bwd_part(const FcBwdArgs& a, int B, int Bp, int part, hipStream_t s) {
-  if (fc_bwd_splits(B) != 1) throw std::runtime_error("fc_bwd two-stream form needs B <= FC_BWD_SPLIT_ROWS");
-  const int nb = fc_bwd_role_b_wgs(B);
-  const int grid = part == 0 ? 1 + nb : ROLE_A_WGS;
-  const int bid0 = part == 0 ? 0 : 1 + nb;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 1);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 1);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
 }
 
 }  // namespace mnist

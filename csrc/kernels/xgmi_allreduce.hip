@@ -43,9 +43,10 @@
 //      observe the latest value in coherence order and is never served from L1.
 // R1 + R2 + R3: when the flag becomes visible at a peer, every payload byte is in the owner's HBM;
 // R1 + R4: the peer's loads read HBM, not a cached copy.  The fences stay available as knobs
-// (MNIST_AMD_XGMI_RELEASE=1: buffer_wbl2 sc0 sc1 before every flag, +13 us per world-1 step;
-// MNIST_AMD_XGMI_ACQUIRE=1: buffer_inv sc0 sc1 after every matched poll) and XgmiComm::ordering()
-// names the mode in use (bench JSON "xgmi_ordering").
+// (XgmiComm::set_fences: buffer_wbl2 sc0 sc1 before every flag, +13 us per world-1 step, and
+// buffer_inv sc0 sc1 after every matched poll - the trainer's fallback when the unfenced schedule
+// fails its cross-rank validation) and XgmiComm::ordering() names the mode in use (bench JSON
+// "xgmi_ordering").
 #include <stdexcept>
 #include <string>
 
@@ -80,17 +81,18 @@ __device__ bool xgmi_stage(const XgmiArgs& a, int stage, int b, int e, int kid) 
   bool ok = true;
   const int p = threadIdx.x;
   if (p < a.world) {
-    // optional system-scope release before the flag (XgmiArgs::release, MNIST_AMD_XGMI_RELEASE=1):
+    // optional system-scope release before the flag (XgmiArgs::release, XgmiComm::set_fences):
     // off by default - the payload stores are write-through (sc0 sc1) into uncached buckets and
     // drained above; the fence's L2 write-back costs ~13 us per world-1 step
     if (a.release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(a.flags[p] + (stage * XGMI_MAX_RANKS + a.rank) * XGMI_MAX_WG + b, e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const int* slot = a.flags[a.rank] + (stage * XGMI_MAX_RANKS + p) * XGMI_MAX_WG + b;
+    const uint64_t tmo = __hip_atomic_load(a.timeout_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();            // 100 MHz
     while (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
         int zero = 0;
         __hip_atomic_compare_exchange_strong(a.err, &zero, (kid << 24) | (stage << 16) | (p << 12) | b,
                                              __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -580,10 +582,11 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
   // which follows it on the compute stream, reads the new conv2 weights
   if (part.wait_a && b == 0 && tid == 0) {
     const int target = __hip_atomic_load(part.wait_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t tmo = __hip_atomic_load(a.timeout_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(part.wait_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
         __hip_atomic_store(part.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

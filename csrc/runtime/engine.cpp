@@ -23,15 +23,10 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
       comm_stream_(comm), world_(world_size), rho_(rho), eps_(eps), wd_(weight_decay) {
   if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_conv_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_w_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_c2_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_join2_, hipEventDisableTiming));
-  alloc_workspace();   // (the wgrad stream of the concurrent schedule is created on demand: every
-                       // stream may take a hardware queue, and queues are a shared resource)
+  alloc_workspace();
 }
 
 Engine::~Engine() {
@@ -45,19 +40,10 @@ Engine::~Engine() {
   }
   for (auto g : side_graphs_)
     if (g) hipGraphExecDestroy(g);
-  for (auto g : side2_graphs_)
-    if (g) hipGraphExecDestroy(g);
   for (auto g : graphs_) hipGraphExecDestroy(g);
   for (auto g : graph_defs_) hipGraphDestroy(g);
-  if (ev_fc_) hipEventDestroy(ev_fc_);
-  if (ev_conv_) hipEventDestroy(ev_conv_);
-  if (ev_done_) hipEventDestroy(ev_done_);
-  if (ev_w_) hipEventDestroy(ev_w_);
-  if (ev_c2_) hipEventDestroy(ev_c2_);
-  if (ev_fork_) hipEventDestroy(ev_fork_);
-  if (ev_join_) hipEventDestroy(ev_join_);
-  if (ev_join2_) hipEventDestroy(ev_join2_);
-  if (wgrad_stream_) hipStreamDestroy(wgrad_stream_);
+  for (hipEvent_t e : {ev_fc_, ev_done_, ev_fork_, ev_join_})
+    if (e) hipEventDestroy(e);
   if (ws_) hipFree(ws_);
 }
 
@@ -81,20 +67,8 @@ void Engine::alloc_workspace() {
   w2part_ = reinterpret_cast<float*>(base + L.w2part);
   fcpart_ = reinterpret_cast<float*>(base + L.fcpart);
   sync_ = reinterpret_cast<int*>(base + L.sync);
-  w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
   w2d_alt_ = reinterpret_cast<uint16_t*>(base + L.w2d_alt);
   c1red_ = reinterpret_cast<float*>(base + L.c1red);
-}
-
-void Engine::set_conv_split(bool on, uintptr_t conv2_stream) {
-  if (on && !conv2_stream) throw std::runtime_error("conv split needs a third stream");
-  conv_split_ = on;
-  conv2_stream_ = on ? reinterpret_cast<hipStream_t>(conv2_stream) : nullptr;
-}
-
-void Engine::set_concurrent(bool on) {
-  if (on && !wgrad_stream_) HIP_OK(hipStreamCreateWithFlags(&wgrad_stream_, hipStreamNonBlocking));
-  concurrent_ = on;
 }
 
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
@@ -102,19 +76,45 @@ void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
   comm_ = std::move(comm);
 }
 
-void Engine::attach_comm2(std::shared_ptr<RcclComm> comm) {
-  if (comm && comm->world_size() != world_) throw std::runtime_error("comm world size mismatch");
-  comm2_ = std::move(comm);
-}
-
 void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
   if (x && x->world_size() != world_) throw std::runtime_error("xgmi world size mismatch");
   if (x && x->world_size() > 1 && !x->connected()) throw std::runtime_error("xgmi communicator not connected");
   if (x && x->numel() != PARAM_TOTAL) throw std::runtime_error("xgmi communicator must cover the flat gradient");
+  if (x && x->channels() <= XGMI_CH_CONV2) throw std::runtime_error("xgmi communicator needs 3 channels");
+  if (!x && sched_ == XGMI) {           // no schedule until set_schedule (enqueue refuses SERIAL at world > 1)
+    sync_streams();
+    sched_ = SERIAL;
+  }
   if (!grad_own_) grad_own_ = buf_.grad;
   // the gradient producers write straight into the communicator's (IPC-exported) input buffer
   buf_.grad = x ? x->in() : grad_own_;
   xgmi_ = std::move(x);
+}
+
+void Engine::set_schedule(int s) {
+  if (s == SERIAL || s == OVERLAP) {
+    if (world_ != 1 || comm_ || xgmi_)
+      throw std::runtime_error("engine: the single-GPU schedules need world size 1 and no transport attached");
+  } else if (s == RCCL) {
+    if (!comm_) throw std::runtime_error("engine: the RCCL schedule needs an RCCL communicator");
+    if (xgmi_) throw std::runtime_error("engine: detach the xgmi communicator before selecting RCCL");
+  } else if (s == XGMI) {
+    if (!xgmi_) throw std::runtime_error("engine: the XGMI schedule needs an xgmi communicator");
+  } else {
+    throw std::runtime_error("engine: unknown schedule " + std::to_string(s));
+  }
+  sched_ = s;
+  reset_counters();
+}
+
+void Engine::reset_counters() {
+  // the hand-off counters only move in matched pairs inside a completed chunk; after a schedule
+  // change or an aborted chunk they restart from zero, and so does the hand-off error flag [2]
+  // (callers read it with check_errors before they get here)
+  sync_streams();
+  HIP_OK(hipMemsetAsync(sync_ + 0, 0, 5 * sizeof(int), compute_));
+  HIP_OK(hipStreamSynchronize(compute_));
+  reset_host_state();
 }
 
 void Engine::begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags) {
@@ -130,8 +130,7 @@ void Engine::phase_begin(const char* name) {
 void Engine::phase_end() {
   if (!trace_) return;
   HIP_OK(hipStreamSynchronize(compute_));
-  if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
-  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
+  HIP_OK(hipStreamSynchronize(comm_stream_));
   roctx_pop();
 }
 
@@ -157,7 +156,8 @@ void Engine::profile_steps(int n, int batch, int stride) {
 void Engine::enqueue_step(int batch, bool last) {
   // the head scales by 1/(B*world): without a transport every rank would train alone on a gradient
   // world times too small
-  if (world_ > 1 && !comm_ && !xgmi_) throw std::runtime_error("engine: world size > 1 but no communicator attached");
+  if (world_ > 1 && sched_ != RCCL && sched_ != XGMI)
+    throw std::runtime_error("engine: world size > 1 needs the RCCL or XGMI schedule");
   const int B = batch, Bp = round_up(B, 32);
   const int stride = idx_stride_;
   float* P = buf_.param;
@@ -166,10 +166,10 @@ void Engine::enqueue_step(int batch, bool last) {
   // world*B batch (scaling by 1/B and then by 1/world rounds the fp32 constant differently and flips
   // bf16 ties: a systematic ~7e-6 gradient offset, tools/ddp_equivalence.py)
   const float gscale = kDdpEpilogueScale;
-  // two-pass capture (capture_train): M = enqueue the compute-stream work, S = the side streams'
+  // split capture (capture_train_split): M = enqueue the compute-stream work, S = the comm stream's
   const bool M = enq_main_, S = enq_side_;
-  // conv2-stream work: its own pass when that stream is a third one, else part of the comm pass
-  const bool T = (conv2_stream_ && conv2_stream_ != comm_stream_) ? enq_side2_ : enq_side_;
+  const bool side = side_schedule();
+  const bool xg = sched_ == XGMI;
 
   // pre-gathered epoch rows when available (one load level less on every step's critical path)
   const bool pre = buf_.epoch_u8 != nullptr;
@@ -178,56 +178,31 @@ void Engine::enqueue_step(int batch, bool last) {
   const int32_t* labels = pre ? buf_.epoch_labels : buf_.train_labels;
   TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
-  // the direct xGMI all-reduce runs in schedule 3 (its two channels = the two RCCL communicators)
-  // single GPU with overlap_fc_update_: the same device-counter schedule without a communicator (the
-  // fc Adadelta step on the comm stream under the conv backward, the conv reduce + update in one launch)
-  const bool local3 = !comm_ && !xgmi_ && overlap_fc_update_ && !concurrent_;
-  const bool sched3 = ((comm_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3) || local3;
-  if (xgmi_ && !sched3 && !comm_) throw std::runtime_error("xgmi all-reduce needs DDP schedule 3 (or an RCCL comm)");
-  const bool split = sched3 && xgmi_ && xgmi_fuse_update_ && conv_split_ && xgmi_->channels() > XGMI_CH_CONV2;
-  if (sched3 && !side_forked_) {       // once per chunk: order the side streams after the chunk start
+  if (side && !side_forked_) {         // once per chunk: order the comm stream after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
-    if (split) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fc_, 0));
     side_forked_ = true;
   }
-  // schedule 2/3: the previous step's fc all-reduce + fc update must be done before fc1_fwd; in
-  // schedule 3 trunk_fwd itself holds its completion for it (device counters, no extra launch)
-  const bool hold = side_pending_ && sched3;
-  if (hold) {
+  // the previous step's fc update (comm stream) must be done before fc1_fwd reads w1: trunk_fwd
+  // holds its completion for it (device counters, no extra launch)
+  if (side && side_pending_) {
     tf.wait_a = sync_ + 1;
     tf.wait_b = sync_ + 0;
     tf.wait_err = sync_ + 2;
   }
+  side_pending_ = false;
   phase_begin("fwd");
   if (M) launch_trunk_fwd(tf, B, true, compute_);
-  if (side_pending_) {
-    if (!hold) HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-    side_pending_ = false;
-  }
-  const bool fuse_head = fc1_head_fusable(B);
-  if (M && !fuse_head) launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
+  if (M) launch_fc1_fwd(p_, buf_.w1, z1part_, B, compute_);
   HeadArgs ha{};
   ha.z1part = z1part_; ha.b_fc1 = P + OFF_FC1_B; ha.w_fc2 = P + OFF_FC2_W; ha.b_fc2 = P + OFF_FC2_B;
   ha.labels = labels; ha.idx = idxp; ha.idx_step_stride = stride;
   ha.state = buf_.state; ha.inv_batch = ddp_head_inv_batch(B, world_);
   ha.loss_rows = loss_rows_; ha.dz1 = dz1_; ha.h_bf = h_bf_; ha.dl_bf = dl_bf_;
-  if (M && fuse_head) launch_fc1_head_train(p_, buf_.w1, ha, B, Bp, sync_ + 16, sync_ + 32, sync_ + 2, compute_);
-  else if (M) launch_head_train(ha, B, Bp, compute_);
+  if (M) launch_head_train(ha, B, Bp, compute_);
   phase_end();
-  const bool dist = comm_ != nullptr || xgmi_ != nullptr;   // world_size 1 + comm: DDP schedule (tests)
-  // single GPU: fc_bwd applies the fc Adadelta step itself (FcUpdate).  Its role B reads the w1t
-  // the step started with while role A writes the updated one, so the transposed shadow alternates
-  // between buf_.w1t and w1t_alt_ (host-tracked, static within a captured chunk); a chunk that
-  // ends on the alternate copy copies it back, so buf_.w1t is current at every chunk boundary.
-  const bool fuse_fc = fuse_fc_update_ && !dist && !concurrent_ && fc_bwd_splits(B) == 1;
-  FcBwdArgs fb{dz1_, p_, pmask_, w1t_in_alt_ ? w1t_alt_ : buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state,
+  FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state,
                buf_.grad, dyc_, buf_.loss_log, gscale, 1.0f / (float)B, fcpart_};
-  if (fuse_fc) {
-    fb.upd = FcUpdate{P, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_, buf_.w1,
-                      w1t_in_alt_ ? buf_.w1t : w1t_alt_};
-    w1t_in_alt_ = !w1t_in_alt_;
-  }
   phase_begin("bwd_fc");
   if (M) launch_fc_bwd(fb, B, Bp, compute_);
   phase_end();
@@ -237,274 +212,157 @@ void Engine::enqueue_step(int batch, bool last) {
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
-  cb.c1_rows = (local3 && dgrad_update_) ? 4 * B : conv_dgrad_c1_rows(B);   // dgrad_update: 4-strip dgrad
-  if (cb.c1_rows > C1_PRE_MIN_SLABS && c1_prereduce_) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
+  cb.c1_rows = conv_dgrad_c1_rows(B);
+  if (cb.c1_rows > C1_PRE_MIN_SLABS) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
-  if (sched3) {
-    // xGMI: the reduced gradients land in the communicator's output buffer, the update reads there
-    if (xgmi_) ad.grad = adc.grad = xgmi_->out();
-    ConvBwdArgs cbs = cb;
-    cbs.signal_ctr = sync_ + 0;                              // wgrad signals: fc grads of this step final
+
+  if (sched_ == SERIAL) {
     phase_begin("bwd_conv_wgrad");
-    if (M) launch_conv_wgrad(cbs, B, compute_);
+    launch_conv_wgrad(cb, B, compute_);
+    phase_end();
+    phase_begin("bwd_conv_dgrad");
+    launch_conv_dgrad(cb, B, compute_);
+    phase_end();
+    phase_begin("grad_reduce+update");          // conv slab reduce + the whole Adadelta update
+    launch_adadelta_reduce(adc, cb, B, compute_);
+    phase_end();
+    return;
+  }
+
+  if (sched_ == RCCL) {
+    if (!two_buckets_) {                        // one bucket: one all-reduce after the whole backward
+      launch_conv_wgrad(cb, B, compute_);
+      launch_conv_dgrad(cb, B, compute_);
+      launch_conv_grad_reduce(cb, B, compute_);
+      comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
+      launch_adadelta(adc, ADA_ALL, compute_);
+      return;
+    }
+    // the fc bucket (98.4 % of the bytes) forks onto the comm stream as soon as fc_bwd is done and
+    // overlaps the conv backward; the conv bucket follows on compute after the join, so the one
+    // communicator sees fc, conv in the same order on every rank and never two collectives at once.
+    // (capture order matters: the graph executor keeps a fork's first-captured child on the
+    // launching queue, so conv2 wgrad is enqueued before the comm branch)
+    HIP_OK(hipEventRecord(ev_fc_, compute_));
+    phase_begin("bwd_conv_wgrad");
+    launch_conv_wgrad(cb, B, compute_);
     phase_end();
     phase_begin("allreduce_fc+update");
-    if (S) launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
-    if (!S) {
-    } else if (xgmi_ && xgmi_fuse_update_) {   // fc bucket all-reduce with the fc Adadelta step fused
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    launch_adadelta(ad, ADA_FC, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    phase_end();
+    phase_begin("bwd_conv_dgrad");
+    launch_conv_dgrad(cb, B, compute_);
+    phase_end();
+    phase_begin("allreduce_conv+update");
+    launch_conv_grad_reduce(cb, B, compute_);
+    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
+    launch_adadelta(adc, ADA_CONV, compute_);
+    phase_end();
+    return;
+  }
+
+  // ---- OVERLAP / XGMI: device-counter hand-offs between the compute and comm streams
+  if (xg) ad.grad = adc.grad = xgmi_->out();    // the update reads the all-reduced gradients
+  ConvBwdArgs cbs = cb;
+  cbs.signal_ctr = sync_ + 0;                     // wgrad's start: fc grads of this step are final
+  phase_begin("bwd_conv_wgrad");
+  if (M) launch_conv_wgrad(cbs, B, compute_);
+  phase_end();
+  phase_begin("allreduce_fc+update");
+  if (S) {
+    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    if (!xg) {
+      launch_adadelta(ad, ADA_FC, comm_stream_);
+    } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
-      if (xgmi_) {
-        xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
-      } else if (comm2_) {             // opt-in second communicator: may overlap comm_'s conv all-reduce
-        comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-      } else if (comm_) {
-        // one communicator for both buckets (DDP's single process group): the fc all-reduce runs here
-        // and publishes its completion in sync_[12]; the compute stream's conv all-reduce waits for
-        // it, so the communicator never has two collectives in flight and every rank issues them in
-        // the same order (fc, conv)
-        comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-        launch_stream_signal(sync_ + 12, comm_stream_);
-      }
+      xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
     }
-    if (S) launch_stream_signal(sync_ + 1, comm_stream_);    // fc update of this step done
+    launch_stream_signal(sync_ + 1, comm_stream_);   // fc update of this step done
+  }
+  phase_end();
+  side_pending_ = true;
+  if (xg && !xgmi_fuse_update_) {
+    // separate launches (reference for the fused kernels' bits): the conv bucket after dgrad
+    phase_begin("bwd_conv_dgrad");
+    if (M) launch_conv_dgrad(cb, B, compute_);
     phase_end();
-    side_pending_ = true;
-    if (split) {
-      // conv2 part: released by dgrad's start (= wgrad done), reduced / exchanged / updated on the
-      // third stream under dgrad; counters [3] conv2 updates published, [4] dgrad starts.  This
-      // step's dgrad reads the conv2 weights' dgrad-layout shadow while the update runs, so the
-      // update writes the OTHER copy (w2d ping-pong, host-tracked like w1t's; a chunk that ends on
-      // the alternate copy copies it back)
-      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
-      uint16_t* w2d_next = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
-      AdadeltaArgs ad2 = adc;
-      ad2.state_inc = nullptr;
-      ad2.w2d = w2d_next;
-      cb.w2d = w2d_cur;
-      if (T) {
-        launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, conv2_stream_);
+    phase_begin("allreduce_conv+update");
+    if (M) {
+      launch_conv_grad_reduce(cb, B, compute_);
+      xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);
+      launch_adadelta(adc, ADA_CONV, compute_);
+    }
+    phase_end();
+  } else {
+    // conv2's slab reduce (+ exchange) + update on the comm stream after the fc update, released by
+    // dgrad's start (= wgrad done, counter [4]) and running under conv2_dgrad, which reads this step's
+    // w2d while the update writes the other copy (ping-pong, host-tracked and static within a
+    // captured chunk; a chunk that ends on the alternate copy copies it back); counter [3] = conv2
+    // updates published.  Only conv1's part (20 reduce workgroups) stays on the compute stream, and
+    // that launch holds its completion until [3] catches up, so the next trunk_fwd reads the new
+    // conv2 weights.
+    uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
+    AdadeltaArgs u2 = adc;
+    u2.state_inc = nullptr;
+    u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
+    cb.w2d = w2d_cur;
+    if (S) {
+      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+      if (xg) {
         XgmiConvPart p2;
         p2.lo = 0;
         p2.hi = RED_W2_PARTS;
-        xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, conv2_stream_, ad2, p2);
-        launch_stream_signal(sync_ + 3, conv2_stream_);
+        xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, comm_stream_, u2, p2);
+      } else {
+        launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
       }
-      ConvBwdArgs cbd = cb;
-      cbd.signal_ctr = sync_ + 4;
-      phase_begin("bwd_conv_dgrad");
-      if (M) launch_conv_dgrad(cbd, B, compute_);
-      phase_end();
-      phase_begin("allreduce_conv+update");
+      launch_stream_signal(sync_ + 3, comm_stream_);
+    }
+    ConvBwdArgs cbd = cb;
+    cbd.signal_ctr = sync_ + 4;
+    phase_begin("bwd_conv_dgrad");
+    if (M) launch_conv_dgrad(cbd, B, compute_);
+    phase_end();
+    phase_begin("allreduce_conv1+update");
+    if (M && xg) {
       XgmiConvPart p1;
       p1.lo = RED_W2_PARTS;
       p1.hi = RED_ALL_PARTS;
       p1.wait_a = sync_ + 3;
       p1.wait_b = sync_ + 4;
       p1.wait_err = sync_ + 2;
-      if (M) xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
-      phase_end();
-      w2d_in_alt_ = !w2d_in_alt_;
-      if (last) {
-        if (M && !skip_join_) {            // (split capture: the replay's join event covers it)
-          HIP_OK(hipEventRecord(ev_c2_, conv2_stream_));
-          HIP_OK(hipStreamWaitEvent(compute_, ev_c2_, 0));
-        }
-        if (w2d_in_alt_) {
-          if (M)
-            HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
-                                  compute_));
-          w2d_in_alt_ = false;
-        }
-      }
-    } else if (local3 && side_conv2_) {
-      // single GPU: conv2's slab reduce + update on the comm stream (after the fc update), released by
-      // dgrad's start (= wgrad done, counter [4]) and running under conv2_dgrad, which reads this
-      // step's w2d while the update writes the other copy (ping-pong, as the split path); counter [3]
-      // = conv2 updates published.  Only conv1's 20 reduce workgroups stay on the compute stream, and
-      // that launch holds its completion until [3] catches up, so the next trunk_fwd reads the new
-      // conv2 weights.
-      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
-      AdadeltaArgs u2 = adc;
-      u2.state_inc = nullptr;
-      u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
-      cb.w2d = w2d_cur;
-      if (S) {
-        launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
-        launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
-        launch_stream_signal(sync_ + 3, comm_stream_);
-      }
-      ConvBwdArgs cbd = cb;
-      cbd.signal_ctr = sync_ + 4;
-      phase_begin("bwd_conv_dgrad");
-      if (M) launch_conv_dgrad(cbd, B, compute_);
-      phase_end();
-      phase_begin("conv1_update");
+      xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc, p1);
+    } else if (M) {
       AdadeltaArgs u1 = adc;
       u1.hold_a = sync_ + 3;
       u1.hold_b = sync_ + 4;
       u1.hold_err = sync_ + 2;
-      if (M) launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
-      phase_end();
-      w2d_in_alt_ = !w2d_in_alt_;
-      if (last && w2d_in_alt_) {
-        if (M)
-          HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
-                                compute_));
-        w2d_in_alt_ = false;
-      }
-    } else if (local3 && dgrad_update_) {
-      // single GPU: conv2's reduce + update inside the dgrad launch (it reads this step's w2d while
-      // the update writes the other copy: ping-pong as in the split path), conv1's after it
-      uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
-      AdadeltaArgs u = adc;
-      u.state_inc = nullptr;
-      u.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
-      cb.w2d = w2d_cur;
-      phase_begin("bwd_conv_dgrad+conv2_update");
-      if (M) launch_conv_dgrad_update(cb, u, B, compute_);
-      phase_end();
-      phase_begin("conv1_update");
-      if (M) launch_adadelta_reduce_parts(adc, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
-      phase_end();
-      w2d_in_alt_ = !w2d_in_alt_;
-      if (last && w2d_in_alt_) {
-        if (M) HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+      launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+    }
+    phase_end();
+    w2d_in_alt_ = !w2d_in_alt_;
+    if (last && w2d_in_alt_) {
+      if (M)
+        HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
                               compute_));
-        w2d_in_alt_ = false;
-      }
-    } else {
-    phase_begin("bwd_conv_dgrad");
-    if (M) launch_conv_dgrad(cb, B, compute_);
-    phase_end();
-    phase_begin("allreduce_conv+update");
-    if (!M) {
-    } else if (xgmi_ && xgmi_fuse_update_) {   // conv bucket: slab reduce + all-reduce + Adadelta in one launch
-      xgmi_->conv_reduce_fused(XGMI_CH_CONV, cb, B, compute_, adc);
-    } else if (local3) {             // single GPU: conv slab reduce + conv Adadelta in one launch
-      launch_adadelta_reduce(adc, cb, B, true, compute_);
-    } else if (xgmi_) {              // separate launches (reference for the fused kernels' bits)
-      launch_conv_grad_reduce(cb, B, compute_);
-      xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_);
-      launch_adadelta(adc, ADA_CONV, compute_);
-    } else {
-      launch_conv_grad_reduce(cb, B, compute_);
-      // single communicator: this step's fc all-reduce (comm stream) has finished before the conv
-      // one starts (sync_[12] >= sync_[0]: both count this step; usually already true - the fc
-      // bucket is reduced under conv2_dgrad)
-      if (!comm2_) launch_stream_wait(sync_ + 12, sync_ + 0, 0, sync_ + 2, compute_);
-      comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
-      launch_adadelta(adc, ADA_CONV, compute_);
+      w2d_in_alt_ = false;
     }
-    phase_end();
-    }
-    if (last) {                                              // chunk end: one real join edge
-      if (M && !skip_join_) {
-        HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-        HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-      }
-      side_pending_ = false;
-      side_forked_ = false;
-    }
-    return;
   }
-  if (dist && comm2_ && two_buckets_ && !concurrent_ && dist_sched_ == 2) {
-    // Cross-step overlap: the fc bucket (fc1.w/b, fc2.w/b = 98.4 % of the bytes) is all-reduced on
-    // its own communicator and updated on the comm stream while the compute stream runs the conv
-    // backward, the conv-bucket all-reduce (first communicator) + conv update, and the next step's
-    // trunk_fwd - which reads only conv weights.  The join sits right before the next fc1_fwd (or
-    // at the end of the captured chunk).  Two communicators because RCCL ops of one communicator
-    // must not be in flight concurrently on two streams.
-    HIP_OK(hipEventRecord(ev_fc_, compute_));
-    launch_conv_wgrad(cb, B, compute_);                 // first-captured child stays on this queue
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
-    comm2_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    side_pending_ = true;
-    launch_conv_dgrad(cb, B, compute_);
-    launch_conv_grad_reduce(cb, B, compute_);
-    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
-    launch_adadelta(adc, ADA_CONV, compute_);
-    if (last) {
+  if (last) {                                              // chunk end: one real join edge
+    if (M && !skip_join_) {
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-      side_pending_ = false;
     }
-    return;
+    side_pending_ = false;
+    side_forked_ = false;
   }
-  if (dist && two_buckets_ && !concurrent_ && dist_sched_ >= 1) {
-    // Every cross-queue edge costs ~5-10 us of signal latency, so the critical path (conv backward,
-    // conv bucket, conv update) never leaves the compute queue; only the fc bucket (98.4 % of the
-    // bytes) forks onto the comm stream, and the join is on an edge that has long completed.
-    // (capture order matters: the graph executor keeps a fork's first-captured child on the
-    // launching queue, so conv2 wgrad is enqueued before the comm branch)
-    HIP_OK(hipEventRecord(ev_fc_, compute_));
-    launch_conv_wgrad(cb, B, compute_);
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
-    comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    launch_conv_dgrad(cb, B, compute_);
-    launch_conv_grad_reduce(cb, B, compute_);
-    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));   // also orders the two all-reduces
-    comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
-    launch_adadelta(adc, ADA_CONV, compute_);
-    return;
-  }
-  // serial mode keeps every kernel of the optimizer / wgrad branches on the compute stream
-  hipStream_t ws = concurrent_ ? wgrad_stream_ : compute_;
-  hipStream_t ms = (concurrent_ || dist) ? comm_stream_ : compute_;
-  // fork: the fc bucket (98.4 % of the bytes) is complete; conv2 wgrad and the fc optimizer branch off
-  HIP_OK(hipEventRecord(ev_fc_, compute_));
-  if (ws != compute_) HIP_OK(hipStreamWaitEvent(ws, ev_fc_, 0));
-  if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_fc_, 0));
-  // single GPU, serial schedule: one fused Adadelta launch over everything at the end of the step
-  const bool one_update = !dist && !concurrent_;
-  if (!one_update && (two_buckets_ || !dist)) {
-    if (dist) comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, ms);
-    launch_adadelta(ad, ADA_FC, ms);
-  }
-  phase_begin("bwd_conv_wgrad");
-  launch_conv_wgrad(cb, B, ws);
-  if (ws != compute_) HIP_OK(hipEventRecord(ev_w_, ws));
-  phase_end();
-  phase_begin("bwd_conv_dgrad");
-  launch_conv_dgrad(cb, B, compute_);
-  if (ws != compute_) HIP_OK(hipStreamWaitEvent(compute_, ev_w_, 0));
-  phase_end();
-  if (one_update) {                     // single GPU: slab reduce + (conv or full) Adadelta in one launch
-    phase_begin("grad_reduce+update");
-    launch_adadelta_reduce(adc, cb, B, fuse_fc, compute_);
-    phase_end();
-    if (last && w1t_in_alt_) {
-      HIP_OK(hipMemcpyAsync(buf_.w1t, w1t_alt_, (size_t)NFLAT * NH * sizeof(uint16_t), hipMemcpyDeviceToDevice,
-                            compute_));
-      w1t_in_alt_ = false;
-    }
-    return;
-  }
-  launch_conv_grad_reduce(cb, B, compute_);
-  HIP_OK(hipEventRecord(ev_conv_, compute_));
-  if (ms != compute_) HIP_OK(hipStreamWaitEvent(ms, ev_conv_, 0));
-  if (dist && !two_buckets_) {
-    comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, ms);
-    launch_adadelta(adc, ADA_ALL, ms);
-  } else {
-    if (dist) comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, ms);
-    launch_adadelta(adc, ADA_CONV, ms);
-  }
-  if (ms != compute_) {
-    HIP_OK(hipEventRecord(ev_done_, ms));
-    HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-  }
-}
-
-bool Engine::uses_side_streams() const {
-  // the schedule-3 family (device-counter hand-offs to the comm / conv2 streams), as enqueue_step decides it
-  const bool local3 = !comm_ && !xgmi_ && overlap_fc_update_ && !concurrent_;
-  return ((comm_ || xgmi_) && two_buckets_ && !concurrent_ && dist_sched_ == 3) || local3;
 }
 
 void Engine::train_steps(int n, int batch, int stride) {
@@ -517,33 +375,14 @@ void Engine::train_steps(int n, int batch, int stride) {
 int Engine::capture_train(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
-  // RCCL side chains stay in ONE graph: launched as a separate side graph, the RCCL schedule ran
-  // 340 us per world-1 step instead of 101 (measured on the box; the xGMI and single-GPU side chains
-  // gain from the split: 100 -> 86 / 95 -> 77 us over a 20-step window)
-  static const bool rccl_split = [] { const char* e = getenv("MNIST_AMD_RCCL_SPLIT"); return e && e[0] == '1'; }();
-  const bool rccl_side = comm_ && !xgmi_ && !rccl_split;
-  if (side_first_ && uses_side_streams() && !rccl_side) return capture_train_split(n, batch);
+  if (side_schedule()) return capture_train_split(n, batch);
+  // SERIAL / RCCL: one graph, steps in order (RCCL: the communicator's collectives are captured in
+  // the order every rank issues them - fc, conv, fc, ... - so RCCL's own ordering of one
+  // communicator's kernels across streams can never chain a collective behind a later step's)
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(compute_, hipStreamCaptureModeRelaxed));
   try {
-    if (side_first_ && uses_side_streams()) {
-      // one graph, two passes: the side-stream nodes are created first, then the compute chain (the
-      // runtime submits a multi-stream graph's branches one after the other, in creation order:
-      // 120 -> 101 us per step for the RCCL schedule over a 20-step window)
-      const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
-      enq_main_ = false;
-      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
-      side_pending_ = sp;
-      w1t_in_alt_ = w1;
-      w2d_in_alt_ = w2;
-      side_forked_ = true;                 // the fork (chunk start -> side streams) is captured
-      enq_main_ = true;
-      enq_side_ = false;
-      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
-      enq_side_ = true;
-    } else {
-      for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
-    }
+    for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
   } catch (...) {
     reset_host_state();
     hipStreamEndCapture(compute_, &g);
@@ -562,90 +401,75 @@ int Engine::capture_train(int n, int batch, int stride) {
 }
 
 void Engine::reset_host_state() {
-  enq_main_ = enq_side_ = enq_side2_ = true;
+  enq_main_ = enq_side_ = true;
   skip_join_ = false;
   side_pending_ = false;
   side_forked_ = false;
-  w1t_in_alt_ = false;
   w2d_in_alt_ = false;
 }
 
-// Schedule-3 chunks as TWO graphs: the side chain (comm stream: per step a counter wait, the fc
-// all-reduce / Adadelta step, a counter signal) and the compute chain, captured in two passes over
-// the same steps (host state - ping-pong shadows, the pending hand-off - replayed identically) and
-// launched concurrently from two host threads (replay()).  One multi-stream graph submitted its
-// side branch only after the whole compute branch (~3.6 us of host time per node), so after every
-// host sync the second step's trunk_fwd sat ~0.45 ms (20-step chunk) on the device counter the
-// side chain had not yet reached the queue to signal: the driver's 20-step bench window read
-// 93-97 us/step against 73.5 steady state.  The fork (chunk start -> comm stream) and the join
+// OVERLAP / XGMI chunks as TWO graphs: the side chain (comm stream: per step counter waits, the fc
+// update or all-reduce, the conv2 part, counter signals) and the compute chain, captured in two
+// passes over the same steps (host state - the w2d ping-pong, the pending hand-off - replayed
+// identically) and launched concurrently from two host threads (replay()).  One multi-stream graph
+// submitted its side branch only after the whole compute branch (~3.6 us of host time per node), so
+// after every host sync the second step's trunk_fwd sat ~0.45 ms (20-step chunk) on the device
+// counter the side chain had not yet reached the queue to signal: the driver's 20-step bench window
+// read 93-97 us/step against 73.5 steady state.  The fork (chunk start -> comm stream) and the join
 // (comm stream -> compute) become two events at replay.
 int Engine::capture_train_split(int n, int batch) {
-  // xGMI conv bucket split on a third stream: its chain (conv2 reduce + exchange + update, released
-  // by conv2_dgrad's start) is a third graph, so it starts under dgrad instead of queueing behind
-  // the fc bucket on the comm stream
-  const bool third = conv2_stream_ && conv2_stream_ != comm_stream_ && xgmi_ && xgmi_fuse_update_ && conv_split_ &&
-                     xgmi_->channels() > XGMI_CH_CONV2;
-  const bool sp = side_pending_, w1 = w1t_in_alt_, w2 = w2d_in_alt_;
-  hipGraph_t gs = nullptr, g2 = nullptr, gm = nullptr;
-  auto pass = [&](hipStream_t s, bool m, bool side, bool side2, hipGraph_t* out) {
+  const bool sp = side_pending_, w2 = w2d_in_alt_;
+  hipGraph_t gs = nullptr, gm = nullptr;
+  auto pass = [&](hipStream_t s, bool m, bool side, hipGraph_t* out) {
     side_pending_ = sp;
-    w1t_in_alt_ = w1;
     w2d_in_alt_ = w2;
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;
     enq_side_ = side;
-    enq_side2_ = side2;
     skip_join_ = true;
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
     HIP_OK(hipStreamEndCapture(s, out));
   };
   try {
-    pass(comm_stream_, false, true, false, &gs);
-    if (third) pass(conv2_stream_, false, false, true, &g2);
-    pass(compute_, true, false, false, &gm);
-    enq_main_ = enq_side_ = enq_side2_ = true;
+    pass(comm_stream_, false, true, &gs);
+    pass(compute_, true, false, &gm);
+    enq_main_ = enq_side_ = true;
     skip_join_ = false;
   } catch (...) {
     reset_host_state();
     hipStreamCaptureStatus st;
-    for (hipStream_t s : {comm_stream_, conv2_stream_, compute_}) {
+    for (hipStream_t s : {comm_stream_, compute_}) {
       hipGraph_t junk = nullptr;
-      if (s && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
-        hipStreamEndCapture(s, &junk);
+      if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive) hipStreamEndCapture(s, &junk);
       if (junk) hipGraphDestroy(junk);
     }
-    for (hipGraph_t g : {gs, g2, gm})
+    for (hipGraph_t g : {gs, gm})
       if (g) hipGraphDestroy(g);
     throw;
   }
-  hipGraphExec_t xs = nullptr, x2 = nullptr, xm = nullptr;
+  hipGraphExec_t xs = nullptr, xm = nullptr;
   HIP_OK(hipGraphInstantiate(&xs, gs, nullptr, nullptr, 0));
-  if (g2) HIP_OK(hipGraphInstantiate(&x2, g2, nullptr, nullptr, 0));
   HIP_OK(hipGraphInstantiate(&xm, gm, nullptr, nullptr, 0));
   graph_defs_.push_back(gs);
-  if (g2) graph_defs_.push_back(g2);
   graph_defs_.push_back(gm);
   graphs_.push_back(xm);
   side_graphs_.push_back(xs);
-  side2_graphs_.resize(graphs_.size(), nullptr);
-  side2_graphs_.back() = x2;
   return (int)graphs_.size() - 1;
 }
 
 // --- side-graph launcher thread: hipGraphLaunch(side, comm stream) + the join event, concurrently
-// with the compute graph's launch on the calling thread
+// with the compute graph's launch on the calling thread (measured 20-step window, single GPU: 75.8
+// vs 78.9 us/step launching both from the calling thread)
 void Engine::side_worker() {
   std::unique_lock<std::mutex> lk(side_mu_);
   for (;;) {
     side_cv_.wait(lk, [this] { return side_stop_ || side_job_ != nullptr; });
     if (side_stop_) return;
-    hipGraphExec_t job = side_job_, job2 = side2_job_;
+    hipGraphExec_t job = side_job_;
     lk.unlock();
     hipError_t e = hipGraphLaunch(job, comm_stream_);
     if (e == hipSuccess) e = hipEventRecord(ev_join_, comm_stream_);
-    if (e == hipSuccess && job2) e = hipGraphLaunch(job2, conv2_stream_);
-    if (e == hipSuccess && job2) e = hipEventRecord(ev_join2_, conv2_stream_);
     lk.lock();
     side_err_ = e;
     side_job_ = nullptr;
@@ -668,28 +492,12 @@ void Engine::replay(int id) {
     HIP_OK(hipGraphLaunch(graphs_[id], compute_));
     return;
   }
-  hipGraphExec_t side2 = id < (int)side2_graphs_.size() ? side2_graphs_[id] : nullptr;
-  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chains ordered after earlier compute work
+  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chain ordered after earlier compute work
   HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
-  if (side2) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fork_, 0));
-  static const bool threaded = [] { const char* e = getenv("MNIST_AMD_SIDE_THREAD"); return !(e && e[0] == '0'); }();
-  if (!threaded) {                                      // (A/B knob) side graphs first, same thread
-    HIP_OK(hipGraphLaunch(side, comm_stream_));
-    HIP_OK(hipEventRecord(ev_join_, comm_stream_));
-    if (side2) {
-      HIP_OK(hipGraphLaunch(side2, conv2_stream_));
-      HIP_OK(hipEventRecord(ev_join2_, conv2_stream_));
-    }
-    HIP_OK(hipGraphLaunch(graphs_[id], compute_));
-    HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));
-    if (side2) HIP_OK(hipStreamWaitEvent(compute_, ev_join2_, 0));
-    return;
-  }
   {
     std::lock_guard<std::mutex> lk(side_mu_);
     if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
     side_job_ = side;
-    side2_job_ = side2;
     side_done_ = false;
   }
   side_cv_.notify_all();
@@ -702,8 +510,7 @@ void Engine::replay(int id) {
   }
   HIP_OK(em);
   HIP_OK(es);
-  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain(s)
-  if (side2) HIP_OK(hipStreamWaitEvent(compute_, ev_join2_, 0));
+  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain
 }
 
 void Engine::enqueue_eval(int n_total, int batch) {
@@ -772,13 +579,7 @@ bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
   return err == 0;
 }
 
-bool Engine::probe_stream_handoff(double timeout_s) {
-  if (!probe_stream_pair(compute_, comm_stream_, timeout_s)) return false;
-  if (conv2_stream_ && conv2_stream_ != comm_stream_ && (!probe_stream_pair(compute_, conv2_stream_, timeout_s) ||
-                        !probe_stream_pair(comm_stream_, conv2_stream_, timeout_s)))
-    return false;
-  return true;
-}
+bool Engine::probe_stream_handoff(double timeout_s) { return probe_stream_pair(compute_, comm_stream_, timeout_s); }
 
 std::pair<int, int> Engine::errors() const {
   int err = 0;
@@ -796,7 +597,7 @@ std::string Engine::describe_xgmi_error(int code) {
 
 void Engine::check_errors() const {
   const auto e = errors();
-  if (e.first) throw std::runtime_error("engine: a schedule-3 stream hand-off timed out (results invalid)");
+  if (e.first) throw std::runtime_error("engine: a stream hand-off timed out (results invalid)");
   if (e.second)
     throw std::runtime_error("engine: an xGMI all-reduce stage timed out (results invalid): " +
                              describe_xgmi_error(e.second));
@@ -804,9 +605,7 @@ void Engine::check_errors() const {
 
 void Engine::sync_streams() {
   HIP_OK(hipStreamSynchronize(compute_));
-  if (comm_stream_) HIP_OK(hipStreamSynchronize(comm_stream_));
-  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
-  if (wgrad_stream_) HIP_OK(hipStreamSynchronize(wgrad_stream_));
+  HIP_OK(hipStreamSynchronize(comm_stream_));
 }
 
 void Engine::synchronize() {

@@ -1,19 +1,25 @@
 // Native training/eval step engine for the MNIST CNN on one MI355X.
 //
 // This is the hot loop of reference mnist_ddp.py:65-86 (train) and :89-105 (test) re-designed
-// for the GPU: the dataset is HBM resident, every step is a fixed sequence of 8 hand-written
-// kernels (no host work, no sync), DDP gradient averaging is an RCCL all-reduce per gradient
-// bucket on a second stream overlapped with the remaining backward kernels, and whole chunks of
-// steps are captured once into a hipGraph and replayed (launch overhead amortised to ~0).
+// for the GPU: the dataset is HBM resident, every step is a fixed sequence of hand-written kernels
+// (no host work, no sync), and whole chunks of steps are captured once into hipGraphs and replayed.
 //
-// Per training step: three streams whose cross-stream events become parallel branches of the
-// captured graph (compute C, wgrad W, comm/optimizer M):
-//   C: trunk_fwd -> fc1_fwd -> head_train -> fc_bwd -ev_fc-> conv2_dgrad -(wait ev_w)-> reduce -ev_conv->
-//   W:                                          wait ev_fc: conv2_wgrad -ev_w->
-//   M:                                          wait ev_fc: [allreduce(fc bucket)] -> adadelta(fc)
-//                                               wait ev_conv: [allreduce(conv bucket)] -> adadelta(conv, step++) -ev_done-> C
-// The fc-bucket all-reduce + its Adadelta update (98.4 % of parameters) overlap the whole conv
-// backward; conv2 wgrad overlaps conv2 dgrad.  With world_size == 1 the all-reduces are skipped.
+// Schedules (set_schedule; C = compute stream, M = comm stream, [k] = device counter sync_[k]):
+//   SERIAL   (single GPU, fallback)  C: trunk, fc1, head, fc_bwd, wgrad, dgrad, reduce+update(all)
+//   OVERLAP  (single GPU, default)   C: trunk(hold [1]>=[0]), fc1, head, fc_bwd, wgrad(+[0]),
+//                                       dgrad(+[4]), conv1 reduce+update(hold [3]>=[4])
+//                                    M: wait [0]: fc update, +[1]; wait [4]: conv2 reduce+update, +[3]
+//   RCCL     (DDP over RCCL)         C: trunk, fc1, head, fc_bwd -ev_fc-> wgrad, dgrad, conv reduce,
+//                                       (wait ev_done) all-reduce(conv), update(conv)
+//                                    M: (wait ev_fc) all-reduce(fc), update(fc) -ev_done->
+//                                    one communicator, collectives issued and run in step order fc ->
+//                                    conv (graph edges, no device counters): one graph per chunk
+//   XGMI     (DDP over the direct xGMI kernels) the OVERLAP structure with the all-reduces fused in:
+//                                    M: fc all-reduce+update (xgmi_fc_fused), conv2 reduce+all-reduce+
+//                                    update; C: conv1 reduce+all-reduce+update (fuse off: separate
+//                                    all-reduce / update launches, conv bucket after dgrad on C)
+// OVERLAP and XGMI chunks are captured as two graphs (M chain, C chain) launched concurrently from two
+// host threads (capture_train_split); a chunk's first fork and last join are replay events.
 #pragma once
 #include <stdlib.h>
 #include <hip/hip_runtime.h>
@@ -65,58 +71,28 @@ class Engine {
          hipStream_t comm, int world_size, float rho, float eps, float weight_decay);
   ~Engine();
 
-  void attach_comm(std::shared_ptr<RcclComm> comm);   // enables the overlapped DDP path
-  // optional second communicator for the fc bucket (opt-in, MNIST_AMD_RCCL_COMMS=2): its all-reduce
-  // may then overlap the conv bucket's on the first.  Concurrent collectives on two communicators are
-  // deadlock-prone in NCCL/RCCL, so by default schedule 3 runs both buckets on ONE communicator,
-  // ordered fc -> conv by a device counter (see enqueue_step)
-  void attach_comm2(std::shared_ptr<RcclComm> comm);
-  // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC over x->in() -> x->out()) in place
-  // of the RCCL all-reduces of schedule 3; while attached the gradient producers write x->in()
-  // instead of buf.grad; RCCL stays attached for the parameter broadcast
+  enum Schedule : int { SERIAL = 0, OVERLAP = 1, RCCL = 2, XGMI = 3 };
+  void attach_comm(std::shared_ptr<RcclComm> comm);   // RCCL schedule transport (+ parameter broadcast)
+  // direct xGMI all-reduce (channels XGMI_CH_CONV / XGMI_CH_FC / XGMI_CH_CONV2 over x->in() -> x->out());
+  // while attached the gradient producers write x->in() instead of buf.grad
   void attach_xgmi(std::shared_ptr<XgmiComm> x);
   static constexpr int XGMI_CH_CONV = 0, XGMI_CH_FC = 1, XGMI_CH_CONV2 = 2;
-  // xGMI fused schedule, conv bucket split (needs a 3-channel communicator and a third stream that
-  // passes probe_stream_handoff): conv2.weight/bias (98 % of the conv bucket, final after
-  // conv2_wgrad) are reduced, exchanged and updated on `conv2_stream` while conv2_dgrad runs; only
-  // conv1's 320 values follow dgrad on the critical path (and that launch holds its completion until
-  // the conv2 update is published, so the next trunk_fwd reads the new conv2 weights)
-  void set_conv_split(bool on, uintptr_t conv2_stream);
-  // xGMI: fold the Adadelta steps into the all-reduce kernels (fc: gather phase; conv: slab reduce
-  // + one-shot + update in one launch).  Off = separate reduce / all-reduce / update launches.
+  // xGMI: fold the Adadelta steps into the all-reduce kernels (fc: gather phase; conv2 on the comm
+  // stream and conv1 on compute: slab reduce + one-shot + update in one launch each).  Off = separate
+  // reduce / all-reduce / update launches (the A/B oracle of the fused kernels' bits).
   void set_xgmi_fuse_update(bool on) { xgmi_fuse_update_ = on; }
-  void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }
-  void set_concurrent(bool on);      // multi-stream single-GPU graph (creates the wgrad stream)
-  // DDP schedule: 0 = conv backward on the forked branch, conv bucket + update on the comm stream;
-  // 1 = only the fc bucket all-reduce + fc update fork off, everything else stays on compute;
-  // 2 (needs attach_comm2) = as 1, but the fc branch is joined just before the next step's fc1,
-  //   so it overlaps the conv backward, the conv bucket, the conv update AND the next trunk_fwd;
-  // 3 = as 2, but the per-step fork / join are device-counter hand-offs (one-WG signal / wait
-  //   kernels) instead of captured cross-queue edges; only each chunk's first fork and last join
-  //   are graph edges.  Needs only attach_comm (or the xGMI comm): with one RCCL communicator the
-  //   conv all-reduce waits on a counter for the fc all-reduce of the same step
-  void set_dist_schedule(int s) { dist_sched_ = s; }
-  // Schedule 3 spins on one stream until the other signals; that is only deadlock-free when the
+  void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }   // RCCL: 2 buckets or 1
+  // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
+  // hand-off counters and their error flag, so a schedule never inherits another's counts (e.g. an
+  // aborted validation).  Detaching the xgmi communicator of the XGMI schedule unsets the schedule.
+  void set_schedule(int s);
+  int schedule() const { return sched_; }
+  void reset_counters();
+  // OVERLAP / XGMI spin on one stream until the other signals; that is only deadlock-free when the
   // compute and comm streams sit on different hardware queues (HIP shares queues beyond
   // GPU_MAX_HW_QUEUES).  Each stream waits (spin kernel, `timeout_s`) for a signal enqueued on the
   // other afterwards; true if both hand-offs completed.  Eager, no graph; call before training.
   bool probe_stream_handoff(double timeout_s);
-  bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
-  // single GPU: fold the fc Adadelta step into fc_bwd (FcUpdate; bitwise equal either way, off by
-  // default: measured 87.2 vs 85.9 us/step at B = 200)
-  void set_fuse_fc_update(bool on) { fuse_fc_update_ = on; }
-  // single GPU: run the fc Adadelta step on the comm stream, overlapped with the conv backward, with
-  // the schedule-3 device-counter hand-offs (needs probe_stream_handoff() to pass)
-  void set_overlap_fc_update(bool on) { overlap_fc_update_ = on; }
-  // single-GPU overlap schedule: the conv2 slab reduce + conv2 update ride in the dgrad launch
-  // (launch_conv_dgrad_update, w2d ping-pong); only the conv1 part stays in the step tail
-  void set_dgrad_update(bool on) { dgrad_update_ = on; }
-  // schedule-3 chunks as two graphs (side chain + compute chain) launched concurrently from two host
-  // threads (default on; see capture_train_split).  Off: one multi-stream graph per chunk.
-  void set_side_first(bool on) { side_first_ = on; }
-  // single-GPU overlap schedule: conv2's slab reduce + update on the comm stream under conv2_dgrad
-  void set_side_conv2(bool on) { side_conv2_ = on; }
-
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -140,7 +116,7 @@ class Engine {
   void broadcast_params(int root);                   // DDP construction: rank-0 params to all
   void synchronize();                                // all streams, then check_errors()
   void sync_streams();                               // all streams, no error-flag read-back
-  // device error flags: (schedule-3 hand-off timeout, xGMI error code); a 4-byte D2H each, call
+  // device error flags: (stream hand-off timeout, xGMI error code); a 4-byte D2H each, call
   // after the work of interest has completed (e.g. once per epoch)
   std::pair<int, int> errors() const;
   void check_errors() const;                         // throws with a decoded message
@@ -152,7 +128,8 @@ class Engine {
 
  private:
   void enqueue_step(int batch, bool last);
-  bool uses_side_streams() const;
+  bool side_schedule() const { return sched_ == OVERLAP || sched_ == XGMI; }
+  bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
   void reset_host_state();
   void side_worker();
@@ -166,50 +143,32 @@ class Engine {
   float rho_, eps_, wd_;
   bool two_buckets_ = true;
   int idx_stride_ = 0;
-  bool concurrent_ = false;
-  int dist_sched_ = 1;
-  std::shared_ptr<RcclComm> comm_, comm2_;
+  int sched_ = SERIAL;
+  std::shared_ptr<RcclComm> comm_;
   std::shared_ptr<XgmiComm> xgmi_;
   float* grad_own_ = nullptr;       // buf_.grad as given (restored when the xGMI comm is detached)
   bool xgmi_fuse_update_ = true;
-  bool side_pending_ = false;       // schedule 2/3: the previous step's fc branch is not joined yet
-  bool side_forked_ = false;        // schedule 3: comm stream already ordered after this chunk's start
-  int* sync_ = nullptr;             // [0] fc grads ready count, [1] fc update done count, [2] error,
-                                    // [3]/[4] conv split, [8..11] probes, [16..31] / [32..47] fc1+head
-                                    // tile counters (FC1_HEAD_MAX_TILES each),
-                                    // [12] fc all-reduce done (1 comm)
-  bool fuse_fc_update_ = false;
-  bool overlap_fc_update_ = false;
-  bool dgrad_update_ = true;
-  bool side_first_ = true;
-  bool side_conv2_ = false;
-  bool enq_main_ = true, enq_side_ = true;   // two-pass capture: which streams enqueue_step feeds
-  bool enq_side2_ = true;                     // split capture: the third (conv2) stream's pass
+  bool side_pending_ = false;       // the previous step's fc update is not joined yet
+  bool side_forked_ = false;        // comm stream already ordered after this chunk's start
+  int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
+                                    // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch
+  bool enq_main_ = true, enq_side_ = true;   // split capture: which stream's pass enqueue_step feeds
   bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
   std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null
-  std::vector<hipGraphExec_t> side2_graphs_;  // per graph id: its conv2-stream graph (third-stream split) or null
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_join2_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   std::thread side_thread_;                   // launches side graphs concurrently with the compute graph
   std::mutex side_mu_;
   std::condition_variable side_cv_;
-  hipGraphExec_t side_job_ = nullptr, side2_job_ = nullptr;
+  hipGraphExec_t side_job_ = nullptr;
   bool side_done_ = false, side_stop_ = false;
   hipError_t side_err_ = hipSuccess;
-  bool conv_split_ = false;
-  hipStream_t conv2_stream_ = nullptr;   // owned by the caller (torch stream)
-  hipEvent_t ev_c2_ = nullptr;
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
   void phase_begin(const char* name);
   void phase_end();
-  uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (fused fc update ping-pong)
-  bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
   float* c1red_ = nullptr;          // conv1 partial group sums (large batches)
-  // MNIST_AMD_C1_PREREDUCE=0 turns the large-batch conv1 pre-reduce off (A/B, numerics checks)
-  bool c1_prereduce_ = [] { const char* e = getenv("MNIST_AMD_C1_PREREDUCE"); return !(e && e[0] == '0'); }();
-  uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv split / dgrad_update ping-pong)
-  bool w2d_in_alt_ = false;
-  hipEvent_t ev_fc_ = nullptr, ev_conv_ = nullptr, ev_done_ = nullptr, ev_w_ = nullptr;
-  hipStream_t wgrad_stream_ = nullptr;
+  uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv2 update on the comm stream)
+  bool w2d_in_alt_ = false;         // enqueue-time: the current w2d lives in w2d_alt_
+  hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr;
   // workspace
   int64_t ws_bytes_ = 0;
   void* ws_ = nullptr;

@@ -31,7 +31,7 @@ constexpr float kDdpEpilogueScale = 1.0f;
 
 // ---------------------------------------------------------------------------- engine workspace
 struct WorkspaceLayout {
-  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w1t_alt, w2d_alt, c1red;
+  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w2d_alt, c1red;
   int64_t total;   // bytes
 };
 
@@ -62,8 +62,7 @@ inline WorkspaceLayout compute_workspace_layout(int max_batch, int max_test_batc
   L.c1part = carve(4 * M * 320 * 4);
   L.w2part = carve((int64_t)wgrad_groups * (18432 + 64) * 4);
   L.fcpart = carve(fc_splits > 1 ? (int64_t)fc_splits * FCB_PART_STRIDE * 4 : 256);   // large-batch partials
-  L.sync = carve(256);                                                                // schedule-3 counters
-  L.w1t_alt = carve((int64_t)NFLAT * NH * 2);                                         // alternate w1t
+  L.sync = carve(256);                                                                // hand-off counters
   L.w2d_alt = carve((int64_t)9 * C1 * C2 * 2);                                         // alternate w2d
   L.c1red = carve((int64_t)C1_PRE_SLABS * 320 * 4);                                    // conv1 group sums
   L.total = off;

@@ -21,29 +21,29 @@ void ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi: ") + what + ": " + hipGetErrorString(e));
 }
 
-// Process-wide free list of exported buffers, keyed by (device, bytes, uncached).  Exported buffers
-// are never returned to the allocator (see the constructor), but a later communicator of the same
-// shape reuses them instead of allocating again, so the probe / validation / test communicators of
-// a long-lived process no longer grow device memory by ~9.6 MB each.  Reuse hands out the SAME
-// memory under the SAME IPC handle, so a peer's import cache maps the right pages; the 16-byte
-// signatures are rewritten by every new communicator, so a peer that kept a stale mapping of an
-// older communicator's buffer is still refused by connect().
+// Process-wide free list of exported buffers, keyed by (device, bytes).  Exported buffers are never
+// returned to the allocator (see the constructor); a communicator whose ranks all unmapped each
+// other (close_peers + barrier + mark_recyclable) hands them to a later communicator of the same
+// shape, so the test communicators of a long-lived process do not grow device memory by ~9.6 MB
+// each.  Reuse hands out the SAME memory under the SAME IPC handle, so a peer's import cache maps
+// the right pages; the 16-byte signatures are rewritten by every new communicator, so a peer that
+// kept a stale mapping of an older communicator's buffer is still refused by connect().
 std::mutex g_pool_mu;
-std::map<std::tuple<int, size_t, bool>, std::vector<void*>> g_pool;
+std::map<std::pair<int, size_t>, std::vector<void*>> g_pool;
 
-void* pool_take(int device, size_t bytes, bool uncached) {
+void* pool_take(int device, size_t bytes) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  auto it = g_pool.find({device, bytes, uncached});
+  auto it = g_pool.find({device, bytes});
   if (it == g_pool.end() || it->second.empty()) return nullptr;
   void* p = it->second.back();
   it->second.pop_back();
   return p;
 }
 
-void pool_give(int device, size_t bytes, bool uncached, void* p) {
+void pool_give(int device, size_t bytes, void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool[{device, bytes, uncached}].push_back(p);
+  g_pool[{device, bytes}].push_back(p);
 }
 
 void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* off) {
@@ -76,15 +76,9 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   // never returned to the allocator either (never a block of torch's caching allocator): a later
   // allocation at the same address would carry an IPC handle a peer's import cache cannot tell
   // from the old one.
-  const char* uc = getenv("MNIST_AMD_XGMI_UNCACHED");
-  const bool uncached = uc ? atoi(uc) != 0 : kUncachedDefault;
-  uncached_ = uncached;
-  auto alloc = [this, uncached, device](void** p, size_t bytes, const char* what) {
-    *p = pool_take(device, bytes, uncached);
-    if (!*p) {
-      if (uncached) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
-      else ok(hipMalloc(p, bytes), what);
-    }
+  auto alloc = [this, device](void** p, size_t bytes, const char* what) {
+    *p = pool_take(device, bytes);
+    if (!*p) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
     owned_.push_back({*p, bytes});
   };
   // every exported buffer ends in a 16-byte signature {magic, rank, pid, buffer id} that peers read
@@ -95,6 +89,7 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
         "hipExtMallocWithFlags(flags)");
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
+  ok(hipMalloc(&timeout_, sizeof(uint64_t)), "hipMalloc(timeout)");
   ok(hipMemset(in_, 0, sizeof(float) * numel), "hipMemset");
   ok(hipMemset(out_, 0, sizeof(float) * numel), "hipMemset");
   ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
@@ -118,14 +113,22 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
 }
 
 XgmiComm::~XgmiComm() {
+  close_peers();
+  // in_, out_, flags_, stage_ were exported: never freed (see the constructor); returned to the
+  // process-wide free list only when every peer is known to have unmapped them (mark_recyclable)
+  if (recyclable_)
+    for (auto& b : owned_) pool_give(device_, b.second, b.first);
+  if (ctr_) hipFree(ctr_);
+  if (err_) hipFree(err_);
+  if (timeout_) hipFree(timeout_);
+}
+
+void XgmiComm::close_peers() {
   hipSetDevice(device_);
   hipDeviceSynchronize();
   for (void* p : opened_) hipIpcCloseMemHandle(p);
-  // in_, out_, flags_, stage_ were exported: never freed (see the constructor), but returned to
-  // the process-wide free list for the next communicator of the same shape
-  for (auto& b : owned_) pool_give(device_, b.second, uncached_, b.first);
-  if (ctr_) hipFree(ctr_);
-  if (err_) hipFree(err_);
+  opened_.clear();
+  if (world_ > 1) connected_ = false;
 }
 
 char* XgmiComm::sig_ptr(int id) const { return sig_at(id, in_, out_, flags_, stage_); }
@@ -139,7 +142,11 @@ char* XgmiComm::sig_at(int id, const void* in, const void* out, const void* flag
   }
 }
 
-void XgmiComm::set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
+void XgmiComm::set_timeout_seconds(double s) {
+  const uint64_t t = (uint64_t)(s * 1e8);
+  ok(hipSetDevice(device_), "hipSetDevice");
+  ok(hipMemcpy(timeout_, &t, sizeof(t), hipMemcpyHostToDevice), "hipMemcpy(timeout)");
+}
 
 std::vector<uint8_t> XgmiComm::record() const {
   XgmiRecord r;
@@ -239,40 +246,18 @@ XgmiArgs XgmiComm::args(int channel, int64_t offset, int64_t count) const {
   a.world = world_;
   a.rank = rank_;
   a.nvec = count / 4;
-  a.timeout_ticks = timeout_ticks_;
+  a.timeout_ticks = timeout_;
   a.max_wg = XGMI_MAX_WG;
-  // system-scope release fence before every stage flag (buffer_wbl2 of the XCD's dirty L2 lines) /
+  // system-scope release fence before every stage flag (buffer_wbl2 of the XCD's dirty L2 lines) +
   // acquire after every matched poll: off by default - rules R1-R4 in xgmi_allreduce.hip order the
   // payload without them; the release fence measured +13 us per world-1 step (100.5 vs 87.5)
-  a.release = fence_release();
-  a.acquire = fence_acquire();
+  a.release = a.acquire = fences_ ? 1 : 0;
   return a;
 }
 
-int XgmiComm::fence_release() {
-  static const int v = [] {
-    const char* e = getenv("MNIST_AMD_XGMI_RELEASE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-int XgmiComm::fence_acquire() {
-  static const int v = [] {
-    const char* e = getenv("MNIST_AMD_XGMI_ACQUIRE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 std::string XgmiComm::ordering() const {
-  const char* uc = getenv("MNIST_AMD_XGMI_UNCACHED");
-  const bool uncached = uc ? atoi(uc) != 0 : kUncachedDefault;
-  std::string s = uncached ? "uncached+sc0sc1" : "cached+sc0sc1";
-  if (fence_release()) s += "+release";
-  if (fence_acquire()) s += "+acquire";
-  if (!fence_release() && !fence_acquire()) s += " (no fence: xgmi_allreduce.hip R1-R4)";
-  return s;
+  return fences_ ? "uncached+sc0sc1+release+acquire (fenced: the unfenced schedule failed validation)"
+                 : "uncached+sc0sc1 (no fence: xgmi_allreduce.hip R1-R4)";
 }
 
 void XgmiComm::allreduce_fc_fused(int channel, hipStream_t stream, const AdadeltaArgs& ada) {
@@ -310,6 +295,18 @@ void XgmiComm::allreduce(int channel, int64_t offset, int64_t count, hipStream_t
     a.max_wg = grids_.twoshot;
     launch_xgmi_allreduce(a, stream);
   }
+}
+
+void XgmiComm::stage_out(const float* buf, int64_t count, hipStream_t stream) {
+  if (count < 0 || count > numel_) throw std::runtime_error("xgmi: stage_out count out of range");
+  ok(hipMemcpyAsync(out_, buf, sizeof(float) * count, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync(stage_out)");
+}
+
+void XgmiComm::read_peer_out(int peer, float* buf, int64_t count, hipStream_t stream) {
+  if (!connected_) throw std::runtime_error("xgmi: connect() first");
+  if (peer < 0 || peer >= world_ || count < 0 || count > numel_) throw std::runtime_error("xgmi: read_peer_out range");
+  ok(hipMemcpyAsync(buf, peer_out_[peer], sizeof(float) * count, hipMemcpyDeviceToDevice, stream),
+     "hipMemcpyAsync(read_peer_out)");
 }
 
 int XgmiComm::error() const {

@@ -58,10 +58,29 @@ class XgmiComm {
   int error() const;
   // how peer-visible payload is ordered (bench JSON "xgmi_ordering"; rules in xgmi_allreduce.hip)
   std::string ordering() const;
-  static int fence_release();   // MNIST_AMD_XGMI_RELEASE
-  static int fence_acquire();   // MNIST_AMD_XGMI_ACQUIRE
+  // system-scope release fence before every stage flag + acquire after every matched poll (off by
+  // default: rules R1-R4 in xgmi_allreduce.hip).  Read at launch / capture time: graphs captured
+  // before a change keep the old mode.  The trainer turns it on when the unfenced schedule fails its
+  // cross-rank validation with wrong sums (not a timeout) and validates again.
+  void set_fences(bool on) { fences_ = on; }
+  bool fences() const { return fences_; }
   const XgmiGrids& grids() const { return grids_; }
+  // stage-wait timeout; kept in device memory and read by every stage wait, so it also applies to
+  // graphs captured earlier (synchronous 8-byte copy: call while no xGMI kernel is running)
   void set_timeout_seconds(double s);
+  // Buffer recycling.  The exported buffers are never returned to the allocator (a peer's import
+  // cache could not tell a new allocation at the same address from the old one); a later
+  // communicator of the same shape may reuse them - but only once EVERY peer has unmapped them, or a
+  // late write of a peer's old kernel could satisfy a new wait.  close_peers() waits for this
+  // device's work and unmaps the peers' buffers; after a barrier that every rank enters only after
+  // its own close_peers(), mark_recyclable() lets the destructor hand the buffers to the free list
+  // (without it they are leaked, as before).
+  void close_peers();
+  void mark_recyclable() { recyclable_ = true; }
+  // broadcast helpers (host-ordered copies; the caller barriers between them): out()[0, count) =
+  // buf on the root; buf = peer's out()[0, count) on the others
+  void stage_out(const float* buf, int64_t count, hipStream_t stream);
+  void read_peer_out(int peer, float* buf, int64_t count, hipStream_t stream);
   int world_size() const { return world_; }
   int rank() const { return rank_; }
   float* in() const { return in_; }
@@ -76,11 +95,12 @@ class XgmiComm {
   int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
   float* stage_ = nullptr;   // [channels][2][oneshot_max_], IPC exported
   std::vector<std::pair<void*, size_t>> owned_;   // the exported buffers (back to the free list)
-  bool uncached_ = true;
+  bool recyclable_ = false;
+  bool fences_ = false;
   int64_t oneshot_max_;
   int* ctr_ = nullptr;       // [channels][XGMI_MAX_WG], local
   int* err_ = nullptr;
-  uint64_t timeout_ticks_;
+  uint64_t* timeout_ = nullptr;   // device: stage-wait timeout in s_memrealtime ticks (100 MHz)
   XgmiGrids grids_;
   bool connected_ = false;
   std::vector<const float*> peer_in_;
@@ -90,7 +110,6 @@ class XgmiComm {
   std::vector<void*> opened_;   // IPC mappings to close
   XgmiArgs args(int channel, int64_t offset, int64_t count) const;
   static constexpr int kSigBytes = 16;
-  static constexpr bool kUncachedDefault = true;   // MNIST_AMD_XGMI_UNCACHED overrides
   static constexpr int32_t kSigMagic = 0x58474d49;   // "XGMI"
   char* sig_ptr(int id) const;
   char* sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const;

@@ -97,6 +97,17 @@ def run(argv=None, ddp_script: bool = True) -> int:
     torch.manual_seed(args.seed)
     device = torch.device(f"cuda:{gpu}" if use_cuda else "cpu") if ddp_script else \
         torch.device("cuda" if use_cuda else "cpu")
+    engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
+    if not use_cuda or getattr(args, "dtype", "bf16") == "fp32":
+        engine = "module"
+    # the fused engine's RCCL communicator initialises on a helper thread while data, model and
+    # trainer are built (its bootstrap is the largest N > 1 startup cost inside the timer)
+    args._pending_comm = None
+    allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
+    if distributed and engine == "fused" and allreduce != "xgmi":
+        from .parallel.distributed import start_rccl_comm
+        with setup.phase("rccl_comm_start"):
+            args._pending_comm = start_rccl_comm(world, rank, gpu)
 
     with setup.phase("data"):
         train_data = load_mnist(args.data_root, True, args.synthetic, args.synthetic_train_size, verbose=rank == 0)
@@ -110,12 +121,8 @@ def run(argv=None, ddp_script: bool = True) -> int:
         test_stream = RandomIndexStream(len(test_data)) if use_cuda else SequentialIndexStream(len(test_data))
 
     model = Net()
-    engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
-    if not use_cuda:
-        engine = "module"
     if getattr(args, "dtype", "bf16") == "fp32":     # stock torch fp32 ops: module engine only
         model.compute_dtype = torch.float32
-        engine = "module"
     if args.resume:
         load_state_dict(model, args.resume, map_location="cpu")
 
@@ -171,13 +178,12 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     t_model = time.perf_counter()
     ms = ModelState(model, device, lr=args.lr)
     model_for_save = model
-    comm = comm2 = None
+    comm = None
     two_buckets = True
     allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
+    setup.add("model", time.perf_counter() - t_model)
     if distributed:
         from .parallel.ddp import DistributedDataParallel, engine_bucket_layout
-        from .parallel.distributed import create_rccl_comms
-        setup.add("model", time.perf_counter() - t_model)
         with setup.phase("ddp_wrap"):
             ddp = DistributedDataParallel(model, device_ids=[gpu], engine_managed=True,
                                           bucket_cap_mb=args.bucket_cap_mb, first_bucket_cap_mb=args.first_bucket_mb)
@@ -185,11 +191,10 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         two_buckets = engine_bucket_layout(ddp.bucket_indices)   # raises on a layout the engine cannot run
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("--allreduce xgmi needs the two-bucket layout (default --bucket-cap-mb/--first-bucket-mb)")
-        if allreduce != "xgmi":              # xgmi-only DDP needs no RCCL communicator at all
-            with setup.phase("rccl_comms"):
-                comm, comm2 = create_rccl_comms(world, rank, gpu)
-    else:
-        setup.add("model", time.perf_counter() - t_model)
+        if args._pending_comm is not None:     # xgmi-only DDP needs no RCCL communicator at all
+            with setup.phase("rccl_comm_wait"):
+                comm = args._pending_comm.result()
+            setup.add_info("rccl_comm_init_thread_s", args._pending_comm.seconds)
     # The optimizer here is the engine's fused Adadelta kernel (state in `ms`); StepLR(step_size=1)
     # (reference mnist_ddp.py:178, :189) reduces to lr <- lr * gamma after every epoch, computed in
     # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
@@ -199,10 +204,10 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
-                           comm2=comm2, allreduce=allreduce, two_buckets=two_buckets)
+                           allreduce=allreduce, two_buckets=two_buckets)
     if distributed and rank == 0 and trainer.allreduce_timings:
-        print(f"| gradient all-reduce: {trainer.allreduce} (probe us/step: {trainer.allreduce_timings})", flush=True)
-    trainer.engine.refresh_shadows()      # parameters may have been broadcast by the DDP wrapper
+        print(f"| gradient all-reduce: {trainer.allreduce} (schedule us/step: {trainer.allreduce_timings})",
+              flush=True)
     if args.profile:
         trainer.profile_left = args.profile_steps
     n_train = len(train_data)
@@ -226,7 +231,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         if epoch == 1:                     # the trainer's phases include epoch 1's graph captures
             setup.update(trainer.setup, prefix="trainer.")
             _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
-                                      "allreduce": trainer.allreduce if distributed else None})
+                                      "setup_info": setup.info, "allreduce": trainer.allreduce if distributed else None,
+                                      "transport_report": trainer.transport_report or None})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
                "img_per_s": st.samples / max(st.train_seconds, 1e-9), "device_train_s": st.device_seconds}
         if st.device_seconds:

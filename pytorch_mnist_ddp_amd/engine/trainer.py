@@ -5,12 +5,13 @@ What changes versus the reference loop, and why (MI355X-first):
 * the whole split lives in HBM as uint8 (47 MB); per epoch only the sampler's index vector is
   uploaded (one 240 KB H2D), the first kernel of each step gathers + normalises its rows -
   no DataLoader worker, no pinned-memory thread, no per-step H2D copy (reference :68);
-* a training step is 8 kernels enqueued by C++ (``_C.Engine``) and chunks of ``graph_steps``
-  steps are captured once into a hipGraph and replayed; the host only syncs where the reference
+* a training step is 7-8 kernels enqueued by C++ (``_C.Engine``) and chunks of ``graph_steps``
+  steps are captured once into hipGraphs and replayed; the host only syncs where the reference
   prints (rank 0, every ``log_interval`` batches) and at eval;
-* DDP: the fc gradient bucket (98.4 % of bytes) is all-reduced over RCCL on a second stream while
-  the conv backward runs, then its Adadelta update runs on that stream too; the conv bucket
-  follows.  Averaging (1/W) is folded into the gradient GEMM epilogues;
+* DDP: the fc gradient bucket (98.4 % of bytes) is all-reduced on the comm stream while the conv
+  backward runs, then its Adadelta update runs on that stream too; the conv bucket follows.  The
+  transport - RCCL or the direct xGMI kernels - is chosen by validating and timing each one's
+  production schedule at startup.  Averaging (1/W) is folded into the head's loss gradient;
 * evaluation (rank 0 only, SequentialSampler over the test set) is one captured graph per epoch
   with per-row losses / hits reduced once on the host side.
 
@@ -29,6 +30,12 @@ from ..data.datasets import MNISTData
 from ..ops import native
 from ..utils.profiling import PhaseTimes
 from .state import FLAG_NO_DROPOUT, ModelState
+
+
+# startup validation: timed replays of the chunk per candidate transport; host watchdog of the RCCL
+# schedule's replays (its first collectives also set up RCCL's channels and proxies)
+VALIDATE_TIMED = 2
+RCCL_WATCHDOG_S = float(os.environ.get("MNIST_AMD_RCCL_WATCHDOG", "120"))
 
 
 def _fault_delay(kind: str, rank: int) -> float:
@@ -51,15 +58,40 @@ class EpochStats:
     device_seconds: float | None = None          # HIP-event time of the epoch's training work
 
 
+class TransportHang(RuntimeError):
+    """A startup replay of the RCCL schedule did not complete within its host watchdog: a collective
+    is stuck on the device (a peer never arrived) and cannot be cancelled - the caller reports and
+    exits the process (``fatal``) instead of waiting for the process group's 10-minute timeout."""
+    fatal = True
+
+
+class StartupValidationError(RuntimeError):
+    """No candidate transport passed: carries every candidate's report and the trainer's setup
+    phases so far (bench.py puts both into its failure JSON)."""
+
+    def __init__(self, msg: str, transport_report: dict, setup: PhaseTimes):
+        super().__init__(msg)
+        self.transport_report = transport_report
+        self.setup = setup
+
+
 class FusedTrainer:
+    """``allreduce`` (DDP): "rccl", "xgmi" or "auto" (default).  Every candidate transport is built
+    and its PRODUCTION schedule - the captured chunk graph training replays - is validated and timed
+    on this node before training (``transport_report``); "auto" keeps the faster valid one.
+    ``overlap`` (single GPU): the OVERLAP schedule (optimizer work on the comm stream) when the two
+    streams pass the hand-off probe, else SERIAL.  ``xgmi_fuse``: the xGMI kernels apply Adadelta
+    themselves (False = separate launches: the fused kernels' bitwise oracle).  ``probe_world1``
+    (tests): with a communicator at world 1, evaluate the xGMI candidate under "auto" too."""
+
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
-                 two_buckets: bool = True, concurrent: bool | None = None, comm2=None,
-                 fuse_fc_update: bool | None = None, allreduce: str | None = None):
+                 two_buckets: bool = True, allreduce: str | None = None, overlap: bool = True,
+                 xgmi_fuse: bool = True, probe_world1: bool = False):
         C = native.load()
         self.C, self.ms = C, mstate
-        # host seconds per setup phase (engine, xgmi_comm, allreduce_probe, stream_probe, validation,
+        # host seconds per setup phase (engine, xgmi_comm, stream_probe, validate.<transport>,
         # graph_capture): the N > 1 startup budget inside the reference's timer
         self.setup = PhaseTimes()
         _t_init = time.perf_counter()
@@ -106,185 +138,177 @@ class FusedTrainer:
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay)
         self.engine.set_bucket_split(two_buckets)
-        self._graphs: dict[tuple[int, int], int] = {}
+        self._graphs: dict[tuple[int, int], int] = {}        # captured chunks of the selected schedule
+        self._graph_sets: dict[str, dict] = {}               # per transport (validation captures)
         self._eval_graph: int | None = None
         # steps still to run in the profiling window (Engine.profile_steps; bitwise the graph path)
         self.profile_left = 0
         self.use_graphs = self.graph_steps > 0
-        self.ramp = int(os.environ.get("MNIST_AMD_GRAPH_RAMP", "0"))   # see _chunks
-        if concurrent is None:
-            concurrent = os.environ.get("MNIST_AMD_CONCURRENT", "0") == "1"
-        self.engine.set_concurrent(bool(concurrent))
-        # single GPU, opt-in (MNIST_AMD_FUSE_FC=1): fc_bwd applies the fc Adadelta step in its
-        # epilogue, bitwise equal to the step-tail update but ~1 us/step slower (the update is
-        # HBM-bound either way and loses its overlap with the conv slab reduce; docs/PERF_NOTES.md)
-        if fuse_fc_update is None:
-            fuse_fc_update = os.environ.get("MNIST_AMD_FUSE_FC", "0") == "1"
-        self.engine.set_fuse_fc_update(bool(fuse_fc_update))
-        # single GPU: fc Adadelta step overlapped with the conv backward on the comm stream
-        # (device-counter hand-offs, schedule-3 style; default on, MNIST_AMD_OVERLAP_FC=0 to disable:
-        # measured 85.2 -> 82.7 us/step at B = 200)
-        self.overlap_fc = (comm is None and world_size == 1 and not fuse_fc_update and not concurrent
-                           and os.environ.get("MNIST_AMD_OVERLAP_FC", "1") == "1")
-        self.engine.set_overlap_fc_update(self.overlap_fc)
-        # single-GPU overlap schedule: conv2 reduce + update as extra workgroups of the dgrad launch
-        # (opt-in MNIST_AMD_DGRAD_UPDATE=1, bitwise equal; measured 81.6-82.2 vs 80.9-81.8 us/step)
-        self.engine.set_dgrad_update(os.environ.get("MNIST_AMD_DGRAD_UPDATE", "0") == "1")
-        # captured chunks: side-stream nodes first, then the compute chain (MNIST_AMD_SIDE_FIRST=0: one
-        # pass in step order; see Engine::capture_train)
-        self.engine.set_side_first(os.environ.get("MNIST_AMD_SIDE_FIRST", "1") == "1")
-        # single GPU: conv2's slab reduce + update on the comm stream under conv2_dgrad (default on,
-        # MNIST_AMD_SIDE_CONV2=0 to compare; bitwise equal: 73.6 / 72.5 -> 70.8 / 71.2 us/step at B = 200)
-        self.engine.set_side_conv2(os.environ.get("MNIST_AMD_SIDE_CONV2", "1") == "1")
-        # DDP schedule: 3 (the fc bucket all-reduced + updated on the comm stream, overlapping the conv
-        # backward and the step boundary, device-counter stream hand-offs; with one communicator the
-        # conv all-reduce waits for the fc one on a counter) whenever a communicator is attached
-        # (see csrc/runtime/engine.h; measured at world 1: 93.9 / 97.3 / 96.9 us for 3 / 2 / 1)
-        sched = int(os.environ.get("MNIST_AMD_DIST_SCHED", "3"))
-        self.engine.set_dist_schedule(sched)
+        self.comm = comm
         if comm is not None:
-            self.engine.attach_comm(comm)
-        if comm2 is not None:
-            self.engine.attach_comm2(comm2)
-        self.comm, self.comm2 = comm, comm2
-        # gradient all-reduce: "rccl" (ncclAllReduce per bucket), "xgmi" (direct reduce-scatter +
-        # all-gather over IPC-mapped peer buckets, csrc/runtime/xgmi_comm.h; self-tested at startup,
-        # falls back to RCCL on every rank if any rank fails) or "auto" (default: with world > 1 and
-        # RCCL comms attached, time both on this node's links and keep the faster).  Used on the DDP
-        # path; RCCL stays attached for the parameter broadcast.
+            self.engine.attach_comm(comm)                    # also the parameter broadcast's transport
         if allreduce is None:
             allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
         if allreduce not in ("rccl", "xgmi", "auto"):
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
-        self.xgmi, self.grad_out, self.allreduce_timings = None, None, {}
-        self.conv_split, self.conv2_stream = False, None
-        self.xgmi_validation = None
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
+        self.xgmi, self.grad_out = None, None
+        self.xgmi_fuse = bool(xgmi_fuse)
+        self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
+        self.transport_report: dict[str, dict] = {}           # candidate -> validation / us per step
+        self.allreduce_timings: dict[str, float] = {}
+        self.xgmi_validation = None
+        self.allreduce = None
         import torch.distributed as _dist
-        want = allreduce == "xgmi" and (comm is not None or world_size > 1 or _dist.is_initialized())
-        probe_always = os.environ.get("MNIST_AMD_PROBE_ALWAYS", "0") == "1"   # tests: probe at world 1
-        want = want or (allreduce == "auto" and comm is not None and two_buckets and (world_size > 1 or probe_always))
-        # Adadelta fused into the xGMI kernels (default; MNIST_AMD_XGMI_FUSE=0: separate launches).
-        # Decided before the probe: only a fused schedule saves the RCCL side's separate conv update.
-        self.xgmi_fuse = os.environ.get("MNIST_AMD_XGMI_FUSE", "1") != "0"
-        if want:
-            from ..parallel.distributed import choose_allreduce, create_xgmi_comm
-            with self.setup.phase("xgmi_comm"):
-                self.xgmi = create_xgmi_comm(world_size, rank, dev, mstate.grad.numel())
-            if self.xgmi is not None and allreduce == "auto":
-                split = mstate.bucket_split
-                upd = []
-                if self.xgmi_fuse:
-                    # the RCCL schedule's separate conv update (fused away on the xGMI side) is timed
-                    # on a scratch copy of the optimizer state, so the probe leaves the model untouched
-                    scratch = {k: getattr(mstate, k).clone() for k in ("param", "square_avg", "acc_delta", "w2f", "w2d")}
-                    p_ = native.ptr
-                    upd = [lambda: C.adadelta(p_(scratch["param"]), p_(mstate.grad), p_(scratch["square_avg"]),
-                                              p_(scratch["acc_delta"]), p_(mstate.lr), mstate.rho, mstate.eps,
-                                              mstate.weight_decay, p_(scratch["w2f"]), p_(scratch["w2d"]),
-                                              p_(mstate.w1), p_(mstate.w1t), 0, 2, True,
-                                              int(torch.cuda.current_stream(dev).cuda_stream))]
-                with torch.cuda.stream(self.compute), self.setup.phase("allreduce_probe"):
-                    pick, self.allreduce_timings = choose_allreduce(
-                        comm2 if comm2 is not None else comm, comm, self.xgmi, mstate.grad,
-                        (0, split), (split, mstate.grad.numel() - split), dev, rccl_extra=upd)
-                upd = None
-                if pick != "xgmi":
-                    self.xgmi = None
-            if self.xgmi is not None:
-                self.engine.set_dist_schedule(3)
-                self.engine.attach_xgmi(self.xgmi)
-                self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
-                # conv bucket split (fused schedule, opt-in MNIST_AMD_CONV_SPLIT=1): conv2's reduce +
-                # exchange + update on a third stream under conv2_dgrad, only conv1's 320 values after
-                # dgrad.  Bitwise equal; at world 1 it costs 1-2 us/step (88.0-89.1 vs 87.0-87.1: two
-                # more hand-off kernels and a third graph branch) and what it saves at world > 1 (the
-                # conv2 slab reduce off the critical path) is unmeasured on one GPU, so it is off.
-                # MNIST_AMD_CONV_SPLIT=comm (default) queues the conv2 part on the comm stream after the
-                # fc bucket instead (no third stream; part of every chunk's side graph): at world 1
-                # neutral (78.9-80.3 vs 79.1-79.6 us/step), at world > 1 it takes conv2's slab reduce
-                # + exchange + update (98 % of the conv bucket) off the critical path; bitwise equal
-                split_mode = os.environ.get("MNIST_AMD_CONV_SPLIT", "comm")
-                if self.xgmi_fuse and split_mode == "1":
-                    self.conv2_stream = torch.cuda.Stream(device=dev)
-                    self.engine.set_conv_split(True, int(self.conv2_stream.cuda_stream))
-                    self.conv_split = True
-                elif self.xgmi_fuse and split_mode == "comm":
-                    self.engine.set_conv_split(True, int(self.comm_stream.cuda_stream))
-                    self.conv_split = "comm"
-        # schedule 3 spins on one stream for the other: make sure they sit on different hardware
-        # queues on EVERY rank, else fall back everywhere to graph-edge joins (schedule 2 / 1, RCCL)
-        uses_sched3 = self.xgmi is not None or (comm is not None and sched == 3) or self.overlap_fc
-        if uses_sched3:
-            from ..parallel.distributed import STARTUP_TIMEOUT_S, _all_ok
-            _t_probe = time.perf_counter()
+        ddp = comm is not None or world_size > 1 or (allreduce == "xgmi" and _dist.is_initialized())
+        if not ddp:
+            self._setup_single_gpu(overlap)
+        else:
+            self._setup_ddp(comm, allreduce, two_buckets, probe_world1, train)
+        self.setup.add("engine", time.perf_counter() - _t_init - self.setup.total())
+
+    # ------------------------------------------------------------------ schedule selection
+    def _probe_streams(self) -> bool:
+        """Both streams on distinct hardware queues (the device-counter hand-offs need it), on every rank."""
+        from ..parallel.distributed import STARTUP_TIMEOUT_S, _all_ok
+        with self.setup.phase("stream_probe"):
             ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
-            if world_size > 1:
-                ok = _all_ok(ok, dev)
-            if not ok and self.conv_split:               # the third stream shares a queue: no split
-                self.conv_split = False
-                self.engine.set_conv_split(False, 0)
-                ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
-                if world_size > 1:
-                    ok = _all_ok(ok, dev)
-            if not ok and self.overlap_fc and self.xgmi is None and comm is None:
-                self.overlap_fc = False                  # single GPU: plain serial schedule instead
-                self.engine.set_overlap_fc_update(False)
-                ok = True
-            if not ok and comm is None:
-                raise RuntimeError("DDP schedule 3 unusable (compute/comm streams share a hardware queue) "
-                                   "and no RCCL communicator to fall back to")
+            return _all_ok(ok) if self.world > 1 else ok
+
+    def _setup_single_gpu(self, overlap: bool) -> None:
+        C = self.C
+        # OVERLAP (default): the fc Adadelta step and conv2's reduce + update on the comm stream under
+        # the conv backward (measured B = 200: 82.7 vs 85.2 us/step serial, then 70.8-71.2 with
+        # conv2's part moved too); SERIAL when the streams share a hardware queue
+        self.overlap = bool(overlap) and self._probe_streams()
+        self.engine.set_schedule(C.SCHED_OVERLAP if self.overlap else C.SCHED_SERIAL)
+
+    def _use_graph_set(self, name: str) -> None:
+        self._graphs = self._graph_sets.setdefault(name, {})
+
+    def _setup_ddp(self, comm, allreduce: str, two_buckets: bool, probe_world1: bool, train) -> None:
+        """Build every candidate transport, validate + time its production schedule, keep the best."""
+        from ..parallel.distributed import create_xgmi_comm, release_xgmi_comm
+        C = self.C
+        self.overlap = False
+        want_x = allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
+                                          and (self.world > 1 or probe_world1))
+        want_r = comm is not None and allreduce in ("rccl", "auto")
+        x = None
+        if want_x:
+            with self.setup.phase("xgmi_comm"):
+                x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel())
+            if x is not None and not self._probe_streams():
+                if self.rank == 0:
+                    print("[engine] compute/comm streams share a hardware queue: no xGMI schedule", flush=True)
+                release_xgmi_comm(x)
+                x = None
+            if x is None:
+                self.transport_report["xgmi"] = {"ok": False, "validation": "setup, self-test or stream probe failed"}
+        # DDP construction semantics: rank 0's parameters everywhere BEFORE the validations (they
+        # compare the ranks' parameters after replaying the same steps)
+        self.broadcast_params(x)
+        if x is not None:
+            self.engine.attach_xgmi(x)
+            self.engine.set_schedule(C.SCHED_XGMI)
+            self.xgmi = x
+            self._use_graph_set("xgmi")
+            ok, why, us = self._validate("xgmi", train)
+            if not ok and "differ" in why:
+                # wrong sums, no timeout: retry with system-scope release / acquire fences around every
+                # stage flag (the ordering rules R1-R4 of xgmi_allreduce.hip assume a memory model the
+                # fences make explicit); graphs captured without them are dropped
+                if self.rank == 0:
+                    print(f"[xgmi] startup validation failed ({why}): retrying with fences", flush=True)
+                x.set_fences(True)
+                self._graph_sets["xgmi"] = {}
+                self._use_graph_set("xgmi")
+                ok, why2, us = self._validate("xgmi", train)
+                why = why2 if ok else f"{why}; fenced: {why2}"
+            self.transport_report["xgmi"] = {"ok": ok, "validation": why, "us_per_step": us,
+                                             "ordering": x.ordering}
+            self.xgmi_validation = why
+            if not ok and self.rank == 0:
+                print(f"[xgmi] startup validation failed ({why})", flush=True)
+            self.engine.attach_xgmi(None)           # detached while RCCL is evaluated (re-attached below)
             if not ok:
-                if rank == 0:
-                    print("[engine] compute/comm streams share a hardware queue: DDP schedule 3 disabled",
-                          flush=True)
-                self.engine.set_dist_schedule(2 if comm2 is not None else 1)   # graph-edge joins
-                if self.xgmi is not None:
-                    self.engine.attach_xgmi(None)
-                    self.xgmi = None
-            self.setup.add("stream_probe", time.perf_counter() - _t_probe)
-        if self.xgmi is not None and os.environ.get("MNIST_AMD_XGMI_VALIDATE", "1") != "0":
-            _t_val, _cap0 = time.perf_counter(), self.setup.s.get("graph_capture", 0.0)
-            ok, self.xgmi_validation = self._validate_xgmi_schedule(train)
-            # (the training graph it captures is booked under graph_capture)
-            self.setup.add("validation", time.perf_counter() - _t_val - (self.setup.s.get("graph_capture", 0.0) - _cap0))
-            if not ok:
-                if comm is None:
-                    raise RuntimeError(f"xGMI schedule failed its startup validation ({self.xgmi_validation}) "
-                                       "and no RCCL communicator to fall back to")
-                if rank == 0:
-                    print(f"[xgmi] startup validation failed ({self.xgmi_validation}): using RCCL", flush=True)
-                self.engine.attach_xgmi(None)
-                self.xgmi = None
-                self._graphs.clear()             # captured with the xGMI kernels: recapture on RCCL
-                self.engine.set_dist_schedule(sched)
-        if world_size > 1 and self.xgmi is None and comm is None:
-            # no transport left (xGMI setup / self-test / validation failed and no RCCL communicator
-            # was created, e.g. --allreduce xgmi): training on would let every rank drift apart
-            # silently with a gradient 1/world too small - fail instead
-            raise RuntimeError(f"world size {world_size}: the xGMI all-reduce is unavailable "
-                               f"({self.xgmi_validation or 'setup or self-test failed'}) and no RCCL "
-                               "communicator is attached; rerun with --allreduce rccl or auto")
-        self.allreduce = "xgmi" if self.xgmi is not None else "rccl"
+                release_xgmi_comm(x)
+                x = self.xgmi = None
+        if want_r:
+            self.engine.set_schedule(C.SCHED_RCCL)
+            self._use_graph_set("rccl")
+            ok, why, us = self._validate("rccl", train)
+            self.transport_report["rccl"] = {"ok": ok, "validation": why, "us_per_step": us}
+        valid = {k: v["us_per_step"] for k, v in self.transport_report.items() if v.get("ok")}
+        self.allreduce_timings = {k: round(v["us_per_step"], 2) for k, v in self.transport_report.items()
+                                  if v.get("us_per_step") is not None}
+        if not valid:
+            msg = "; ".join(f"{k}: {v.get('validation')}" for k, v in self.transport_report.items())
+            hint = "" if comm is not None else " (no RCCL communicator: rerun with --allreduce rccl or auto)"
+            raise StartupValidationError(f"world size {self.world}: no gradient all-reduce passed its startup "
+                                         f"validation ({msg or 'no candidate'}){hint}", self.transport_report,
+                                         self.setup)
+        pick = min(valid, key=valid.get)
+        if pick == "xgmi":
+            self.engine.attach_xgmi(x)
+            self.engine.set_schedule(C.SCHED_XGMI)
+        else:
+            if x is not None:
+                release_xgmi_comm(x)
+                x = self.xgmi = None
+            self.engine.set_schedule(C.SCHED_RCCL)
+        self._use_graph_set(pick)
+        self.allreduce = pick
         # the all-reduced gradients (xGMI: the communicator's output buffer; the inputs are written
         # to its input buffer instead of mstate.grad while it is attached)
         self.grad_out = self.xgmi.grad_out if self.xgmi is not None else None
-        self.setup.add("engine", time.perf_counter() - _t_init - self.setup.total())
+
+    def broadcast_params(self, x=None) -> None:
+        """DDP construction (reference mnist_ddp.py:173): rank 0's parameters to every rank, over the
+        framework's transport - the xGMI peer mappings, else the RCCL communicator, else (gloo
+        rehearsals) the process group - then the bf16 shadows are rebuilt."""
+        if self.world == 1:
+            return
+        x = x if x is not None else self.xgmi
+        from ..parallel.distributed import broadcast_, xgmi_broadcast_
+        with torch.cuda.stream(self.compute), self.setup.phase("broadcast"):
+            if x is not None:
+                xgmi_broadcast_(x, self.ms.param, 0)
+            elif self.comm is not None:
+                self.engine.broadcast_params(0)
+                self._wait_compute(RCCL_WATCHDOG_S, "RCCL parameter broadcast")
+            else:
+                broadcast_(self.ms.param, 0)
+            self.engine.refresh_shadows()
+            torch.cuda.synchronize(self.device)
+
+    def _wait_compute(self, timeout_s: float, what: str) -> None:
+        """Host watchdog on the compute stream (every chunk and step joins the comm stream into it)."""
+        ev = torch.cuda.Event()
+        ev.record(self.compute)
+        t0 = time.perf_counter()
+        while not ev.query():
+            if time.perf_counter() - t0 > timeout_s:
+                raise TransportHang(f"rank {self.rank}: {what} did not complete within {timeout_s:.0f} s "
+                                    "(a collective is stuck on the device)")
+            time.sleep(0.0002)
 
     # ------------------------------------------------------------------ startup validation
-    def _validate_xgmi_schedule(self, train: MNISTData) -> tuple[bool, str]:
-        """Run the production xGMI DDP schedule before training starts: the captured chunk graph of
-        ``graph_steps`` steps that training replays (cached and reused by training; eager steps only
-        when graphs are off), dropout off, STARTUP_TIMEOUT_S stage timeouts (baked into that graph's
-        kernel arguments), on the live state, which is restored bit for bit afterwards.  With the
-        fused kernels the separate-launch schedule runs too (its own graph, not kept) and must give
-        the same bits.  Passes when no rank timed out, fused == separate, and every rank holds the
-        same parameters afterwards.  Every mode's verdict is collective (all ranks stop at the first
-        failing mode, so no rank is left waiting in kernels its peers never launch) and the message
-        names every failing rank.  Fault injection for tests: ``MNIST_AMD_FAULT=validate_delay:R:S``
-        holds rank R's replay back S seconds (its peers' stage waits must time out)."""
-        from ..parallel.distributed import STARTUP_TIMEOUT_S, gather_strings, params_fingerprint_equal
+    def _validate(self, name: str, train: MNISTData) -> tuple[bool, str, float | None]:
+        """Run the selected production schedule before training starts: the captured chunk graph of
+        ``graph_steps`` steps that training replays (cached for training; eager steps when graphs are
+        off), dropout off, on the live state, which is restored bit for bit afterwards.  Passes when
+        no rank timed out (xGMI: STARTUP_TIMEOUT_S stage waits, read from device memory so the cached
+        graph picks up the run timeout afterwards; RCCL: a host watchdog of RCCL_WATCHDOG_S - a stuck
+        collective cannot be cancelled, so that raises TransportHang) and every rank holds the same
+        parameters afterwards.  Then the chunk is replayed ``VALIDATE_TIMED`` more times and timed:
+        the transport's µs per step (max over ranks) is the "auto" choice's measure.  The verdict is
+        collective and names every failing rank.  Fault injection for tests:
+        ``MNIST_AMD_FAULT=validate_delay:R:S`` holds rank R's replay back S seconds."""
+        from ..parallel.distributed import (RUN_TIMEOUT_S, STARTUP_TIMEOUT_S, _max_over_ranks, gather_strings,
+                                            params_fingerprint_equal)
+        _t0 = time.perf_counter()
         ms, eng = self.ms, self.engine
         n = self.graph_steps if self.use_graphs else 3
         n = max(1, min(n, self.steps_per_epoch))
@@ -292,60 +316,77 @@ class FusedTrainer:
         torch.cuda.synchronize(self.device)
         snap = {k: getattr(ms, k).clone() for k in keys}
         idx = torch.arange(n * self.B, dtype=torch.int64) % max(1, len(train))
-        modes = [True, False] if self.xgmi_fuse else [False]
         delay = _fault_delay("validate_delay", self.rank)
-        results, why = [], ""
-        self.xgmi.set_timeout_seconds(STARTUP_TIMEOUT_S)
-        for fuse in modes:
-            mode = "fused" if fuse else "separate"
-            t0 = time.perf_counter()
+        rccl = name == "rccl"
+        if self.xgmi is not None and not rccl:
+            self.xgmi.set_timeout_seconds(STARTUP_TIMEOUT_S)
+        why, us, result = "", None, None
+
+        def run_chunk():
+            eng.begin_epoch(self.seed, 0, 0, FLAG_NO_DROPOUT)
+            if self.use_graphs:
+                eng.replay(self._graph(n, self.B))
+            else:
+                eng.train_steps(n, self.B, self.B)
+
+        def wait():
+            if rccl:
+                self._wait_compute(RCCL_WATCHDOG_S, "RCCL schedule validation")
+            eng.synchronize()                        # raises on a stage / hand-off timeout
+
+        try:
+            self.upload_indices(idx)
+            if self.use_graphs:
+                self._graph(n, self.B)               # captured (and cached) before the clock
+            torch.cuda.synchronize(self.device)
+            if delay:
+                time.sleep(delay)
+            run_chunk()
+            wait()
+            result = ms.param.clone()
+            if not torch.isfinite(result).all():
+                why = f"rank {self.rank}: non-finite parameters"
+        except TransportHang:
+            raise
+        except RuntimeError as e:
+            why = f"rank {self.rank}: {e} (after {time.perf_counter() - _t0:.1f} s)"
+        msgs = gather_strings(why)                   # collective: every rank stops here together
+        why = "; ".join(m for m in msgs if m)
+        if not why and self.world > 1 and not params_fingerprint_equal(result):
+            why = "parameters differ across ranks after the validation chunk"
+        if not why:
+            # timed replays of the same chunk (state need not be restored in between: the numbers do
+            # not matter, the schedule's time does)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             try:
-                with torch.no_grad():
-                    for k in keys:
-                        getattr(ms, k).copy_(snap[k])
                 torch.cuda.synchronize(self.device)
-                eng.refresh_shadows()
-                eng.set_xgmi_fuse_update(fuse)
-                self.upload_indices(idx)
-                eng.begin_epoch(self.seed, 0, 0, FLAG_NO_DROPOUT)
-                if self.use_graphs:
-                    # the training graph itself for the trainer's mode; the other mode's is throwaway
-                    gid = self._graph(n, self.B) if fuse == self.xgmi_fuse else eng.capture_train(n, self.B, self.B)
-                    if delay:
-                        eng.synchronize()
-                        time.sleep(delay)
-                    eng.replay(gid)
-                else:
-                    eng.train_steps(n, self.B, self.B)
-                eng.synchronize()                       # raises on a stage / hand-off timeout
-                results.append(ms.param.clone())
-                if not torch.isfinite(results[-1]).all():
-                    why = f"{mode}: non-finite parameters"
+                ev0.record(self.compute)
+                for _ in range(VALIDATE_TIMED):
+                    run_chunk()
+                ev1.record(self.compute)
+                wait()
+                us = ev0.elapsed_time(ev1) * 1000.0 / (VALIDATE_TIMED * n)
+            except TransportHang:
+                raise
             except RuntimeError as e:
-                why = f"{mode}: {e} (after {time.perf_counter() - t0:.1f} s)"
-            msgs = gather_strings(why)                  # collective: every rank stops at the same mode
-            if any(msgs):
-                why = "; ".join(f"rank {r}: {m}" for r, m in enumerate(msgs) if m)
-                break
-        if not why and len(results) == 2 and not torch.equal(results[0], results[1]):
-            why = f"rank {self.rank}: fused kernels differ from the separate launches"
-        if self.world > 1:
-            ok_fp = not why and params_fingerprint_equal(results[0], self.device)
-            msgs = gather_strings(why or ("" if ok_fp else f"rank {self.rank}: parameters differ across ranks"))
-            why = "; ".join(sorted(set(m for m in msgs if m)))
+                why = f"rank {self.rank}: timed replay: {e}"
+            why = "; ".join(m for m in gather_strings(why) if m)
+            if not why:
+                us = _max_over_ranks(us)
         with torch.no_grad():
             for k in keys:
                 getattr(ms, k).copy_(snap[k])
         torch.cuda.synchronize(self.device)
         eng.refresh_shadows()
-        eng.set_xgmi_fuse_update(self.xgmi_fuse)
-        self.xgmi.set_timeout_seconds(60.0)
+        eng.reset_counters()                         # (an aborted chunk leaves the hand-offs unpaired)
+        if self.xgmi is not None and not rccl:
+            self.xgmi.set_timeout_seconds(RUN_TIMEOUT_S)
         torch.cuda.synchronize(self.device)
+        self.setup.add(f"validate.{name}", time.perf_counter() - _t0)
         if why:
-            return False, why
-        what = "fused == separate" if len(modes) == 2 else "separate"
+            return False, why, None
         how = f"graph replay of the {n}-step training chunk" if self.use_graphs else f"{n} eager steps"
-        return True, f"ok ({how}, {what})"
+        return True, f"ok ({how}, ranks bitwise equal, {VALIDATE_TIMED} timed replays)", us
 
     def reset_model(self, module) -> None:
         """Start over from ``module``'s parameters with fresh optimizer state (zero Adadelta
@@ -474,7 +515,7 @@ class FusedTrainer:
         dev_s = None
         if sync:
             self.compute.synchronize()
-            if self.xgmi is not None or self.comm is not None or self.overlap_fc:
+            if self.xgmi is not None or self.comm is not None or self.overlap:
                 self.check_errors()        # fail at the first bad epoch, not after the last one
             dev_s = ev0.elapsed_time(ev1) / 1000.0
         return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged, dev_s)
@@ -488,19 +529,9 @@ class FusedTrainer:
         self.rng_base += 2 * (idx.numel() // self.B)
 
     def _chunks(self, n: int) -> list[int]:
-        """Graph sizes ``run_steps(n)`` replays: ``graph_steps`` each, the last one shorter; with a
-        launch ramp (``self.ramp`` = r > 0) the first graphs are r, 2r, 4r, .. steps, so after a host
-        sync the GPU starts on a small graph while the host is still submitting the larger ones (a
-        graph's host-side launch grows with its node count, ~2.4 us per node on ROCm 7)."""
+        """Graph sizes ``run_steps(n)`` replays: ``graph_steps`` each, the last one shorter."""
         c = self.graph_steps if self.graph_steps > 0 else max(1, n)
-        k = min(self.ramp, c) if self.ramp > 0 else c
-        out = []
-        while n > 0:
-            take = min(k, n)
-            out.append(take)
-            n -= take
-            k = min(2 * k, c)
-        return out
+        return [min(c, n - k) for k in range(0, n, c)]
 
     def precapture(self, n: int) -> None:
         """Capture every graph ``run_steps(n)`` will replay (capture executes nothing)."""

@@ -231,7 +231,11 @@ class DistributedDataParallel(nn.Module):
         self.engine_managed = engine_managed
         params = [p for p in module.parameters() if p.requires_grad]
         self._verify_shapes(params)
-        self._sync_module_states()
+        if not engine_managed:
+            self._sync_module_states()
+        # engine_managed: the fused engine broadcasts rank 0's parameters itself, over its own
+        # transport, once that exists (FusedTrainer.broadcast_params) - a broadcast here would make
+        # ProcessGroupNCCL build a communicator only for it
         cap = (25.0 if bucket_cap_mb is None else bucket_cap_mb) * 1024 * 1024
         first = first_bucket_cap_mb * 1024 * 1024
         ready_order = list(reversed(range(len(params))))
@@ -250,6 +254,11 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ construction-time sync
     def _verify_shapes(self, params) -> None:
         digest = hashlib.sha1(repr([tuple(p.shape) for p in params]).encode()).digest()[:8]
+        if self.engine_managed:                  # host collective over the store (no device comm)
+            from .hostcomm import get_hostcomm
+            if not get_hostcomm().all_equal(digest):
+                raise RuntimeError("DDP: parameter shapes differ across ranks")
+            return
         mine = torch.tensor([int.from_bytes(digest, "little", signed=True)], dtype=torch.int64)
         dev = params[0].device if params and dist.get_backend(self.process_group) == "nccl" else torch.device("cpu")
         mine = mine.to(dev)

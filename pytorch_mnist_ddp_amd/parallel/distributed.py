@@ -1,4 +1,5 @@
-"""Process-group bootstrap: reference ``init_distributed_mode`` (mnist_ddp.py:13-37) + RCCL comm.
+"""Process-group bootstrap: reference ``init_distributed_mode`` (mnist_ddp.py:13-37) + the
+framework's communicators.
 
 Rank discovery order and printed lines are the reference's:
   (a) ``RANK`` and ``WORLD_SIZE`` in the environment (torchrun / torch.distributed.launch)
@@ -10,18 +11,25 @@ Then ``set_device(gpu)``, print ``| distributed init (rank r): url, local rank:g
 and ``init_process_group``.  The backend is ``"nccl"`` (= RCCL on ROCm) on GPU and ``"gloo"``
 for ``--no-cuda`` runs (the reference hardcodes nccl, which cannot work without a GPU).
 
-On top of that, :func:`create_rccl_comm` builds the framework's own RCCL communicator for the
-native gradient all-reduce: rank 0 draws an ``ncclUniqueId`` and publishes it through the c10d
-TCPStore that ``env://`` already created, every rank joins with ``ncclCommInitRank``.
+The process group is created lazily (no ``device_id``): ProcessGroupNCCL builds its RCCL
+communicator only on its first collective, and the fused engine never issues one - its gradient
+all-reduce runs on the framework's own RCCL communicator (:func:`create_rccl_comm`, uid through the
+c10d TCPStore) or on the direct xGMI kernels (:func:`create_xgmi_comm`), and its startup verdicts
+are host collectives over the same store (``hostcomm``).  So each rank initialises ONE RCCL
+communicator (or none with ``--allreduce xgmi``), and that one is created on a helper thread while
+the main thread builds data, model and trainer (:func:`start_rccl_comm`).
 """
 from __future__ import annotations
 
 import os
+import threading
 import time
 from datetime import timedelta
 
 import torch
 import torch.distributed as dist
+
+from .hostcomm import get_hostcomm
 
 
 def init_distributed_mode(args) -> None:
@@ -51,22 +59,24 @@ def init_distributed_mode(args) -> None:
         args.dist_backend = "gloo"
     print(f"| distributed init (rank {args.rank}): {args.dist_url}, local rank:{args.gpu}, "
           f"world size:{args.world_size}", flush=True)
-    kwargs = dict(backend=args.dist_backend, init_method=args.dist_url, world_size=args.world_size,
-                  rank=args.rank, timeout=timedelta(minutes=10))
-    if use_cuda and args.dist_backend == "nccl":
-        kwargs["device_id"] = torch.device("cuda", args.gpu)
-    dist.init_process_group(**kwargs)
+    dist.init_process_group(backend=args.dist_backend, init_method=args.dist_url, world_size=args.world_size,
+                            rank=args.rank, timeout=timedelta(minutes=10))
 
 
 _UID_KEY = "pytorch_mnist_ddp_amd/rccl_unique_id"
+_rccl_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
 
 
-def create_rccl_comm(world_size: int, rank: int, device: int, tag: str = "0"):
+def create_rccl_comm(world_size: int, rank: int, device: int, tag: str | None = None):
     """Framework-owned RCCL communicator (requires an initialised default process group)."""
     from ..ops import native
+    global _rccl_seq
     C = native.load()
     if not C.RcclComm.available():
         raise RuntimeError("RCCL not found in this process")
+    if tag is None:
+        tag = str(_rccl_seq)
+    _rccl_seq += 1
     store = dist.distributed_c10d._get_default_store()
     key = f"{_UID_KEY}/{tag}"
     if rank == 0:
@@ -78,6 +88,43 @@ def create_rccl_comm(world_size: int, rank: int, device: int, tag: str = "0"):
     return C.RcclComm(bytes(uid), world_size, rank, device)
 
 
+class PendingRcclComm:
+    """:func:`create_rccl_comm` on a helper thread (``ncclCommInitRank`` blocks for its bootstrap -
+    socket rendezvous, topology detection, channel setup - and releases the GIL meanwhile).
+    ``result()`` joins and returns the communicator (or re-raises its error); ``seconds`` is how
+    long the init took on the helper thread."""
+
+    def __init__(self, world_size: int, rank: int, device: int):
+        global _rccl_seq
+        self._tag = str(_rccl_seq)          # claimed now: the store keys follow the callers' order
+        _rccl_seq += 1
+        self._args = (world_size, rank, device)
+        self._comm, self._err, self.seconds = None, None, None
+        self._t = threading.Thread(target=self._run, name="rccl-init", daemon=True)
+        self._t.start()
+
+    def _run(self):
+        t0 = time.perf_counter()
+        try:
+            torch.cuda.set_device(self._args[2])
+            self._comm = create_rccl_comm(*self._args, tag=self._tag)
+        except BaseException as e:  # noqa: BLE001 - re-raised in result()
+            self._err = e
+        self.seconds = time.perf_counter() - t0
+
+    def result(self, timeout_s: float = 600.0):
+        self._t.join(timeout_s)
+        if self._t.is_alive():
+            raise RuntimeError(f"RCCL communicator init did not finish within {timeout_s:.0f} s")
+        if self._err is not None:
+            raise self._err
+        return self._comm
+
+
+def start_rccl_comm(world_size: int, rank: int, device: int) -> PendingRcclComm:
+    return PendingRcclComm(world_size, rank, device)
+
+
 def get_rank() -> int:
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
@@ -87,68 +134,40 @@ def get_world_size() -> int:
 
 
 def barrier() -> None:
-    if dist.is_available() and dist.is_initialized():
-        dist.barrier()
-
-
-def rccl_comm_count() -> int:
-    """Framework RCCL communicators the fused engine creates: 1 (default - both gradient buckets on
-    one communicator, ordered fc -> conv on the device, like DDP's single process group) or 2
-    (``MNIST_AMD_RCCL_COMMS=2``, opt-in: the fc bucket on its own communicator may overlap the conv
-    bucket's all-reduce; concurrent collectives on two communicators are deadlock-prone in NCCL/RCCL
-    when ranks interleave them differently, which is why it is not the default)."""
-    n = int(os.environ.get("MNIST_AMD_RCCL_COMMS", "1"))
-    if n not in (1, 2):
-        raise ValueError(f"MNIST_AMD_RCCL_COMMS must be 1 or 2, got {n}")
-    return n
-
-
-def create_rccl_comms(world_size: int, rank: int, device: int, n: int | None = None):
-    """``(comm, comm2)``: the engine's RCCL communicator and, when ``n`` (default
-    :func:`rccl_comm_count`) is 2, a second one for the fc bucket (else ``None``)."""
-    n = rccl_comm_count() if n is None else n
-    comms = [create_rccl_comm(world_size, rank, device, tag=str(i)) for i in range(n)]
-    return comms[0], (comms[1] if n > 1 else None)
-
+    """Host barrier of the default group's ranks (TCPStore; never creates a device communicator)."""
+    get_hostcomm().barrier()
 
 
 _XGMI_KEY = "pytorch_mnist_ddp_amd/xgmi_record"
 # stage-wait timeout of the startup self-test / schedule validation: long enough that a peer delayed
 # by the GPU's queue scheduling (many processes on one GPU in rehearsals) is not mistaken for a hang
 STARTUP_TIMEOUT_S = float(os.environ.get("MNIST_AMD_STARTUP_TIMEOUT", "15"))
+RUN_TIMEOUT_S = 60.0   # stage-wait timeout while training (covers rank 0's evaluation, host stalls)
 _xgmi_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
 
 
-def _all_ok(flag: bool, device) -> bool:
-    """Every rank's verdict (MIN over the default process group)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return flag
-    on_gpu = dist.get_backend() == "nccl"
-    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device if on_gpu else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    return bool(t.item())
+def _all_ok(flag: bool, device=None) -> bool:
+    """Every rank's verdict (host collective)."""
+    return get_hostcomm().all_ok(flag)
 
 
-def params_fingerprint_equal(t: torch.Tensor, device) -> bool:
-    """True when every rank's fp32 tensor ``t`` is bitwise identical (all-gather of a fingerprint)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+def _max_over_ranks(v: float, device=None) -> float:
+    return get_hostcomm().max(v)
+
+
+def params_fingerprint_equal(t: torch.Tensor, device=None) -> bool:
+    """True when every rank's fp32 tensor ``t`` is bitwise identical (fingerprints compared on the host)."""
+    hc = get_hostcomm()
+    if hc.world == 1:
         return True
     from .ddp import params_fingerprint
-    fp = params_fingerprint([t])
-    if dist.get_backend() != "nccl":
-        fp = fp.cpu()
-    allv = [torch.zeros_like(fp) for _ in range(dist.get_world_size())]
-    dist.all_gather(allv, fp)
-    return all(torch.equal(v, allv[0]) for v in allv)
+    fp = params_fingerprint([t]).cpu().numpy().tobytes()
+    return hc.all_equal(fp)
 
 
 def gather_strings(msg: str) -> list[str]:
-    """Every rank's ``msg`` in rank order (collective)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return [msg]
-    out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, msg)
-    return [str(m) for m in out]
+    """Every rank's ``msg`` in rank order (host collective)."""
+    return get_hostcomm().gather_strings(msg)
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> None:
@@ -164,6 +183,29 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> None:
         dist.broadcast(t, src=src)
 
 
+def xgmi_broadcast_(x, t: torch.Tensor, src: int = 0) -> None:
+    """``t`` (fp32, on this rank's GPU, at most the communicator's size) from rank ``src`` to every
+    rank through the xGMI communicator's IPC-mapped output buffers: ``src`` stages it, every other
+    rank copies it out of ``src``'s buffer over xGMI (DDP construction without any RCCL)."""
+    from ..ops import native
+    hc = get_hostcomm()
+    if hc.world == 1:
+        return
+    n = t.numel()
+    s = torch.cuda.current_stream(t.device)
+    if hc.rank == src:
+        x.stage_out(native.ptr(t), n, s.cuda_stream)
+    s.synchronize()
+    hc.barrier()
+    if hc.rank != src:
+        x.read_peer_out(src, native.ptr(t), n, s.cuda_stream)
+    s.synchronize()
+    hc.barrier()                 # every copy out of src's buffer is done before anyone reuses it
+    with torch.no_grad():
+        x.grad_out.zero_()
+    s.synchronize()
+
+
 def _device_identity(device) -> str:
     p = torch.cuda.get_device_properties(torch.device(device))
     return "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
@@ -174,10 +216,10 @@ def ranks_per_device(device) -> int:
     production layout; > 1 in the one-GPU multi-process rehearsal).  The xGMI kernels wait per
     workgroup on their peers, so the residency planner (``xgmi_plan_grids``) sizes their grids for
     this many ranks' spinning workgroups on one GPU."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    hc = get_hostcomm()
+    if hc.world == 1:
         return 1
-    ids = [None] * dist.get_world_size()
-    dist.all_gather_object(ids, _device_identity(device))
+    ids = hc.gather_strings(_device_identity(device))
     return max(ids.count(i) for i in ids)
 
 
@@ -224,15 +266,28 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     except RuntimeError as e:
         print(f"[xgmi] rank {rank}: setup failed ({e})", flush=True)
         ok = False
-    if not _all_ok(ok, dev):
+    if not _all_ok(ok):
+        release_xgmi_comm(x)
         return None
     if verify:
         ok = _verify_xgmi(x, world_size, rank, x.grad_in, x.grad_out, channels)
-        if not _all_ok(ok, dev):
+        if not _all_ok(ok):
             if rank == 0:
                 print("[xgmi] self-test failed: keeping the RCCL all-reduce", flush=True)
+            release_xgmi_comm(x)
             return None
     return x
+
+
+def release_xgmi_comm(x) -> None:
+    """Collective teardown of an xGMI communicator: every rank unmaps its peers, then (host barrier)
+    the buffers may be recycled by a later communicator of the same shape.  Call on every rank;
+    ``x`` may be None on some (a failed setup), the barrier still matches."""
+    if x is not None:
+        x.close_peers()
+    get_hostcomm().barrier()
+    if x is not None:
+        x.mark_recyclable()
 
 
 def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torch.Tensor, channels: int) -> bool:
@@ -250,7 +305,7 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
     x.set_timeout_seconds(STARTUP_TIMEOUT_S)
     ok = True
     try:
-        for it in range(3):                              # repeated calls exercise the per-WG counters
+        for it in range(2):                              # repeated calls exercise the per-WG counters
             scale = float(it + 1)
             # every rank must be done READING the previous call's output shards before anyone
             # rewrites its buffers from outside the kernel protocol (the fill below): the kernels only
@@ -292,7 +347,7 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
         print(f"[xgmi] rank {rank}: self-test error ({e})", flush=True)
         ok = False
     finally:
-        x.set_timeout_seconds(60.0)
+        x.set_timeout_seconds(RUN_TIMEOUT_S)
         # the last call's peers may still be READING this rank's output shard (all-gather phase): the
         # host-side zeroing below is outside the kernels' hand-off protocol, so every rank first waits
         # until all ranks have finished their last call (seen at W = 8 on one GPU: a fast rank zeroed
@@ -303,61 +358,3 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
             grad_out.zero_()
         torch.cuda.synchronize(grad_in.device)
     return ok
-
-
-def _max_over_ranks(v: float, device) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return v
-    on_gpu = dist.get_backend() == "nccl"
-    t = torch.tensor([v], dtype=torch.float64, device=device if on_gpu else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def time_bucket_allreduce(calls, device, iters: int = 20, warmup: int = 3) -> float:
-    """Microseconds per invocation of ``calls`` (a list of zero-argument launchers enqueued on the
-    current stream), max over ranks; all ranks must call this collectively."""
-    for _ in range(warmup):
-        for c in calls:
-            c()
-    torch.cuda.synchronize(device)
-    barrier()
-    t0 = torch.cuda.Event(enable_timing=True)
-    t1 = torch.cuda.Event(enable_timing=True)
-    t0.record()
-    for _ in range(iters):
-        for c in calls:
-            c()
-    t1.record()
-    t1.synchronize()
-    return _max_over_ranks(t0.elapsed_time(t1) * 1000.0 / iters, device)
-
-
-def choose_allreduce(rccl_fc, rccl_conv, xgmi, grad: torch.Tensor, fc_range: tuple[int, int],
-                     conv_range: tuple[int, int], device, rccl_extra=None) -> tuple[str, dict]:
-    """Measure one step's two bucket all-reduces with RCCL and with the direct xGMI kernel on this
-    node and return the faster (``"rccl"`` / ``"xgmi"``) plus the timings - the same decision on
-    every rank (timings are maxima over ranks).  ``grad`` is the RCCL side's flat buffer; the xGMI
-    side runs on the communicator's own buffers.  ``rccl_extra`` (zero-argument launchers) is work
-    only the RCCL schedule has on its critical path - the separate conv-bucket update that the xGMI
-    kernels fuse - and is timed into the RCCL side.  Buffers are zeroed afterwards."""
-    from ..ops import native
-    s = torch.cuda.current_stream(device).cuda_stream
-    gp = native.ptr(grad)
-    with torch.no_grad():
-        grad.zero_()
-        xgmi.grad_in.zero_()
-    rc = [lambda: rccl_fc.allreduce_sum(gp + 4 * fc_range[0], fc_range[1], 0, s),
-          lambda: rccl_conv.allreduce_sum(gp + 4 * conv_range[0], conv_range[1], 0, s)] + list(rccl_extra or [])
-    xc = [lambda: xgmi.allreduce(1, fc_range[0], fc_range[1], s),
-          lambda: xgmi.allreduce(0, conv_range[0], conv_range[1], s)]
-    t_r = time_bucket_allreduce(rc, device)
-    t_x = time_bucket_allreduce(xc, device)
-    err = _max_over_ranks(float(xgmi.error()), device)
-    with torch.no_grad():
-        grad.zero_()
-        xgmi.grad_in.zero_()
-        xgmi.grad_out.zero_()
-    torch.cuda.synchronize(device)
-    pick = "xgmi" if (err == 0 and t_x < t_r) else "rccl"
-    return pick, {"rccl_us": round(t_r, 1), "xgmi_us": round(t_x, 1)}

@@ -54,6 +54,7 @@ class PhaseTimes:
 
     def __init__(self):
         self.s: dict[str, float] = {}
+        self.info: dict[str, float] = {}   # seconds spent off the critical path (helper threads)
 
     @contextlib.contextmanager
     def phase(self, name: str):
@@ -66,9 +67,15 @@ class PhaseTimes:
     def add(self, name: str, seconds: float) -> None:
         self.s[name] = self.s.get(name, 0.0) + seconds
 
+    def add_info(self, name: str, seconds: float | None) -> None:
+        if seconds is not None:
+            self.info[name] = round(float(seconds), 4)
+
     def update(self, other: "PhaseTimes | dict", prefix: str = "") -> None:
         for k, v in (other.s if isinstance(other, PhaseTimes) else other).items():
             self.add(prefix + k, v)
+        if isinstance(other, PhaseTimes):
+            self.info.update({prefix + k: v for k, v in other.info.items()})
 
     def rounded(self, nd: int = 4) -> dict[str, float]:
         return {k: round(v, nd) for k, v in self.s.items()}

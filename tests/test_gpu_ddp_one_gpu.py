@@ -73,18 +73,25 @@ def test_mnist_ddp_xgmi_without_rccl(cuda_device, tmp_path, W):
     setups = [x for x in recs if "setup_s" in x]
     assert len(setups) == W and all(x["allreduce"] == "xgmi" for x in setups)
     for x in setups:
-        assert {"pg_init", "data", "ddp_wrap", "trainer.xgmi_comm", "trainer.validation"} <= set(x["setup_s"])
-        assert "rccl_comms" not in x["setup_s"]                 # --allreduce xgmi: no RCCL communicator
+        assert {"pg_init", "data", "ddp_wrap", "trainer.xgmi_comm", "trainer.validate.xgmi"} <= set(x["setup_s"])
+        assert not any(k.startswith("rccl") for k in x["setup_s"])   # --allreduce xgmi: no RCCL communicator
+        assert x["transport_report"]["xgmi"]["ok"] and x["transport_report"]["xgmi"]["us_per_step"] > 0
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("W", [2, 8])
-def test_bench_reports_correctness(cuda_device, tmp_path, W):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
-           "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(W), "--steps", "20", "--warmup", "5", "--epochs", "2", "--dist-backend", "gloo",
-           "--allreduce", "xgmi"] + (["--no-script-run"] if W > 4 else [])   # W ranks + a W-rank child
-    # job would hold 2W processes on the one GPU (the box allows 16)
+@pytest.mark.parametrize("W,launcher", [(2, "torchrun"), (8, "self")])
+def test_bench_reports_correctness(cuda_device, tmp_path, W, launcher):
+    """``bench.py --gpus W`` under torchrun, and (W = 8) launching its W ranks itself with no launcher
+    (the driver's plain command): ONE JSON line with n_gpus W, params in sync, the transport, its
+    validation and the per-phase setup seconds."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(W), "--steps", "20", "--warmup", "5", "--epochs", "2",
+            "--dist-backend", "gloo", "--allreduce", "xgmi"] + (["--no-script-run"] if W > 4 else [])
+    # (W ranks + a W-rank child job would hold 2W processes on the one GPU; the box allows 16)
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+               "--nnodes", "1", "--nproc-per-node", str(W)] + args
+    else:
+        cmd = [sys.executable] + args
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=tmp_path, env=_env())
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -94,7 +101,10 @@ def test_bench_reports_correctness(cuda_device, tmp_path, W):
     assert j["config"]["allreduce"] == "xgmi" and j["config"]["rccl_world"] is None
     assert j["config"]["rccl_comms"] == 0 and j["config"]["xgmi_ordering"].startswith("uncached")
     assert j["config"]["xgmi_validation"].startswith("ok (graph replay")
-    assert "trainer.validation" in j["setup_phases_s"] and "warm_replay" in j["setup_phases_s"]
+    assert j["config"]["transport_report"]["xgmi"]["us_per_step"] > 0
+    assert "trainer.validate.xgmi" in j["setup_phases_s"] and "warm_replay" in j["setup_phases_s"]
+    if launcher == "self":
+        assert j["launcher"]["child_rc"] == 0 and j["launcher"]["kind"].startswith("bench.py self-launch")
     if W <= 4:
         rs = j["reference_script"]
         assert rs["rc"] == 0 and rs["ranks_reporting"] == W, rs
@@ -119,3 +129,27 @@ def test_validation_fault_in_replayed_graph_is_named(cuda_device, tmp_path):
     assert "failed its startup validation" in err, err[-3000:]
     assert "timed out" in err and "rank " in err, err[-3000:]
     assert "Train Epoch" not in r.stdout                         # nothing trained on the bad comm
+
+
+@pytest.mark.timeout(200)
+def test_bench_startup_fault_reports_json(cuda_device, tmp_path):
+    """The same fault through ``bench.py --gpus 4`` (self-launched ranks): rank 0 still prints ONE
+    JSON line - value null, the failing phase, the decoded error and every rank's failure record
+    with its transport report and setup phases - and the exit code is non-zero."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "20", "--warmup", "5",
+           "--no-full-run", "--dist-backend", "gloo", "--allreduce", "xgmi", "--batch-size", "100"]
+    env = _env(MNIST_AMD_FAULT="validate_delay:2:6", MNIST_AMD_STARTUP_TIMEOUT="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=tmp_path, env=env)
+    assert r.returncode != 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    j = json.loads(lines[0])
+    assert j["value"] is None and j["n_gpus"] == 4 and j["failed_phase"] == "trainer"
+    assert "no gradient all-reduce passed its startup validation" in j["error"]
+    assert "timed out" in j["error"]
+    recs = j["rank_failures"]
+    assert "0" in recs and len(recs) >= 2, recs.keys()
+    r0 = recs["0"]
+    assert {"pg_init", "data_model", "trainer.xgmi_comm", "trainer.validate.xgmi"} <= set(r0["setup_phases_s"])
+    assert r0["transport_report"]["xgmi"]["ok"] is False and "timed out" in r0["transport_report"]["xgmi"]["validation"]
+    assert j["launcher"]["child_rc"] != 0

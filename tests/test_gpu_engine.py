@@ -61,24 +61,30 @@ def test_partial_last_batch_and_dry_run(cuda_device):
 
 
 @pytest.mark.parametrize("graph_steps", [0, 3, 4])
-def test_fused_fc_update_bitwise_equals_step_tail_update(cuda_device, graph_steps):
-    """fc_bwd's fused fc Adadelta epilogue (w1t ping-pong, odd and even chunk lengths, eager) ==
-    the separate step-tail update, bit for bit, including every bf16 shadow."""
+def test_overlap_schedule_bitwise_equals_serial(cuda_device, graph_steps):
+    """The OVERLAP schedule (fc update and conv2's reduce + update on the comm stream with device-
+    counter hand-offs, w2d ping-pong across odd and even chunk lengths, split side / compute graphs
+    launched from two threads, or eager) == the SERIAL one-stream schedule, bit for bit, including
+    every bf16 shadow and the evaluation after training (the side-stream schedules had
+    only manual A/B evidence)."""
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(5))
-    _, ms_f, tf = _trainer(cuda_device, graph_steps=graph_steps, fuse_fc_update=True)
-    _, ms_u, tu = _trainer(cuda_device, graph_steps=graph_steps, fuse_fc_update=False)
+    _, ms_o, to = _trainer(cuda_device, graph_steps=graph_steps, overlap=True)
+    _, ms_s, ts = _trainer(cuda_device, graph_steps=graph_steps, overlap=False)
+    assert to.overlap and not ts.overlap
+    C = to.C
+    assert to.engine.schedule == C.SCHED_OVERLAP and ts.engine.schedule == C.SCHED_SERIAL
     for ep in (1, 2):
-        tf.train_epoch(ep, idx)
-        tu.train_epoch(ep, idx)
+        to.train_epoch(ep, idx)
+        ts.train_epoch(ep, idx)
     torch.cuda.synchronize()
-    for name in ("param", "grad", "square_avg", "acc_delta", "w1", "w1t", "w2f", "w2d"):
-        assert torch.equal(getattr(ms_f, name), getattr(ms_u, name)), name
-    assert torch.equal(tf.loss_log, tu.loss_log)
-    w1 = ms_f.views(ms_f.param)["fc1.weight"]
-    assert torch.equal(ms_f.w1t.view(9216, 128), w1.t().contiguous().to(torch.bfloat16))
-    lf, cf, _ = tf.evaluate()
-    lu, cu, _ = tu.evaluate()
-    assert lf == lu and cf == cu
+    for name in ("param", "square_avg", "acc_delta", "w1", "w1t", "w2f", "w2d"):
+        assert torch.equal(getattr(ms_o, name), getattr(ms_s, name)), name
+    assert torch.equal(to.loss_log, ts.loss_log)
+    w1 = ms_o.views(ms_o.param)["fc1.weight"]
+    assert torch.equal(ms_o.w1t.view(9216, 128), w1.t().contiguous().to(torch.bfloat16))
+    lo, co, _ = to.evaluate()
+    ls, cs, _ = ts.evaluate()
+    assert lo == ls and co == cs
 
 
 def test_whole_split_eval_bitwise_equals_test_batch_chunks(cuda_device):
@@ -113,7 +119,7 @@ def test_torch_profiler_sees_native_kernels(cuda_device):
 
 
 def test_stream_handoff_probe(cuda_device):
-    """The schedule-3 precondition check: compute and comm streams progress independently (each
+    """The OVERLAP / XGMI precondition check: compute and comm streams progress independently (each
     waits on a device counter the other signals afterwards) and the probe is repeatable."""
     _, ms, t = _trainer(cuda_device, graph_steps=0)
     assert t.engine.probe_stream_handoff(2.0)
@@ -161,42 +167,6 @@ def test_module_path_reuses_step_buffers(cuda_device):
     assert sum(len(v) for v in st.pool.values()) == 1
 
 
-def test_single_gpu_overlapped_fc_update_bitwise_equal(cuda_device, monkeypatch):
-    """MNIST_AMD_OVERLAP_FC (default): the fc Adadelta step on the comm stream (device-counter hand-offs)
-    gives the bits of the serial single-GPU schedule."""
-    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(9))
-    monkeypatch.setenv("MNIST_AMD_OVERLAP_FC", "0")
-    _, ms_s, ts = _trainer(cuda_device, graph_steps=4)
-    assert not ts.overlap_fc
-    monkeypatch.setenv("MNIST_AMD_OVERLAP_FC", "1")
-    _, ms_o, to = _trainer(cuda_device, graph_steps=4)
-    assert to.overlap_fc
-    ts.train_epoch(1, idx)
-    to.train_epoch(1, idx)
-    to.synchronize()
-    torch.cuda.synchronize()
-    assert torch.equal(ms_s.param, ms_o.param) and torch.equal(ts.loss_log, to.loss_log)
-    assert torch.equal(ms_s.w1t, ms_o.w1t) and torch.equal(ms_s.w2f, ms_o.w2f)
-
-
-def test_dgrad_update_bitwise_equal(cuda_device, monkeypatch):
-    """MNIST_AMD_DGRAD_UPDATE (default): the conv2 slab reduce + update as extra workgroups of the
-    dgrad launch (w2d ping-pong across steps, odd graph chunks end on the alternate copy) gives the
-    bits of the separate step-tail launch; the eval after training sees the current shadows."""
-    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(13))
-    monkeypatch.setenv("MNIST_AMD_DGRAD3", "0")          # the dgrad-launch update rides the 4-strip dgrad
-    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "0")
-    _, ms_a, ta = _trainer(cuda_device, graph_steps=3)
-    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "1")
-    _, ms_b, tb = _trainer(cuda_device, graph_steps=3)
-    ta.train_epoch(1, idx)
-    tb.train_epoch(1, idx)
-    tb.synchronize()
-    torch.cuda.synchronize()
-    assert torch.equal(ms_a.param, ms_b.param) and torch.equal(ta.loss_log, tb.loss_log)
-    assert torch.equal(ms_a.w2f, ms_b.w2f) and torch.equal(ms_a.w2d, ms_b.w2d)
-
-
 def test_large_batch_conv1_prereduce_matches_functional(cuda_device):
     """B = 512 (4B > C1_PRE_MIN_SLABS): the engine pre-reduces the 4B conv1 partial rows in 256
     fixed-order groups before the conv reduce; its gradients equal the functional path's (one pass
@@ -233,87 +203,53 @@ def test_large_batch_conv1_prereduce_matches_functional(cuda_device):
         assert err < 1e-4, (name, err)
 
 
-@pytest.mark.parametrize("B", [200, 512])
-def test_dgrad_strip_forms_agree(cuda_device, monkeypatch, B):
-    """conv2_dgrad in 3 strips (9/9/8 rows, conv2 weights from L2) and in 4 strips (7 rows, weights in
-    LDS): identical per-pixel math; only the conv1 gradient partials are grouped differently, so the
-    trained parameters agree to fp32 summation-order level."""
-    idx = torch.randperm(B * 4, generator=torch.Generator().manual_seed(17))
-    out = {}
-    for form in ("0", "1"):
-        monkeypatch.setenv("MNIST_AMD_DGRAD3", form)
-        _, ms, t = _trainer(cuda_device, graph_steps=2, n_train=B * 4, B=B, dropout=False)
-        t.train_epoch(1, idx)
-        t.synchronize()
-        torch.cuda.synchronize()
-        out[form] = (ms.param.clone(), t.loss_log.clone())
-    p4, l4 = out["0"]
-    p3, l3 = out["1"]
-    assert torch.isfinite(p3).all()
-    rel = ((p3 - p4).norm() / p4.norm()).item()
-    assert rel < 1e-5, rel
-    assert (l3 - l4).abs().max().item() < 1e-3
-
-
-@pytest.mark.parametrize("B,grid", [(200, "1"), (200, "37"), (512, "512")])
-def test_dgrad_persistent_bitwise_equal(cuda_device, monkeypatch, B, grid):
+@pytest.mark.parametrize("B,grid", [(200, 800), (200, 37), (512, 512)])
+def test_dgrad_persistent_grid_independent(cuda_device, B, grid):
     """Persistent conv2_dgrad (conv2 weights staged once per workgroup, items it, it+G, ... with the
-    next item's loads in flight under the MFMA loop; default) gives the bits of the per-item grid,
-    including a small odd grid (37 workgroups: ~22 items each, ragged last round)."""
+    next item's loads in flight under the MFMA loop): any grid gives the bits of the default one -
+    one item per workgroup (4B), a small odd grid (37 workgroups: ~22 items each, ragged last round)."""
     idx = torch.randperm(B * 4, generator=torch.Generator().manual_seed(23))
     out = {}
-    monkeypatch.setenv("MNIST_AMD_DGRAD3", "0")
-    monkeypatch.setenv("MNIST_AMD_DGRAD_UPDATE", "0")
-    for form in ("0", grid):
-        monkeypatch.setenv("MNIST_AMD_DGRAD_PERSIST", form)
-        _, ms, t = _trainer(cuda_device, graph_steps=2, n_train=B * 4, B=B)
-        t.train_epoch(1, idx)
-        t.synchronize()
-        torch.cuda.synchronize()
-        out[form] = (ms.param.clone(), t.loss_log.clone(), ms.grad.clone())
-    a, b = out["0"], out[grid]
+    C = None
+    try:
+        for g in (0, grid):
+            from pytorch_mnist_ddp_amd.ops import native
+            C = native.load()
+            C.set_dgrad_grid(g)
+            _, ms, t = _trainer(cuda_device, graph_steps=2, n_train=B * 4, B=B)
+            t.train_epoch(1, idx)
+            t.synchronize()
+            torch.cuda.synchronize()
+            out[g] = (ms.param.clone(), t.loss_log.clone(), ms.grad.clone())
+    finally:
+        if C is not None:
+            C.set_dgrad_grid(0)
+    a, b = out[0], out[grid]
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
 
 
 @pytest.mark.parametrize("B", [200, 512])
-def test_wgrad_staggered_halves_agree(cuda_device, monkeypatch, B):
+def test_wgrad_staggered_halves_agree(cuda_device, B):
     """conv2_wgrad with two staggered 4-wave halves (alternate chunks, accumulators summed half 0 +
-    half 1; the large-batch default) vs the 8-wave lockstep kernel: the same conv gradients up to
-    fp32 summation order, and each form repeats bit for bit."""
+    half 1; the large-batch default) vs the 8-wave lean kernel: the same conv gradients up to fp32
+    summation order, and each form repeats bit for bit."""
+    from pytorch_mnist_ddp_amd.ops import native
+    C = native.load()
     idx = torch.randperm(B, generator=torch.Generator().manual_seed(29))
     grads = {}
-    for form in ("0", "1", "1"):
-        monkeypatch.setenv("MNIST_AMD_WGRAD_STAG", form)
-        _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=B, B=B, dropout=False)
-        t.train_epoch(1, idx)
-        t.synchronize()
-        torch.cuda.synchronize()
-        g = ms.grad.clone()
-        if form in grads:
-            assert torch.equal(grads[form], g)
-        grads[form] = g
-    g0, g1 = grads["0"], grads["1"]
-    rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < 1e-5, rel
-
-
-@pytest.mark.parametrize("B", [200, 512])
-def test_wgrad_lean_matches_previous_kernels(cuda_device, monkeypatch, B):
-    """VALU-lean conv2_wgrad (planar a1 tile, k -> pixel remap, bias on a ones-tile MFMA; B = 512 takes
-    the lean staggered form) vs the previous kernels (MNIST_AMD_WGRAD_LEAN=0): the same conv gradients
-    up to fp32 summation order, and the lean form repeats bit for bit."""
-    idx = torch.randperm(B, generator=torch.Generator().manual_seed(31))
-    grads = {}
-    for form in ("0", "1", "1"):
-        monkeypatch.setenv("MNIST_AMD_WGRAD_LEAN", form)
-        _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=B, B=B, dropout=False)
-        t.train_epoch(1, idx)
-        t.synchronize()
-        torch.cuda.synchronize()
-        g = ms.grad.clone()
-        if form in grads:
-            assert torch.equal(grads[form], g)
-        grads[form] = g
-    g0, g1 = grads["0"], grads["1"]
+    try:
+        for form in (0, 1, 1):
+            C.set_wgrad_form(form)
+            _, ms, t = _trainer(cuda_device, graph_steps=0, n_train=B, B=B, dropout=False, overlap=False)
+            t.train_epoch(1, idx)
+            t.synchronize()
+            torch.cuda.synchronize()
+            g = ms.grad.clone()
+            if form in grads:
+                assert torch.equal(grads[form], g)
+            grads[form] = g
+    finally:
+        C.set_wgrad_form(-1)
+    g0, g1 = grads[0], grads[1]
     rel = ((g1 - g0).norm() / g0.norm()).item()
     assert rel < 1e-5, rel

@@ -129,26 +129,25 @@ def test_ddp_wrapper_and_engine_ddp_schedule_on_one_gpu(cuda_device):
         for a_, b_, c_ in zip(*grads):
             assert torch.equal(a_, b_) and torch.equal(a_, c_)
         # engine with an attached RCCL communicator: fc bucket all-reduce + Adadelta on the comm
-        # stream overlapped with the conv backward, captured into graphs; must equal no-comm run
+        # stream overlapped with the conv backward, captured into graphs; must equal no-comm runs
         C = native.load()
         comm = C.RcclComm(C.RcclComm.unique_id(), 1, 0, 0)
-        comm2 = C.RcclComm(C.RcclComm.unique_id(), 1, 0, 0)
         tr = load_mnist(synthetic_data=True, train=True, synthetic_size=1024, verbose=False)
         idx = torch.randperm(1024, generator=torch.Generator().manual_seed(0))
         res = []
-        # schedule 1 (one comm), schedule 2 (cross-step fc branch, two comms), eager schedule 2,
-        # schedule 3 with RCCL and with the xGMI all-reduce (world 1: its output buffer path), no comm
-        for c, c2, gs, sched, ar in ((comm, None, 4, 1, "rccl"), (comm, None, 4, 3, "rccl"),
-                                     (comm, None, 0, 3, "rccl"), (comm, comm2, 4, 2, "rccl"),
-                                     (comm, comm2, 0, 2, "rccl"), (comm, comm2, 4, 3, "rccl"),
-                                     (comm, comm2, 0, 3, "rccl"), (comm, comm2, 4, 3, "xgmi"),
-                                     (comm, comm2, 0, 3, "xgmi"), (None, None, 4, 1, "rccl")):
+        # RCCL schedule (graphs / eager / one bucket), xGMI schedule (world 1: its output buffer path;
+        # fused and separate launches, graphs / eager), single GPU OVERLAP and SERIAL
+        for c, gs, ar, kw, sched in ((comm, 4, "rccl", {}, C.SCHED_RCCL), (comm, 0, "rccl", {}, C.SCHED_RCCL),
+                                     (comm, 4, "rccl", {"two_buckets": False}, C.SCHED_RCCL),
+                                     (comm, 4, "xgmi", {}, C.SCHED_XGMI), (comm, 0, "xgmi", {}, C.SCHED_XGMI),
+                                     (comm, 4, "xgmi", {"xgmi_fuse": False}, C.SCHED_XGMI),
+                                     (None, 4, None, {"overlap": False}, C.SCHED_SERIAL),
+                                     (None, 4, None, {}, C.SCHED_OVERLAP)):
             torch.manual_seed(5)
             ms = ModelState(Net(), cuda_device)
-            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=gs, comm2=c2,
-                             allreduce=ar)
-            assert t.allreduce == ar
-            t.engine.set_dist_schedule(sched)
+            t = FusedTrainer(ms, tr, None, 128, 1, num_samples=1024, comm=c, graph_steps=gs,
+                             allreduce=ar or "auto", **kw)
+            assert t.allreduce == ar and t.engine.schedule == sched, (ar, kw)
             t.train_epoch(1, idx)
             t.synchronize()
             res.append(ms.param.clone())

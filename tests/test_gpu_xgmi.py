@@ -27,84 +27,77 @@ def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps, f
     assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
 
 
-def test_allreduce_auto_choice_plumbing_world1(cuda_device):
-    """choose_allreduce at world 1 (RCCL comms + the xGMI communicator's copy path): both launch
-    sequences run, the timings come back and the buffers are left zeroed."""
+def _world1_trainer(dev, comm, **kw):
+    import torch
+    from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+    from pytorch_mnist_ddp_amd.engine.state import ModelState
+    from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer
+    from pytorch_mnist_ddp_amd.models.net import Net
+    torch.manual_seed(1)
+    ms = ModelState(Net(), dev, lr=1.0)
+    train = load_mnist(train=True, synthetic_data=True, synthetic_size=2000, verbose=False)
+    t = FusedTrainer(ms, train, None, 200, 1000, num_samples=2000, comm=comm, seed=1, graph_steps=4, **kw)
+    return ms, t
+
+
+def test_transport_choice_by_schedule_replay_world1(cuda_device):
+    """--allreduce auto picks the transport by replaying each candidate's PRODUCTION schedule: at
+    world 1 with an RCCL communicator and the xGMI candidate forced in (probe_world1), both captured
+    chunk graphs are validated and timed (us per step in transport_report), the faster is kept, and
+    training on it is bitwise the single-transport runs (RCCL schedule; xGMI schedule) - the
+    validation replays leave no trace in the model, the optimizer state or the step counter."""
     import torch
     import torch.distributed as dist
     from conftest import init_world1_pg
-    from pytorch_mnist_ddp_amd.parallel.distributed import choose_allreduce, create_rccl_comms, create_xgmi_comm
+    from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comm
     init_world1_pg("nccl", cuda_device)
     try:
-        c0, c1 = create_rccl_comms(1, 0, 0, n=2)
-        n, split = 1200000, 1181120
-        g = torch.randn(n, device=cuda_device)
-        x = create_xgmi_comm(1, 0, cuda_device, n)
-        assert x is not None
-        gin, gout = x.grad_in, x.grad_out
-        assert gin.shape == (n,) and gin.is_cuda and gin.data_ptr() != gout.data_ptr()
-        gin.normal_()
-        gout.normal_()
-        pick, t = choose_allreduce(c1, c0, x, g, (0, split), (split, n - split), cuda_device)
-        assert pick in ("rccl", "xgmi") and t["rccl_us"] > 0 and t["xgmi_us"] > 0
-        for b in (g, gin, gout):
-            assert int(b.abs().sum().item()) == 0
+        comm = create_rccl_comm(1, 0, 0)
+        idx = torch.randperm(2000, generator=torch.Generator().manual_seed(4))
+        res = {}
+        for name, kw in (("auto", dict(allreduce="auto", probe_world1=True)), ("rccl", dict(allreduce="rccl")),
+                         ("xgmi", dict(allreduce="xgmi"))):
+            ms, t = _world1_trainer(cuda_device, comm, **kw)
+            if name == "auto":
+                rep = t.transport_report
+                assert set(rep) == {"xgmi", "rccl"}, rep
+                assert all(r["ok"] and r["us_per_step"] > 0 for r in rep.values()), rep
+                assert rep["xgmi"]["validation"].startswith("ok (graph replay of the 4-step")
+                fast = min(rep, key=lambda k: rep[k]["us_per_step"])
+                assert t.allreduce == fast
+                assert set(t.setup.s) >= {"validate.xgmi", "validate.rccl", "xgmi_comm", "stream_probe"}
+            else:
+                assert t.allreduce == name and set(t.transport_report) == {name}
+            assert ms.get_step() == 0
+            t.train_epoch(1, idx)
+            t.synchronize()
+            res[name] = (ms.param.clone(), t.loss_log.clone())
+        for name in ("rccl", "xgmi"):
+            assert torch.equal(res[name][0], res["auto"][0]) and torch.equal(res[name][1], res["auto"][1]), name
     finally:
         dist.destroy_process_group()
 
 
-def test_trainer_auto_probe_path_world1(tmp_path):
-    """The trainer's --allreduce auto path (probe of both implementations on scratch optimizer
-    state, forced at world 1) runs and leaves training bit-identical to a plain RCCL run."""
-    outs = {}
-    for name, env in (("auto", {"MNIST_AMD_PROBE_ALWAYS": "1"}), ("rccl", {"MNIST_AMD_ALLREDUCE": "rccl"})):
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--standalone",
-               "--local-addr", "127.0.0.1", os.path.join(ROOT, "bench.py"),
-               "--force-comm", "--no-full-run", "--steps", "40", "--warmup", "10"]
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
-                           env=dict(os.environ, PYTHONPATH=ROOT, **env))
-        assert r.returncode == 0, r.stderr[-3000:]
-        import json
-        outs[name] = json.loads(r.stdout.strip().splitlines()[-1])
-    assert outs["auto"]["config"]["allreduce_probe_us"]["rccl_us"] > 0
-    assert outs["auto"]["last_train_loss"] == outs["rccl"]["last_train_loss"]
-
-
-@pytest.mark.timeout(200)
-@pytest.mark.parametrize("mode", ["1", "comm"])
-def test_conv_bucket_split_bitwise_at_two_ranks(cuda_device, mode):
-    """Opt-in conv bucket split (MNIST_AMD_CONV_SPLIT=1: a third stream, =comm: queued on the comm
-    stream after the fc bucket, inside the side graph): the startup validation inside the engine
-    check compares it bitwise with the separate launches, at 2 ranks on one GPU (4 HW queues per
-    process: the split's third stream needs its own queue)."""
-    cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "xgmi_check.py"), "--world", "2", "--same-device",
-           "--iters", "10", "--engine-steps", "20", "--timeout", "170"]
-    env = dict(os.environ, PYTHONPATH=ROOT, MNIST_AMD_CONV_SPLIT=mode, GPU_MAX_HW_QUEUES="4")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=185, env=env)
-    print(r.stdout[-3000:])
-    assert r.returncode == 0 and "XGMI_CHECK PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
-    assert ("conv split True" if mode == "1" else "conv split comm") in r.stdout
-
-
-def test_rccl_single_communicator_schedule_world1(tmp_path):
-    """DDP schedule 3 on ONE RCCL communicator (the default: fc all-reduce on the comm stream, the
-    conv all-reduce on the compute stream ordered after it by a device counter) trains bitwise like
-    the opt-in two-communicator schedule and like the plain single-GPU step (world 1, --force-comm)."""
+def test_rccl_schedule_world1_matches_single_gpu(tmp_path):
+    """The RCCL DDP schedule (fc bucket forked onto the comm stream, conv bucket after the join, one
+    communicator, one graph per chunk in step order) at world 1 (--force-comm) trains bitwise like the
+    plain single-GPU step, and the bench JSON names one communicator and the startup validation."""
     import json
     outs = {}
-    runs = (("one", ["--force-comm"], {}), ("two", ["--force-comm"], {"MNIST_AMD_RCCL_COMMS": "2"}),
-            ("plain", [], {}))
-    for name, extra, env in runs:
+    runs = (("rccl", ["--force-comm"]), ("plain", []))
+    for name, extra in runs:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--standalone",
                "--local-addr", "127.0.0.1", os.path.join(ROOT, "bench.py"), "--allreduce", "rccl",
                "--no-full-run", "--steps", "60", "--warmup", "10", *extra]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
-                           env=dict(os.environ, PYTHONPATH=ROOT, **env))
+                           env=dict(os.environ, PYTHONPATH=ROOT))
         assert r.returncode == 0, (name, r.stderr[-3000:])
         outs[name] = json.loads(r.stdout.strip().splitlines()[-1])
-    assert outs["one"]["config"]["rccl_comms"] == 1 and outs["two"]["config"]["rccl_comms"] == 2
-    assert outs["plain"]["config"]["rccl_comms"] == 0
-    assert outs["one"]["last_train_loss"] == outs["two"]["last_train_loss"] == outs["plain"]["last_train_loss"]
+    c = outs["rccl"]["config"]
+    assert c["rccl_comms"] == 1 and c["rccl_world"] == 1 and c["allreduce"] == "rccl" and c["schedule"] == "rccl"
+    assert c["transport_report"]["rccl"]["ok"] and c["allreduce_schedule_us"]["rccl"] > 0
+    assert outs["plain"]["config"]["rccl_comms"] == 0 and outs["plain"]["config"]["schedule"] == "overlap"
+    assert outs["rccl"]["last_train_loss"] == outs["plain"]["last_train_loss"]
 
 
 def test_world_gt1_without_transport_refuses(cuda_device, monkeypatch):

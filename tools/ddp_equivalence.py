@@ -14,8 +14,8 @@ materialised) against the world-1 gradient of the W*B batch, ||g_W - g_1|| / ||g
 after S fused steps, ||p_W - p_1|| / ||p_1|| <= max(1e-3, 3 x noise).  The noise floors are the same
 world-1 runs perturbed only in fp32 summation order, the max over: the rows of every batch permuted
 (shards in reverse order; a full random permutation of each step's W*B rows) and a different
-decomposition of the same sums (the large-batch conv1 pre-reduce toggled; conv2_dgrad in 3 strips
-instead of 4, which regroups the conv1 gradient partials).  W ranks at B rows and
+decomposition of the same sums (the other conv2-wgrad kernel form, which accumulates the conv2
+weight gradient in a different order).  W ranks at B rows and
 one rank at W*B rows run different kernel decompositions (fc1 split-K, fc_bwd K blocking, per-rank
 then cross-rank sums), so row permutations alone - which keep the decomposition - under-sample the
 order sensitivity of the first, nearly sign-like Adadelta steps.
@@ -57,16 +57,12 @@ def _train(torch, dev, world, rank, B, steps, rows, allreduce, fuse=True, grads=
     torch.manual_seed(1)
     ms = ModelState(Net(), dev, lr=1.0)
     train = load_mnist(train=True, synthetic_data=True, verbose=False)
-    comm = comm2 = None
+    comm = None
     if grads and world == 1:
         C = native.load()
-        comm, comm2 = (C.RcclComm(C.RcclComm.unique_id(), 1, 0, dev.index or 0) for _ in range(2))
-    os.environ["MNIST_AMD_XGMI_FUSE"] = "1" if fuse else "0"
-    try:
-        tr = FusedTrainer(ms, train, None, B, 1000, num_samples=steps * B, world_size=world, rank=rank, seed=1,
-                          graph_steps=5, dropout=False, allreduce=allreduce, comm=comm, comm2=comm2)
-    finally:
-        os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
+        comm = C.RcclComm(C.RcclComm.unique_id(), 1, 0, dev.index or 0)
+    tr = FusedTrainer(ms, train, None, B, 1000, num_samples=steps * B, world_size=world, rank=rank, seed=1,
+                      graph_steps=5, dropout=False, allreduce=allreduce, comm=comm, xgmi_fuse=fuse)
     if world > 1:
         assert tr.allreduce == "xgmi", f"xGMI unavailable ({tr.xgmi_validation})"
     tr.start_stream(rows, gather=True)
@@ -115,21 +111,17 @@ def worker(rank, world, port, args, q):
             gp = torch.Generator().manual_seed(7)
             shuffled = torch.stack([st.reshape(-1)[torch.randperm(W * B, generator=gp)] for st in stream])
             samples = []
-            flip_pre = {"MNIST_AMD_C1_PREREDUCE": "0" if os.environ.get("MNIST_AMD_C1_PREREDUCE") != "0" else "1"}
-            flip_dg = {"MNIST_AMD_DGRAD3": "1" if os.environ.get("MNIST_AMD_DGRAD3") != "1" else "0"}
-            for name, perm, env in (("shards reversed", stream.flip(1), {}), ("rows shuffled", shuffled, {}),
-                                    ("conv1 pre-reduce toggled", stream, flip_pre),
-                                    ("dgrad strips 4<->3", stream, flip_dg)):
-                saved = {k: os.environ.get(k) for k in env}
-                os.environ.update(env)
+            from pytorch_mnist_ddp_amd.ops import native
+            C = native.load()
+            # both conv2-wgrad forms (one buffer pair / staggered halves; the default is one of them):
+            # the same sums in a different accumulation order
+            for name, perm, form in (("shards reversed", stream.flip(1), -1), ("rows shuffled", shuffled, -1),
+                                     ("wgrad lean form", stream, 0), ("wgrad staggered form", stream, 1)):
+                C.set_wgrad_form(form)
                 try:
                     p1r, l1r, _ = _train(torch, dev, 1, 0, W * B, S, perm.reshape(-1), "rccl")
                 finally:
-                    for k, v in saved.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
+                    C.set_wgrad_form(-1)
                 p1r, l1r = p1r.cpu(), l1r.cpu()
                 n = float((p1r - p1).norm() / p1.norm())
                 samples.append(f"{name} {n:.2e}")

@@ -141,24 +141,16 @@ def _fault_check(torch, dist, world, rank, dev, x, s) -> str:
 def _engine_check(torch, dist, world, rank, dev, steps) -> str:
     """Fused (all-reduce + update kernels) and separate-launch xGMI schedules must give the same bits."""
     res = []
-    modes = os.environ.get("XGMI_CHECK_FUSE_MODES", "1,0").split(",")
-    for fuse in modes:                   # "1" / "0" pin the schedule; "auto" = the trainer's default
-        if fuse == "auto":
-            os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
-        else:
-            os.environ["MNIST_AMD_XGMI_FUSE"] = fuse
+    for fuse in (True, False):
         try:
-            res.append(_engine_run(torch, dist, world, rank, dev, steps))
+            res.append(_engine_run(torch, dist, world, rank, dev, steps, fuse))
         except Exception as e:
-            raise RuntimeError(f"engine run with MNIST_AMD_XGMI_FUSE={fuse}: {e}") from e
-    os.environ.pop("MNIST_AMD_XGMI_FUSE", None)
-    if len(res) == 1:
-        return res[0][1] + f", fuse={modes[0]} only"
+            raise RuntimeError(f"engine run with xgmi_fuse={fuse}: {e}") from e
     assert torch.equal(res[0][0], res[1][0]), "fused updates differ from the separate launches"
     return res[0][1] + ", fused == separate launches"
 
 
-def _engine_run(torch, dist, world, rank, dev, steps):
+def _engine_run(torch, dist, world, rank, dev, steps, fuse=True):
     from pytorch_mnist_ddp_amd.data.datasets import load_mnist
     from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream
     from pytorch_mnist_ddp_amd.engine.state import ModelState
@@ -170,7 +162,7 @@ def _engine_run(torch, dist, world, rank, dev, steps):
     train = load_mnist(train=True, synthetic_data=True, verbose=False)
     sampler = DistributedIndexStream(len(train), world, rank, shuffle=True, seed=0)
     tr = FusedTrainer(ms, train, None, B, 1000, num_samples=steps * B, world_size=world, rank=rank,
-                      seed=1, graph_steps=10, dropout=False, allreduce="xgmi")
+                      seed=1, graph_steps=10, dropout=False, allreduce="xgmi", xgmi_fuse=fuse)
     assert tr.allreduce == "xgmi", f"engine fell back to RCCL ({tr.xgmi_validation})"
     sampler.set_epoch(1)
     idx = sampler.epoch_indices()[: steps * B]
@@ -186,8 +178,8 @@ def _engine_run(torch, dist, world, rank, dev, steps):
     assert torch.isfinite(losses).all(), "non-finite loss"
     first, last = float(losses[:5].mean()), float(losses[-5:].mean())
     assert last < first, f"loss did not decrease ({first:.4f} -> {last:.4f})"
-    return p, (f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical; conv split "
-               f"{tr.conv_split}; startup validation {tr.xgmi_validation})")
+    return p, (f"engine ok ({steps} steps, loss {first:.3f} -> {last:.3f}, params identical; "
+               f"startup validation {tr.xgmi_validation})")
 
 
 def main() -> int:
