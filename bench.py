@@ -113,6 +113,13 @@ def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 9
             ep = [rc for rc in recs if "epoch" in rc]
             if ep:
                 out["epochs_train_s_rank_sum"] = round(sum(rc.get("train_s", 0.0) for rc in ep), 3)
+            tls = [rc["timeline_s"] for rc in recs if "timeline_s" in rc]
+            if tls:                  # wall-clock marks since the timer's start, max over ranks
+                keys = list(dict.fromkeys(k for t in tls for k in t))
+                tl = {k: max(t.get(k, 0.0) for t in tls) for k in keys}
+                out["timeline_s"] = {k: tl[k] for k in keys if not k.startswith("epoch") or k.startswith(("epoch1_", f"epoch{epochs}_"))}
+                out["timeline_epochs_s"] = round(tl.get(f"epoch{epochs}_eval", tl.get(f"epoch{epochs}_train", 0.0))
+                                                 - tl.get("trainer", 0.0), 3)
         except (OSError, ValueError):
             pass
         finally:

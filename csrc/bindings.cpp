@@ -13,6 +13,17 @@
 #include "runtime/rccl_comm.h"
 
 namespace py = pybind11;
+
+#ifdef MNIST_TIMELINE
+namespace mnist {
+void tl_dump_trunk(std::vector<uint64_t>&);
+void tl_dump_fc_head(std::vector<uint64_t>&);
+void tl_dump_conv_bwd(std::vector<uint64_t>&);
+void tl_dump_adadelta(std::vector<uint64_t>&);
+void tl_dump_comm(std::vector<uint64_t>&);
+void tl_dump_xgmi(std::vector<uint64_t>&);
+}  // namespace mnist
+#endif
 using namespace mnist;
 
 namespace {
@@ -352,6 +363,23 @@ PYBIND11_MODULE(_C, m) {
       .def_static("describe_xgmi_error", &Engine::describe_xgmi_error)
       .def_property_readonly("workspace_bytes", &Engine::workspace_bytes);
 
+#ifdef MNIST_TIMELINE
+  m.attr("TIMELINE") = true;
+  // every instrumented wave since the last dump as little-endian uint64 triples (kernel id, start,
+  // end; s_memrealtime ticks of 10 ns); the rings are rewound
+  m.def("timeline_dump", []() {
+    std::vector<uint64_t> v;
+    tl_dump_trunk(v);
+    tl_dump_fc_head(v);
+    tl_dump_conv_bwd(v);
+    tl_dump_adadelta(v);
+    tl_dump_comm(v);
+    tl_dump_xgmi(v);
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(uint64_t));
+  });
+#else
+  m.attr("TIMELINE") = false;
+#endif
   m.def("roctx_push", [](const std::string& s) { roctx_push(s.c_str()); });
   m.def("roctx_pop", []() { roctx_pop(); });
 }

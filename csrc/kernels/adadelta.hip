@@ -14,6 +14,7 @@
 // lr is read from device memory so a captured graph picks up StepLR changes.
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 #include "conv_grad_reduce.h"
 
 #include <stdexcept>
@@ -101,6 +102,7 @@ __device__ __forceinline__ void fc1_tile(const AdadeltaArgs& a, const Ada& ad, i
 
 template <bool UPDATE>
 __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int region) {
+  TL_SCOPE(region == ADA_FC ? TL_ADA_FC : region == ADA_CONV ? TL_ADA_CONV : TL_ADA_ALL);
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
   int bid = blockIdx.x;
@@ -122,6 +124,7 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
 // single-GPU schedule updates the fc parameters on the comm stream and splits conv2 / conv1)
 __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int conv_only,
                                                               int bid0) {
+  TL_SCOPE(!conv_only ? TL_RED_ALL : bid0 == 0 ? TL_RED_CONV2 : TL_RED_CONV1);
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   __shared__ float4 red[256];
   int bid = blockIdx.x;
@@ -174,5 +177,7 @@ __global__ void set_state_kernel(StepState* st, StepState v) { *st = v; }
 void launch_set_state(StepState* st, const StepState& v, hipStream_t s) {
   hipLaunchKernelGGL(set_state_kernel, dim3(1), dim3(1), 0, s, st, v);
 }
+
+TL_DEFINE_HOST(adadelta)
 
 }  // namespace mnist

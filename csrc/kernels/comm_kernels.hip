@@ -2,6 +2,7 @@
 // parameter's gradient into its bucket view, pre-scaled by 1/world_size (torch DDP's
 // "divide before all-reduce", reducer.hpp copy_grad_to_bucket), 16 B per lane where aligned.
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 
 namespace mnist {
 
@@ -43,10 +44,12 @@ namespace mnist {
 // e.g. rank 0's test-set evaluation) sets err and returns (no GPU hang on a protocol bug); once err
 // is set every later wait returns immediately and Engine::synchronize() raises.
 __global__ void stream_signal_kernel(int* ctr) {
+  TL_SCOPE(TL_SIGNAL);
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* err, uint64_t timeout_ticks) {
+  TL_SCOPE(TL_WAIT);
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
@@ -83,6 +86,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
                                                           const int32_t* __restrict__ idx, int64_t start,
                                                           int64_t n, uint8_t* __restrict__ dst_u8,
                                                           int32_t* __restrict__ dst_labels) {
+  TL_SCOPE(TL_GATHER);
   constexpr int CH = 784 / 16;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -100,6 +104,8 @@ void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const 
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src_u8, src_labels,
                      idx, start, n, dst_u8, dst_labels);
 }
+
+TL_DEFINE_HOST(comm)
 
 }  // namespace mnist
 

@@ -18,6 +18,7 @@
 //    the 1/(B*world) DDP averaging).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 #include "conv_grad_reduce.h"
 
 #include <stdexcept>
@@ -451,6 +452,7 @@ __device__ __forceinline__ void dgrad_compute(const ConvBwdArgs& a, int strip, i
 // conv1-gradient MFMA, c1part row) does not depend on the grid: any G gives the same bits.
 template <int XM>
 __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs a, int B) {
+  TL_SCOPE(TL_DGRAD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[DG_LDS];
   const int tid = threadIdx.x, n = 4 * B, G = gridDim.x;
   int it = blockIdx.x;
@@ -680,6 +682,7 @@ __device__ __forceinline__ void wl_mfma(const unsigned char* buf, int nks, int b
 }  // namespace
 
 __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArgs a, int B) {
+  TL_SCOPE(TL_WGRAD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // 8 waves = 2 co-tile pairs x 4 groups of the 18 (tap, ci-half) n-tiles (5, 5, 4, 4); the two
@@ -762,6 +765,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
 // waves (61 VGPRs) stay co-resident under it (at 250 they could not, and the overlapped update was
 // held back until wgrad ended: B = 8192 0.986 -> 1.051 ms/step)
 __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdArgs a, int B) {
+  TL_SCOPE(TL_WGRAD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[WG_LDS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int half = wave >> 2, hw = wave & 3, htid = tid & 255;
@@ -851,6 +855,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
 // --------------------------------------------------------------------------------------------
 // Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
+  TL_SCOPE(TL_CONV_REDUCE);
   __shared__ float4 red[256];
   float* grad = a.grad;
   reduce_conv_grads(a, B, blockIdx.x, red, [grad](int64_t e, float v) { grad[e] = v; });
@@ -863,6 +868,7 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
 // then the 3 slices are added in order.
 __global__ __launch_bounds__(256) void c1_prereduce_kernel(const float* __restrict__ c1part, int nslab,
                                                            float* __restrict__ c1red) {
+  TL_SCOPE(TL_C1_PRE);
   __shared__ float4 sh[240];
   const int j = blockIdx.x, tid = threadIdx.x;
   const int R = (nslab + C1_PRE_SLABS - 1) / C1_PRE_SLABS;
@@ -930,5 +936,7 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_WGS), dim3(256), 0, s, a, B);
 }
+
+TL_DEFINE_HOST(conv_bwd)
 
 }  // namespace mnist

@@ -5,6 +5,7 @@
 // and their autograd backward at :72.
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 
 #include <stdexcept>
 #include <stdlib.h>
@@ -76,6 +77,7 @@ template <int MR>
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
                                                       const uint16_t* __restrict__ w1,
                                                       float* __restrict__ z1part, int B) {
+  TL_SCOPE(TL_FC1);
   fc1_tile<MR>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
 }
 
@@ -96,6 +98,7 @@ __device__ __forceinline__ int f1b_swz(int row) { return (row >> 1) & 7; }
 __global__ __launch_bounds__(256) void fc1_fwd_big_kernel(const uint16_t* __restrict__ p,
                                                           const uint16_t* __restrict__ w1,
                                                           float* __restrict__ z1part, int B) {
+  TL_SCOPE(TL_FC1);
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * F1B_STAGE];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m = lane & 15, kg = lane >> 4;
@@ -356,6 +359,7 @@ __device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, 
 
 template <int KS, bool IDX>
 __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
+  TL_SCOPE(TL_HEAD);
   head_train_row<KS, IDX>(a, B, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
@@ -719,6 +723,7 @@ __host__ __device__ inline int fc_bwd_role_b_wgs(int B) {
 // workgroups [C | A | B]; bid0 offsets a partial grid (launch_fc_bwd_role)
 template <bool BIG>
 __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
+  TL_SCOPE(TL_FC_BWD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -740,6 +745,7 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
 // [0, OFF_FC2_B + 10)), scaled by grad_scale (1.0 from the engine: the head carries 1/(B*world)),
 // plus the mean loss.
 __global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B, int S) {
+  TL_SCOPE(TL_FC_BWD);
   constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;   // float4 columns (the tail pads into fc2.b's pad)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < N4) {
@@ -785,5 +791,7 @@ void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t
   if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
   else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
 }
+
+TL_DEFINE_HOST(fc_head)
 
 }  // namespace mnist

@@ -18,6 +18,7 @@
 //     across launch geometries and graph replays.
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 
 namespace mnist {
 
@@ -90,6 +91,7 @@ enum TrunkX { TX_PRE = 0, TX_IDX = 1, TX_XIN = 2 };
 
 template <bool TRAIN, int NS, int XM>
 __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(TrunkFwdArgs a) {
+  TL_SCOPE(TL_TRUNK);
   using K = TrunkCfg<NS>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[K::LDS];
   float* xs = reinterpret_cast<float*>(smem + K::XS_OFF);
@@ -366,5 +368,7 @@ void launch_trunk_fwd(const TrunkFwdArgs& a, int B, bool train, hipStream_t s) {
     else launch_trunk<false, 1>(a, dim3(3, B), s);
   }
 }
+
+TL_DEFINE_HOST(trunk)
 
 }  // namespace mnist

@@ -52,6 +52,7 @@
 
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
+#include "../include/timeline.h"
 #include "../runtime/host_logic.h"
 #include "conv_grad_reduce.h"
 
@@ -138,6 +139,7 @@ __device__ __forceinline__ void ada_update4(const XgmiArgs& a, const Ada& ad, in
 // edges need no guards, and a zero-length descriptor turns a load into a no-op.
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
+  TL_SCOPE(TL_XGMI_TWOSHOT);
   __shared__ int s_epoch, s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
@@ -225,6 +227,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
 // hand-off per call suffices (the two-shot kernel needs two).
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
+  TL_SCOPE(TL_XGMI_ONESHOT);
   __shared__ int s_epoch, s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
@@ -335,6 +338,7 @@ __device__ __forceinline__ int fcu_f4(int u, int h, int tid) {
 
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
+  TL_SCOPE(TL_XGMI_FC);
   constexpr int PU = W <= 2 ? 2 : 1;                             // phase-1 units in flight per lane
   constexpr int PG = 2;                                          // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;
@@ -499,6 +503,7 @@ constexpr int CONV_SLOTS_PER_LANE = CONV_SLOTS / 256;
 
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a, ConvBwdArgs c, int B, XgmiConvPart part) {
+  TL_SCOPE(part.lo == 0 ? TL_XGMI_CONV2 : TL_XGMI_CONV);
   __shared__ float4 red[256];
   __shared__ float s_val[CONV_SLOTS];
   __shared__ int s_idx[CONV_SLOTS];
@@ -699,5 +704,7 @@ XgmiGrids xgmi_plan_grids(int world, int co_ranks, int64_t oneshot_max_floats, d
                              " ranks per GPU cannot all be resident");
   return g;
 }
+
+TL_DEFINE_HOST(xgmi)
 
 }  // namespace mnist

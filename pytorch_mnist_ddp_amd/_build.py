@@ -25,6 +25,9 @@ OBJ_DIR = os.path.join(ROOT, "build", "obj")
 ARCH = "gfx950"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
+# debug variant with the in-kernel timeline (csrc/include/timeline.h): same module name, own file
+OBJ_DIR_TL = os.path.join(ROOT, "build", "obj_tl")
+OUTPUT_TL = os.path.join(PKG_DIR, "_C_tl" + EXT_SUFFIX)
 
 
 def _hipcc() -> str:
@@ -66,9 +69,9 @@ def _headers() -> list[str]:
     return sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True))
 
 
-def _obj_path(src: str) -> str:
+def _obj_path(src: str, timeline: bool = False) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
-    return os.path.join(OBJ_DIR, rel + ".o")
+    return os.path.join(OBJ_DIR_TL if timeline else OBJ_DIR, rel + ".o")
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -78,9 +81,11 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def _compile(src: str, kernel: bool, verbose: bool) -> str:
-    obj = _obj_path(src)
+def _compile(src: str, kernel: bool, verbose: bool, timeline: bool = False) -> str:
+    obj = _obj_path(src, timeline)
     cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes()]
+    if timeline:
+        cmd.append("-DMNIST_TIMELINE")
     if kernel:
         cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
     else:
@@ -95,20 +100,22 @@ def _compile(src: str, kernel: bool, verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
-    """Compile + link the extension if anything changed; return the .so path."""
-    os.makedirs(OBJ_DIR, exist_ok=True)
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, timeline: bool = False) -> str:
+    """Compile + link the extension if anything changed; return the .so path.  ``timeline``: the
+    debug variant with in-kernel wave timestamps (``_C_tl``, loaded when MNIST_AMD_TIMELINE=1)."""
+    obj_dir, output = (OBJ_DIR_TL, OUTPUT_TL) if timeline else (OBJ_DIR, OUTPUT)
+    os.makedirs(obj_dir, exist_ok=True)
     kernels, host = sources()
     headers = _headers()
     todo = [(s, True) for s in kernels] + [(s, False) for s in host]
-    stale = [(s, k) for s, k in todo if force or _stale(_obj_path(s), [s, *headers])]
+    stale = [(s, k) for s, k in todo if force or _stale(_obj_path(s, timeline), [s, *headers])]
     jobs = jobs or min(8, max(1, len(stale)))
     if stale:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            list(ex.map(lambda sk: _compile(sk[0], sk[1], verbose), stale))
-    objs = [_obj_path(s) for s, _ in todo]
-    if force or stale or _stale(OUTPUT, objs):
-        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUTPUT + ".tmp", "-ldl"]
+            list(ex.map(lambda sk: _compile(sk[0], sk[1], verbose, timeline), stale))
+    objs = [_obj_path(s, timeline) for s, _ in todo]
+    if force or stale or _stale(output, objs):
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", output + ".tmp", "-ldl"]
         tl = _torch_lib_dir()
         if tl:  # resolve libamdhip64/librccl to the copies torch ships (one HIP runtime per process)
             cmd += ["-Wl,-rpath," + tl]
@@ -117,8 +124,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
-        os.replace(OUTPUT + ".tmp", OUTPUT)
-    return OUTPUT
+        os.replace(output + ".tmp", output)
+    return output
 
 
 def main(argv=None) -> int:
@@ -126,8 +133,9 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--timeline", action="store_true", help="debug variant with in-kernel timestamps (_C_tl)")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, timeline=a.timeline)
     print(out)
     return 0
 

@@ -80,13 +80,16 @@ def _test_module(model, device, loader):
 
 
 # ----------------------------------------------------------------------------- main flows
-def run(argv=None, ddp_script: bool = True) -> int:
+def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int:
+    # startup phases inside the reference timer (--json-log "setup_s") + wall-clock marks since the
+    # timer's start ("timeline_s": where the rest goes - epochs, evaluation, teardown)
+    setup = PhaseTimes(origin=t_start)
     args = cli.parse_args(ddp=ddp_script, argv=argv)
     args._ddp_script = ddp_script
     use_cuda = not args.no_cuda and torch.cuda.is_available()
     distributed, world, rank, gpu = False, 1, 0, 0
-    setup = PhaseTimes()             # startup phases inside the reference timer (--json-log "setup_s")
     args._setup = setup
+    setup.mark("args")
     if ddp_script:
         from .parallel.distributed import init_distributed_mode
         with setup.phase("pg_init"):
@@ -109,9 +112,11 @@ def run(argv=None, ddp_script: bool = True) -> int:
         with setup.phase("rccl_comm_start"):
             args._pending_comm = start_rccl_comm(world, rank, gpu)
 
+    setup.mark("pg_init")
     with setup.phase("data"):
         train_data = load_mnist(args.data_root, True, args.synthetic, args.synthetic_train_size, verbose=rank == 0)
         test_data = load_mnist(args.data_root, False, args.synthetic, args.synthetic_test_size, verbose=rank == 0)
+    setup.mark("data")
     if ddp_script:
         train_stream = (DistributedIndexStream(len(train_data), world, rank, shuffle=True) if distributed
                         else RandomIndexStream(len(train_data)))
@@ -175,6 +180,13 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     from .engine.trainer import FusedTrainer
     from .utils.profiling import roctx_range
     setup = args._setup
+    with setup.phase("hip_init"):            # HIP context + the first device allocation
+        torch.cuda.init()
+        torch.empty(1, device=device)
+    with setup.phase("native_load"):         # the _C extension (gfx950 code objects registered)
+        from .ops import native
+        native.load()
+    setup.mark("hip_native")
     t_model = time.perf_counter()
     ms = ModelState(model, device, lr=args.lr)
     model_for_save = model
@@ -205,6 +217,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
                            allreduce=allreduce, two_buckets=two_buckets)
+    setup.mark("trainer")
     if distributed and rank == 0 and trainer.allreduce_timings:
         print(f"| gradient all-reduce: {trainer.allreduce} (schedule us/step: {trainer.allreduce_timings})",
               flush=True)
@@ -228,6 +241,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         with roctx_range(f"train_epoch_{epoch}", args.profile):
             st = trainer.train_epoch(epoch, idx, args.log_interval,
                                      dry_run=args.dry_run, log_fn=log_fn if log_rank else None)
+        setup.mark(f"epoch{epoch}_train")
         if epoch == 1:                     # the trainer's phases include epoch 1's graph captures
             setup.update(trainer.setup, prefix="trainer.")
             _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
@@ -245,6 +259,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                 loss_sum, correct, n = trainer.evaluate()
             print(test_line(loss_sum / n, correct, n))
             rec.update(test_loss=loss_sum / n, correct=correct)
+            setup.mark(f"epoch{epoch}_eval")
         if distributed and args.check_sync:
             from .parallel.ddp import assert_params_in_sync
             trainer.synchronize()
@@ -252,7 +267,10 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         _json_log(args.json_log, rec)
         lr = lr * args.gamma                                   # scheduler.step()
     trainer.synchronize()
+    setup.mark("train_done")
     _save(args, model_for_save, distributed, rank, ddp_script)
+    setup.mark("saved")
+    _json_log(args.json_log, {"timeline_s": setup.marks})
 
 
 def _save(args, model, distributed, rank, ddp_script):
@@ -273,7 +291,7 @@ def main_mnist(argv=None) -> int:
 
 def main_mnist_ddp(argv=None) -> int:
     start = time.time()
-    rc = run(argv, ddp_script=True)
+    rc = run(argv, ddp_script=True, t_start=start)
     print(total_time_line(time.time() - start))
     sys.stdout.flush()
     return rc

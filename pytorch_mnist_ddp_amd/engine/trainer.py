@@ -174,7 +174,7 @@ class FusedTrainer:
         from ..parallel.distributed import STARTUP_TIMEOUT_S, _all_ok
         with self.setup.phase("stream_probe"):
             ok = bool(self.engine.probe_stream_handoff(STARTUP_TIMEOUT_S))
-            return _all_ok(ok) if self.world > 1 else ok
+            return _all_ok(ok, world=self.world)
 
     def _setup_single_gpu(self, overlap: bool) -> None:
         C = self.C
@@ -202,7 +202,7 @@ class FusedTrainer:
             if x is not None and not self._probe_streams():
                 if self.rank == 0:
                     print("[engine] compute/comm streams share a hardware queue: no xGMI schedule", flush=True)
-                release_xgmi_comm(x)
+                release_xgmi_comm(x, self.world)
                 x = None
             if x is None:
                 self.transport_report["xgmi"] = {"ok": False, "validation": "setup, self-test or stream probe failed"}
@@ -233,7 +233,7 @@ class FusedTrainer:
                 print(f"[xgmi] startup validation failed ({why})", flush=True)
             self.engine.attach_xgmi(None)           # detached while RCCL is evaluated (re-attached below)
             if not ok:
-                release_xgmi_comm(x)
+                release_xgmi_comm(x, self.world)
                 x = self.xgmi = None
         if want_r:
             self.engine.set_schedule(C.SCHED_RCCL)
@@ -255,7 +255,7 @@ class FusedTrainer:
             self.engine.set_schedule(C.SCHED_XGMI)
         else:
             if x is not None:
-                release_xgmi_comm(x)
+                release_xgmi_comm(x, self.world)
                 x = self.xgmi = None
             self.engine.set_schedule(C.SCHED_RCCL)
         self._use_graph_set(pick)
@@ -350,9 +350,9 @@ class FusedTrainer:
             raise
         except RuntimeError as e:
             why = f"rank {self.rank}: {e} (after {time.perf_counter() - _t0:.1f} s)"
-        msgs = gather_strings(why)                   # collective: every rank stops here together
+        msgs = gather_strings(why, self.world)       # collective: every rank stops here together
         why = "; ".join(m for m in msgs if m)
-        if not why and self.world > 1 and not params_fingerprint_equal(result):
+        if not why and self.world > 1 and not params_fingerprint_equal(result, world=self.world):
             why = "parameters differ across ranks after the validation chunk"
         if not why:
             # timed replays of the same chunk (state need not be restored in between: the numbers do
@@ -370,9 +370,9 @@ class FusedTrainer:
                 raise
             except RuntimeError as e:
                 why = f"rank {self.rank}: timed replay: {e}"
-            why = "; ".join(m for m in gather_strings(why) if m)
+            why = "; ".join(m for m in gather_strings(why, self.world) if m)
             if not why:
-                us = _max_over_ranks(us)
+                us = _max_over_ranks(us, world=self.world)
         with torch.no_grad():
             for k in keys:
                 getattr(ms, k).copy_(snap[k])

@@ -20,6 +20,9 @@ def load(build_if_missing: bool = True):
     global _C, _err
     if _C is not None:
         return _C
+    if os.environ.get("MNIST_AMD_TIMELINE") == "1":
+        _C = _load_timeline_variant(build_if_missing)
+        return _C
     try:
         _C = importlib.import_module("pytorch_mnist_ddp_amd._C")
         return _C
@@ -31,6 +34,26 @@ def load(build_if_missing: bool = True):
         _C = importlib.import_module("pytorch_mnist_ddp_amd._C")
         return _C
     raise RuntimeError(f"native extension pytorch_mnist_ddp_amd._C is not available: {_err}")
+
+
+def _load_timeline_variant(build_if_missing: bool):
+    """The debug build with in-kernel wave timestamps (``_C_tl``, csrc/include/timeline.h), imported
+    under the module name ``_C`` (its PyInit symbol) so every caller gets it."""
+    import importlib.util
+    import sys
+    import sysconfig
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "_C_tl" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RuntimeError(f"timeline build {path} missing (python -m pytorch_mnist_ddp_amd._build --timeline)")
+        from .. import _build
+        _build.build(timeline=True)
+    spec = importlib.util.spec_from_file_location("pytorch_mnist_ddp_amd._C", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["pytorch_mnist_ddp_amd._C"] = mod
+    return mod
 
 
 def available() -> bool:

@@ -133,9 +133,9 @@ def get_world_size() -> int:
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def barrier() -> None:
+def barrier(world: int | None = None) -> None:
     """Host barrier of the default group's ranks (TCPStore; never creates a device communicator)."""
-    get_hostcomm().barrier()
+    get_hostcomm(world).barrier()
 
 
 _XGMI_KEY = "pytorch_mnist_ddp_amd/xgmi_record"
@@ -146,18 +146,18 @@ RUN_TIMEOUT_S = 60.0   # stage-wait timeout while training (covers rank 0's eval
 _xgmi_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
 
 
-def _all_ok(flag: bool, device=None) -> bool:
+def _all_ok(flag: bool, device=None, world: int | None = None) -> bool:
     """Every rank's verdict (host collective)."""
-    return get_hostcomm().all_ok(flag)
+    return get_hostcomm(world).all_ok(flag)
 
 
-def _max_over_ranks(v: float, device=None) -> float:
-    return get_hostcomm().max(v)
+def _max_over_ranks(v: float, device=None, world: int | None = None) -> float:
+    return get_hostcomm(world).max(v)
 
 
-def params_fingerprint_equal(t: torch.Tensor, device=None) -> bool:
+def params_fingerprint_equal(t: torch.Tensor, device=None, world: int | None = None) -> bool:
     """True when every rank's fp32 tensor ``t`` is bitwise identical (fingerprints compared on the host)."""
-    hc = get_hostcomm()
+    hc = get_hostcomm(world)
     if hc.world == 1:
         return True
     from .ddp import params_fingerprint
@@ -165,9 +165,9 @@ def params_fingerprint_equal(t: torch.Tensor, device=None) -> bool:
     return hc.all_equal(fp)
 
 
-def gather_strings(msg: str) -> list[str]:
+def gather_strings(msg: str, world: int | None = None) -> list[str]:
     """Every rank's ``msg`` in rank order (host collective)."""
-    return get_hostcomm().gather_strings(msg)
+    return get_hostcomm(world).gather_strings(msg)
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> None:
@@ -188,7 +188,7 @@ def xgmi_broadcast_(x, t: torch.Tensor, src: int = 0) -> None:
     rank through the xGMI communicator's IPC-mapped output buffers: ``src`` stages it, every other
     rank copies it out of ``src``'s buffer over xGMI (DDP construction without any RCCL)."""
     from ..ops import native
-    hc = get_hostcomm()
+    hc = get_hostcomm(x.world_size)
     if hc.world == 1:
         return
     n = t.numel()
@@ -211,12 +211,12 @@ def _device_identity(device) -> str:
     return "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
 
 
-def ranks_per_device(device) -> int:
+def ranks_per_device(device, world: int | None = None) -> int:
     """Largest number of ranks of the default process group that drive one physical GPU (1 in the
     production layout; > 1 in the one-GPU multi-process rehearsal).  The xGMI kernels wait per
     workgroup on their peers, so the residency planner (``xgmi_plan_grids``) sizes their grids for
     this many ranks' spinning workgroups on one GPU."""
-    hc = get_hostcomm()
+    hc = get_hostcomm(world)
     if hc.world == 1:
         return 1
     ids = hc.gather_strings(_device_identity(device))
@@ -250,7 +250,7 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     _xgmi_seq += 1
     dev = torch.device(device)
     if co_ranks is None:
-        co_ranks = ranks_per_device(dev)
+        co_ranks = ranks_per_device(dev, world_size)
     x = None
     try:
         x = C.XgmiComm(world_size, rank, dev.index or 0, int(numel), channels, oneshot_max, co_ranks)
@@ -266,26 +266,27 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     except RuntimeError as e:
         print(f"[xgmi] rank {rank}: setup failed ({e})", flush=True)
         ok = False
-    if not _all_ok(ok):
-        release_xgmi_comm(x)
+    if not _all_ok(ok, world=world_size):
+        release_xgmi_comm(x, world_size)
         return None
     if verify:
         ok = _verify_xgmi(x, world_size, rank, x.grad_in, x.grad_out, channels)
-        if not _all_ok(ok):
+        if not _all_ok(ok, world=world_size):
             if rank == 0:
                 print("[xgmi] self-test failed: keeping the RCCL all-reduce", flush=True)
-            release_xgmi_comm(x)
+            release_xgmi_comm(x, world_size)
             return None
     return x
 
 
-def release_xgmi_comm(x) -> None:
+def release_xgmi_comm(x, world: int | None = None) -> None:
     """Collective teardown of an xGMI communicator: every rank unmaps its peers, then (host barrier)
     the buffers may be recycled by a later communicator of the same shape.  Call on every rank;
     ``x`` may be None on some (a failed setup), the barrier still matches."""
     if x is not None:
         x.close_peers()
-    get_hostcomm().barrier()
+        world = x.world_size
+    get_hostcomm(world).barrier()
     if x is not None:
         x.mark_recyclable()
 
@@ -310,7 +311,7 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
             # every rank must be done READING the previous call's output shards before anyone
             # rewrites its buffers from outside the kernel protocol (the fill below): the kernels only
             # protect their own next call (its stage 0), not host-side writes
-            barrier()
+            barrier(world)
             with torch.no_grad():
                 grad_in.copy_(base * (scale * (rank + 1)))
                 grad_out.fill_(float("nan"))
@@ -352,7 +353,7 @@ def _verify_xgmi(x, world: int, rank: int, grad_in: torch.Tensor, grad_out: torc
         # host-side zeroing below is outside the kernels' hand-off protocol, so every rank first waits
         # until all ranks have finished their last call (seen at W = 8 on one GPU: a fast rank zeroed
         # its output under a slow rank's phase-2 reads -> whole shards of zeros)
-        barrier()
+        barrier(world)
         with torch.no_grad():
             grad_in.zero_()
             grad_out.zero_()

@@ -104,11 +104,12 @@ _default: HostComm | None = None
 _default_pg = None
 
 
-def get_hostcomm() -> HostComm:
+def get_hostcomm(world: int | None = None) -> HostComm:
     """The process's host collectives over the default process group's store (world 1 when no
-    process group is initialised)."""
+    process group is initialised, or when the caller's job is a world of 1 - e.g. a single-rank
+    reference run inside a multi-rank tool's process group)."""
     global _default, _default_pg
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if world == 1 or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return _World1()
     pg = dist.distributed_c10d._get_default_group()
     if _default is None or _default_pg is not pg:

@@ -52,9 +52,16 @@ class PhaseTimes:
     startup work that lands inside the reference's ``Total cost time`` (mnist_ddp.py:200-203):
     process group, communicators, xGMI map + self-test, all-reduce probe, validation, capture."""
 
-    def __init__(self):
+    def __init__(self, origin: float | None = None):
         self.s: dict[str, float] = {}
         self.info: dict[str, float] = {}   # seconds spent off the critical path (helper threads)
+        # wall-clock marks in seconds since `origin` (time.time() of the reference timer's start):
+        # where the non-phase time goes (epochs, evaluation, teardown)
+        self.origin = time.time() if origin is None else origin
+        self.marks: dict[str, float] = {}
+
+    def mark(self, name: str) -> None:
+        self.marks[name] = round(time.time() - self.origin, 4)
 
     @contextlib.contextmanager
     def phase(self, name: str):

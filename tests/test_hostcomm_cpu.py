@@ -68,6 +68,7 @@ def _hc_worker(rank, world, port, q, mode):
                     q.put((rank, "no error"))
                 except RuntimeError as e:
                     q.put((rank, f"{time.perf_counter() - t0:.1f}|{e}"))
+            time.sleep(3.0)                           # keep rank 0's store up until every rank has read it
         reset_hostcomm()
     finally:
         dist.destroy_process_group()

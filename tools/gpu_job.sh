@@ -35,7 +35,7 @@ run_step() {
   case $kind in
     tests)
       [ $# -eq 0 ] && set -- tests
-      timeout -k 10 1500 python -u -m pytest "$@" -m gpu -x -q --timeout 300 --timeout-method thread \
+      timeout -k 10 1500 python -u -m pytest "$@" -m gpu -x -v --timeout 170 --timeout-method thread \
         > gpurun_out/tests.log 2>&1; local rc=$?
       tail -4 gpurun_out/tests.log; fatal $rc "tests $*";;
     smoke)
