@@ -69,11 +69,34 @@ inline WorkspaceLayout compute_workspace_layout(int max_batch, int max_test_batc
   return L;
 }
 
+// ---------------------------------------------------------------------------- xGMI export block
+// Everything a peer reads or writes lives in ONE exported allocation per rank, so a peer maps it
+// with one hipIpcOpenMemHandle (W-1 per rank instead of 4(W-1): the IPC import is the dominant
+// per-peer setup cost inside the reference's timer).  Regions 4 KiB aligned:
+//   in [numel f32] | out [numel f32] | flags [channels][XGMI_FLAG_INTS] | stage [channels][2][oneshot_max] (+4) | sig [4][4 int32]
+struct XgmiBlockLayout {
+  int64_t in_off, out_off, flags_off, stage_off, sig_off, bytes;
+};
+constexpr int64_t kXgmiSigBytes = 16;
+inline XgmiBlockLayout xgmi_block_layout(int64_t numel, int channels, int64_t oneshot_max) {
+  if (numel < 4 || channels < 1 || oneshot_max < 0) throw std::runtime_error("xgmi block layout: bad sizes");
+  auto al = [](int64_t x) { return (x + 4095) & ~int64_t(4095); };
+  XgmiBlockLayout L{};
+  L.in_off = 0;
+  L.out_off = al(L.in_off + 4 * numel);
+  L.flags_off = al(L.out_off + 4 * numel);
+  L.stage_off = al(L.flags_off + 4LL * XGMI_FLAG_INTS * channels);
+  L.sig_off = al(L.stage_off + 4LL * (2 * oneshot_max + 4) * channels);
+  L.bytes = al(L.sig_off + 4 * kXgmiSigBytes);
+  return L;
+}
+
 // ---------------------------------------------------------------------------- xGMI export record
-// What one rank publishes (through the c10d store) about its buffers; peers map them with IPC.
+// What one rank publishes (through the c10d store) about its block; peers map it with IPC.
 struct XgmiRecord {
-  hipIpcMemHandle_t in_h, out_h, flags_h, stage_h;
-  int64_t in_off, out_off;
+  hipIpcMemHandle_t blk_h;
+  int64_t blk_off;                                  // the block's offset inside the IPC allocation
+  XgmiBlockLayout layout;
   int64_t numel, oneshot_max;
   int32_t world, rank, channels, pid, device;
   int32_t grid_fc, grid_conv, grid_two, grid_one;   // residency-planned grids (must agree across ranks)
@@ -93,8 +116,9 @@ inline XgmiRecord decode_record(const std::vector<uint8_t>& bytes, int q, int wo
   memcpy(&r, bytes.data(), sizeof(r));
   if (r.rank != q || r.world != world || r.numel != numel || r.channels != channels || r.oneshot_max != oneshot_max)
     throw std::runtime_error("xgmi: peer record does not match this communicator");
-  if (r.in_off < 0 || r.out_off < 0 || r.in_off % 4 || r.out_off % 4)
-    throw std::runtime_error("xgmi: peer record has bad buffer offsets");
+  const XgmiBlockLayout L = xgmi_block_layout(numel, channels, oneshot_max);
+  if (r.blk_off < 0 || r.blk_off % 256 || memcmp(&r.layout, &L, sizeof(L)) != 0)
+    throw std::runtime_error("xgmi: peer record has a different buffer layout");
   if (r.grid_fc != grids.fc_fused || r.grid_conv != grids.conv_fused || r.grid_two != grids.twoshot ||
       r.grid_one != grids.oneshot)
     throw std::runtime_error("xgmi: ranks planned different kernel grids (mixed GPUs or co_ranks?)");

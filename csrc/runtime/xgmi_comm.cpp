@@ -67,40 +67,41 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   if (numel < 4 || (numel & 3)) throw std::runtime_error("xgmi: numel must be a positive multiple of 4");
   ok(hipSetDevice(device), "hipSetDevice");
   grids_ = xgmi_plan_grids(world, co_ranks, oneshot_max, budget);   // throws when not co-resident
-  // Every buffer a peer reads or writes is this communicator's own UNCACHED allocation
+  // Every buffer a peer reads or writes lives in this communicator's own UNCACHED allocation
   // (hipDeviceMallocUncached: no L2 allocation on any XCD of any GPU).  The per-XCD L2s are not
   // coherent: with cached memory a clean line left in one XCD's L2 by an earlier plain access (a
   // fill, the optimizer's read of the reduced bucket, a previous call's gather) is served to a later
   // system-scope load from that XCD even after the owner rewrote the bytes write-through - observed
-  // on one GPU as whole shards of stale sums.  Uncached, every load reaches memory.  The buffers are
+  // on one GPU as whole shards of stale sums.  Uncached, every load reaches memory.  The block is
   // never returned to the allocator either (never a block of torch's caching allocator): a later
   // allocation at the same address would carry an IPC handle a peer's import cache cannot tell
-  // from the old one.
-  auto alloc = [this, device](void** p, size_t bytes, const char* what) {
-    *p = pool_take(device, bytes);
-    if (!*p) ok(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached), what);
-    owned_.push_back({*p, bytes});
-  };
-  // every exported buffer ends in a 16-byte signature {magic, rank, pid, buffer id} that peers read
-  // back through their mappings after connect() (a mapping that does not show it is refused)
-  alloc(reinterpret_cast<void**>(&in_), sizeof(float) * numel + kSigBytes, "hipExtMallocWithFlags(in)");
-  alloc(reinterpret_cast<void**>(&out_), sizeof(float) * numel + kSigBytes, "hipExtMallocWithFlags(out)");
-  alloc(reinterpret_cast<void**>(&flags_), sizeof(int) * XGMI_FLAG_INTS * channels + kSigBytes,
-        "hipExtMallocWithFlags(flags)");
+  // from the old one.  ONE block per rank (in | out | flags | staging | signatures): a peer maps it
+  // with a single IPC import.
+  const XgmiBlockLayout L = xgmi_block_layout(numel, channels, oneshot_max);
+  block_bytes_ = L.bytes;
+  block_ = static_cast<char*>(pool_take(device, (size_t)L.bytes));
+  if (!block_) ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&block_), (size_t)L.bytes, hipDeviceMallocUncached),
+                  "hipExtMallocWithFlags(block)");
+  in_ = reinterpret_cast<float*>(block_ + L.in_off);
+  out_ = reinterpret_cast<float*>(block_ + L.out_off);
+  flags_ = reinterpret_cast<int*>(block_ + L.flags_off);
+  stage_ = reinterpret_cast<float*>(block_ + L.stage_off);
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
   ok(hipMalloc(&timeout_, sizeof(uint64_t)), "hipMalloc(timeout)");
-  ok(hipMemset(in_, 0, sizeof(float) * numel), "hipMemset");
-  ok(hipMemset(out_, 0, sizeof(float) * numel), "hipMemset");
-  ok(hipMemset(flags_, 0, sizeof(int) * XGMI_FLAG_INTS * channels), "hipMemset");
+  ok(hipMemset(block_, 0, (size_t)L.sig_off), "hipMemset");
   ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
   ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
-  alloc(reinterpret_cast<void**>(&stage_), sizeof(float) * (2 * oneshot_max + 4) * channels + kSigBytes,
-        "hipExtMallocWithFlags(stage)");
+  // signatures {magic, rank, pid, region id} that peers read back through their mapping after
+  // connect() (a mapping that does not show them is refused)
+  int32_t sig[4][4];
   for (int id = 0; id < 4; ++id) {
-    const int32_t sig[4] = {kSigMagic, rank, (int32_t)getpid(), id};
-    ok(hipMemcpy(sig_ptr(id), sig, kSigBytes, hipMemcpyHostToDevice), "hipMemcpy(signature)");
+    sig[id][0] = kSigMagic;
+    sig[id][1] = rank;
+    sig[id][2] = (int32_t)getpid();
+    sig[id][3] = id;
   }
+  ok(hipMemcpy(block_ + L.sig_off, sig, sizeof(sig), hipMemcpyHostToDevice), "hipMemcpy(signature)");
   ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   set_timeout_seconds(60.0);
   if (world == 1) {                       // nothing to map: the kernel runs against itself
@@ -114,10 +115,9 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
 
 XgmiComm::~XgmiComm() {
   close_peers();
-  // in_, out_, flags_, stage_ were exported: never freed (see the constructor); returned to the
-  // process-wide free list only when every peer is known to have unmapped them (mark_recyclable)
-  if (recyclable_)
-    for (auto& b : owned_) pool_give(device_, b.second, b.first);
+  // the block was exported: never freed (see the constructor); returned to the process-wide free
+  // list only when every peer is known to have unmapped it (mark_recyclable)
+  if (recyclable_) pool_give(device_, (size_t)block_bytes_, block_);
   if (ctr_) hipFree(ctr_);
   if (err_) hipFree(err_);
   if (timeout_) hipFree(timeout_);
@@ -131,17 +131,6 @@ void XgmiComm::close_peers() {
   if (world_ > 1) connected_ = false;
 }
 
-char* XgmiComm::sig_ptr(int id) const { return sig_at(id, in_, out_, flags_, stage_); }
-
-char* XgmiComm::sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const {
-  switch (id) {
-    case 0: return (char*)in + sizeof(float) * numel_;
-    case 1: return (char*)out + sizeof(float) * numel_;
-    case 2: return (char*)flags + sizeof(int) * XGMI_FLAG_INTS * channels_;
-    default: return (char*)stage + sizeof(float) * (2 * oneshot_max_ + 4) * channels_;
-  }
-}
-
 void XgmiComm::set_timeout_seconds(double s) {
   const uint64_t t = (uint64_t)(s * 1e8);
   ok(hipSetDevice(device_), "hipSetDevice");
@@ -151,13 +140,8 @@ void XgmiComm::set_timeout_seconds(double s) {
 std::vector<uint8_t> XgmiComm::record() const {
   XgmiRecord r;
   memset(&r, 0, sizeof(r));
-  export_ptr(in_, &r.in_h, &r.in_off);
-  export_ptr(out_, &r.out_h, &r.out_off);
-  int64_t foff = 0;
-  export_ptr(flags_, &r.flags_h, &foff);
-  if (foff != 0) throw std::runtime_error("xgmi: flag block is not an allocation base");
-  export_ptr(stage_, &r.stage_h, &foff);
-  if (foff != 0) throw std::runtime_error("xgmi: staging block is not an allocation base");
+  export_ptr(block_, &r.blk_h, &r.blk_off);
+  r.layout = xgmi_block_layout(numel_, channels_, oneshot_max_);
   r.numel = numel_;
   r.oneshot_max = oneshot_max_;
   r.world = world_;
@@ -180,26 +164,10 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
   peer_out_.assign(world_, nullptr);
   peer_flags_.assign(world_, nullptr);
   peer_stage_.assign(world_, nullptr);
-  // one mapping per distinct handle (the input and output buckets may share a caching-allocator segment)
-  std::vector<std::pair<hipIpcMemHandle_t, void*>> maps;
-  auto open = [&](const hipIpcMemHandle_t& h) -> char* {
-    for (auto& m : maps)
-      if (memcmp(&m.first, &h, sizeof(h)) == 0) return (char*)m.second;
-    void* p = nullptr;
-    ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    opened_.push_back(p);
-    maps.emplace_back(h, p);
-    return (char*)p;
-  };
   char host[64] = {0};
   gethostname(host, sizeof(host) - 1);
   for (int q = 0; q < world_; ++q) {
     const XgmiRecord r = decode_record(records[q], q, world_, numel_, channels_, oneshot_max_, grids_, host);
-    if (q != rank_ && r.device != device_) {
-      int can = 0;
-      ok(hipDeviceCanAccessPeer(&can, device_, r.device), "hipDeviceCanAccessPeer");
-      if (!can) throw std::runtime_error("xgmi: no peer access to device " + std::to_string(r.device));
-    }
     if (q == rank_) {
       peer_in_[q] = in_;
       peer_out_[q] = out_;
@@ -207,22 +175,28 @@ void XgmiComm::connect(const std::vector<std::vector<uint8_t>>& records) {
       peer_stage_[q] = stage_;
       continue;
     }
-    peer_in_[q] = reinterpret_cast<const float*>(open(r.in_h) + r.in_off);
-    peer_out_[q] = reinterpret_cast<float*>(open(r.out_h) + r.out_off);
-    peer_flags_[q] = reinterpret_cast<int*>(open(r.flags_h));
-    peer_stage_[q] = reinterpret_cast<float*>(open(r.stage_h));
-    // read every buffer's signature through the new mapping: it must be peer q's
-    static const char* names[] = {"input", "output", "flag", "staging"};
-    for (int id = 0; id < 4; ++id) {
-      int32_t sig[4] = {0, 0, 0, 0};
-      ok(hipMemcpy(sig, sig_at(id, peer_in_[q], peer_out_[q], peer_flags_[q], peer_stage_[q]), kSigBytes,
-                   hipMemcpyDeviceToHost),
-         "hipMemcpy(peer signature)");
-      if (sig[0] != kSigMagic || sig[1] != q || sig[2] != r.pid || sig[3] != id)
-        throw std::runtime_error("xgmi: the IPC mapping of rank " + std::to_string(q) + "'s " + names[id] +
-                                 " buffer does not show its signature (got rank " + std::to_string(sig[1]) +
-                                 ", pid " + std::to_string(sig[2]) + ", buffer " + std::to_string(sig[3]) + ")");
+    if (r.device != device_) {
+      int can = 0;
+      ok(hipDeviceCanAccessPeer(&can, device_, r.device), "hipDeviceCanAccessPeer");
+      if (!can) throw std::runtime_error("xgmi: no peer access to device " + std::to_string(r.device));
     }
+    void* p = nullptr;
+    ok(hipIpcOpenMemHandle(&p, r.blk_h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    opened_.push_back(p);
+    char* b = static_cast<char*>(p) + r.blk_off;
+    peer_in_[q] = reinterpret_cast<const float*>(b + r.layout.in_off);
+    peer_out_[q] = reinterpret_cast<float*>(b + r.layout.out_off);
+    peer_flags_[q] = reinterpret_cast<int*>(b + r.layout.flags_off);
+    peer_stage_[q] = reinterpret_cast<float*>(b + r.layout.stage_off);
+    // read the block's signatures through the new mapping: they must be peer q's
+    int32_t sig[4][4];
+    ok(hipMemcpy(sig, b + r.layout.sig_off, sizeof(sig), hipMemcpyDeviceToHost), "hipMemcpy(peer signature)");
+    for (int id = 0; id < 4; ++id)
+      if (sig[id][0] != kSigMagic || sig[id][1] != q || sig[id][2] != r.pid || sig[id][3] != id)
+        throw std::runtime_error("xgmi: the IPC mapping of rank " + std::to_string(q) +
+                                 "'s block does not show its signature (got rank " + std::to_string(sig[id][1]) +
+                                 ", pid " + std::to_string(sig[id][2]) + ", region " + std::to_string(sig[id][3]) +
+                                 ")");
   }
   connected_ = true;
 }

@@ -90,11 +90,12 @@ class XgmiComm {
 
  private:
   int world_, rank_, device_, channels_;
+  char* block_ = nullptr;    // the one IPC-exported allocation (host_logic.h xgmi_block_layout)
+  int64_t block_bytes_ = 0;
   float *in_ = nullptr, *out_ = nullptr;
   int64_t numel_;
-  int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS], IPC exported
-  float* stage_ = nullptr;   // [channels][2][oneshot_max_], IPC exported
-  std::vector<std::pair<void*, size_t>> owned_;   // the exported buffers (back to the free list)
+  int* flags_ = nullptr;     // [channels][XGMI_FLAG_INTS]
+  float* stage_ = nullptr;   // [channels][2][oneshot_max_]
   bool recyclable_ = false;
   bool fences_ = false;
   int64_t oneshot_max_;
@@ -109,10 +110,7 @@ class XgmiComm {
   std::vector<float*> peer_stage_;
   std::vector<void*> opened_;   // IPC mappings to close
   XgmiArgs args(int channel, int64_t offset, int64_t count) const;
-  static constexpr int kSigBytes = 16;
   static constexpr int32_t kSigMagic = 0x58474d49;   // "XGMI"
-  char* sig_ptr(int id) const;
-  char* sig_at(int id, const void* in, const void* out, const void* flags, const void* stage) const;
 };
 
 }  // namespace mnist

@@ -75,7 +75,7 @@ static XgmiGrids grids() {
 static XgmiRecord make_record(int q) {
   XgmiRecord r;
   memset(&r, 0, sizeof(r));
-  r.in_off = 256; r.out_off = 1024; r.numel = 1200000; r.oneshot_max = 32768;
+  r.blk_off = 0; r.layout = xgmi_block_layout(1200000, 2, 32768); r.numel = 1200000; r.oneshot_max = 32768;
   r.world = 8; r.rank = q; r.channels = 2; r.pid = 1234; r.device = q;
   const XgmiGrids g = grids();
   r.grid_fc = g.fc_fused; r.grid_conv = g.conv_fused; r.grid_two = g.twoshot; r.grid_one = g.oneshot;
@@ -96,7 +96,8 @@ static void test_records() {
   for (int q = 0; q < 8; ++q) {
     const std::vector<uint8_t> enc = encode_record(make_record(q));
     const XgmiRecord back = decode_record(enc, q, 8, 1200000, 2, 32768, grids(), "node-a");
-    CHECK(back.rank == q && back.in_off == 256 && back.out_off == 1024 && back.device == q);
+    CHECK(back.rank == q && back.layout.out_off >= back.layout.in_off + 4800000 && back.device == q);
+    CHECK(back.layout.bytes % 4096 == 0 && back.layout.sig_off + 64 <= back.layout.bytes);
     CHECK(rejects(enc, (q + 1) % 8));                                   // wrong rank slot
     std::vector<uint8_t> shorter(enc.begin(), enc.end() - 1), longer = enc;
     longer.push_back(0);
@@ -106,8 +107,10 @@ static void test_records() {
     XgmiRecord r = make_record(q);
     r.numel = 4; CHECK(rejects(encode_record(r), q));
     r = make_record(q); r.grid_conv = 87; CHECK(rejects(encode_record(r), q));
-    r = make_record(q); r.in_off = -16; CHECK(rejects(encode_record(r), q));
-    r = make_record(q); r.out_off = 6; CHECK(rejects(encode_record(r), q));
+    r = make_record(q); r.blk_off = -256; CHECK(rejects(encode_record(r), q));
+    r = make_record(q); r.blk_off = 6; CHECK(rejects(encode_record(r), q));
+    r = make_record(q); r.layout.out_off += 4096; CHECK(rejects(encode_record(r), q));
+    r = make_record(q); r.layout.bytes -= 4096; CHECK(rejects(encode_record(r), q));
     r = make_record(q); snprintf(r.host, sizeof(r.host), "node-b"); CHECK(rejects(encode_record(r), q));
     r = make_record(q); memset(r.host, 'x', sizeof(r.host)); CHECK(rejects(encode_record(r), q));   // no NUL
   }
@@ -117,7 +120,7 @@ static void test_records() {
     for (auto& b : junk) b = (uint8_t)rng();
     if (junk.size() == sizeof(XgmiRecord) && it % 2 == 0) {            // plausible header, garbage rest
       XgmiRecord r = make_record(3);
-      memcpy(junk.data(), &r, offsetof(XgmiRecord, in_off));
+      memcpy(junk.data(), &r, offsetof(XgmiRecord, blk_off));
     }
     (void)rejects(junk, 3);
   }

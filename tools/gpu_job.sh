@@ -13,6 +13,7 @@
 #   xgmi W [ARGS]              tools/xgmi_check.py --world W --same-device ARGS
 #   ddpeq W B                  tools/ddp_equivalence.py --world W --same-device --batch B
 #   ab TAG "ENV=a" "ENV=b" ... -- [BENCH ARGS]   tools/ab_multi.sh
+#   py TAG SCRIPT [ARGS]       python -u SCRIPT ARGS -> gpurun_out/py_TAG.log
 #
 # usage (on the box): bash tools/gpu_job.sh "tests tests/test_gpu_xgmi.py" "bench exact --gpus 1 --steps 20 --warmup 5"
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -73,6 +74,10 @@ run_step() {
       tail -3 gpurun_out/ddpeq_w$1.log; fatal $rc "ddpeq $1";;
     ab)
       bash tools/ab_multi.sh "$@"; fatal $? "ab $1";;
+    py)
+      local tag=$1; shift
+      timeout -k 10 400 python -u "$@" > gpurun_out/py_$tag.log 2>&1; local rc=$?
+      tail -40 gpurun_out/py_$tag.log; fatal $rc "py $tag";;
     *)
       echo "unknown step kind '$kind'"; exit 2;;
   esac
