@@ -122,6 +122,16 @@ class FusedTrainer:
             self.test_idx = torch.arange(self.n_test, dtype=torch.int32, device=dev)
             self.test_loss_rows = torch.zeros(self.n_test, dtype=torch.float32, device=dev)
             self.test_correct = torch.zeros(self.n_test, dtype=torch.int32, device=dev)
+            # pinned landing buffers of the per-epoch evaluation read-back (allocated once: a pinned
+            # allocation is a driver call inside every epoch of the reference's timer otherwise)
+            self._eval_rows_h = torch.empty(self.n_test, dtype=torch.float32, pin_memory=True)
+            self._eval_hits_h = torch.empty(self.n_test, dtype=torch.int32, pin_memory=True)
+        # two pinned staging buffers for the per-epoch index upload (alternating; the event of a
+        # buffer's last H2D is waited on before the host rewrites it)
+        self._idx_h = [torch.empty(self.steps_per_epoch * self.B, dtype=torch.int32, pin_memory=True)
+                       for _ in range(2)]
+        self._idx_ev = [None, None]
+        self._idx_k = 0
         bufs = mstate.buffers()
         p = native.ptr
         bufs.update(loss_log=p(self.loss_log), train_u8=p(self.train_u8), train_labels=p(self.train_labels),
@@ -442,9 +452,17 @@ class FusedTrainer:
         n = idx.numel()
         if n > self.train_idx.numel():
             raise ValueError("epoch index vector larger than the device buffer")
-        host = idx.to(torch.int32).pin_memory() if torch.cuda.is_available() else idx.to(torch.int32)
+        k = self._idx_k
+        self._idx_k ^= 1
+        if self._idx_ev[k] is not None:
+            self._idx_ev[k].synchronize()           # that buffer's previous upload has been consumed
+        host = self._idx_h[k][:n]
+        host.copy_(idx)                              # (int64 -> int32)
         with torch.cuda.stream(self.compute):
             self.train_idx[:n].copy_(host, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.compute)
+        self._idx_ev[k] = ev
         if gather:
             self.engine.gather_rows(0, n)
 
@@ -580,8 +598,7 @@ class FusedTrainer:
             self.engine.eval(self.n_test, self.eval_batch)
         # per-row results to the host (40 + 40 KB) and summed there in float64: no torch reduction
         # kernel (whose first use loads a code object inside the timed run) and a fixed order
-        rows = torch.empty(self.n_test, dtype=torch.float32, pin_memory=True)
-        hits = torch.empty(self.n_test, dtype=torch.int32, pin_memory=True)
+        rows, hits = self._eval_rows_h, self._eval_hits_h
         with torch.cuda.stream(self.compute):
             rows.copy_(self.test_loss_rows, non_blocking=True)
             hits.copy_(self.test_correct, non_blocking=True)

@@ -153,3 +153,20 @@ def test_bench_startup_fault_reports_json(cuda_device, tmp_path):
     assert {"pg_init", "data_model", "trainer.xgmi_comm", "trainer.validate.xgmi"} <= set(r0["setup_phases_s"])
     assert r0["transport_report"]["xgmi"]["ok"] is False and "timed out" in r0["transport_report"]["xgmi"]["validation"]
     assert j["launcher"]["child_rc"] != 0
+
+
+@pytest.mark.timeout(200)
+def test_bench_nccl_process_group_stays_lazy_w4(cuda_device, tmp_path):
+    """Production bootstrap on one GPU: the default ``nccl`` process group (lazy - no device_id) with
+    the xGMI transport.  RCCL refuses two ranks on one GPU, so this passes only if nothing in the
+    fused path issues a torch collective (ProcessGroupNCCL would build a communicator): shape check,
+    broadcast (over the xGMI mappings), verdicts, timing maxima and fingerprints all go over the
+    TCPStore."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "20", "--warmup", "5",
+           "--no-full-run", "--allreduce", "xgmi"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=tmp_path, env=_env())
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    j = json.loads(lines[-1])
+    assert j["n_gpus"] == 4 and j["params_in_sync"] is True and j["config"]["allreduce"] == "xgmi"
+    assert "pg_init" in j["setup_phases_s"] and j["config"]["rccl_comms"] == 0
