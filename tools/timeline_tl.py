@@ -121,7 +121,10 @@ def analyse(recs, steps):
         table.append({"kernel": NAMES[kid] if kid < len(NAMES) else str(kid), "launches": n,
                       "start_us": round(st, 2), "end_us": round(en, 2), "dur_us": round(en - st, 2),
                       "waves": round(sum(x[2] for x in v) / n, 1)})
-    span = {"period_us": round(period, 2), "steps": len(starts)}
+    span = {"period_us": round(period, 2), "steps": len(starts),
+            "step_periods_us": [round((b - a) / 100.0, 1) for a, b in zip(starts, starts[1:])]}
+    ends = [c[1] for launches in cl.values() for c in launches]
+    span["window_us"] = round((max(ends) - starts[0]) / 100.0, 1)       # first trunk start -> last end
     return table, span
 
 
@@ -169,6 +172,8 @@ def main() -> int:
              f"{args.graph_steps}), schedule {['serial', 'overlap', 'rccl', 'xgmi'][sched]}", "",
              f"period (trunk_fwd start to start, steps 2..{span['steps']}): {span['period_us']} us/step "
              f"(timeline build); product build, same command: {round(prod, 2) if prod else 'n/a'} us/step", "",
+             f"device window (first trunk_fwd start to last kernel end): {span['window_us']} us for "
+             f"{span['steps']} steps; step periods: {span['step_periods_us']}", "",
              "| kernel | stream | launches | start us | end us | duration us | waves |", "|---|---|---|---|---|---|---|"]
     for r in table:
         lines.append(f"| {r['kernel']} | {'comm' if r['kernel'] in COMM else 'compute'} | {r['launches']} | "
