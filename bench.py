@@ -195,6 +195,8 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--force-comm", action="store_true",
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="bf16: the bf16-MFMA step (default); fp32: the fp32 step (f32_net.hip, RCCL at N > 1)")
     ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
                     help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernels, or "
                          "auto (validate and time both production schedules at startup, keep the faster)")
@@ -353,7 +355,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     t_tr = time.perf_counter()
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
-                      two_buckets=not args.single_bucket, allreduce=args.allreduce)
+                      two_buckets=not args.single_bucket, allreduce=args.allreduce,
+                      fp32=args.dtype == "fp32")
     diag.tr = tr
     tr.lead_steps = args.lead_steps
     phases.add("trainer", time.perf_counter() - t_tr)
@@ -491,6 +494,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                     extra += ["--dist-backend", args.dist_backend]
                 if args.allreduce != "auto":
                     extra += ["--allreduce", args.allreduce]
+                if args.dtype != "bf16":
+                    extra += ["--dtype", args.dtype]
                 script = run_reference_script(world, B, args.epochs, extra=extra)
             except Exception as e:  # noqa: BLE001 - reported in the JSON
                 script = {"error": f"{type(e).__name__}: {e}"}
@@ -516,7 +521,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / base_img_s, 2) if base_img_s else None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic (60k/10k 28x28 uint8, deterministic); random-init weights",
             "config": {"model": "mnist_cnn (reference Net: conv32-conv64-maxpool-fc128-fc10, 1.2M params)",
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,

@@ -331,12 +331,14 @@ PYBIND11_MODULE(_C, m) {
   // ---------------- engine ----------------
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict bufs, int max_batch, int max_test_batch, uintptr_t compute, uintptr_t comm,
-                       int world, float rho, float eps, float wd) {
+                       int world, float rho, float eps, float wd, bool fp32) {
              return new Engine(buffers_from_dict(bufs), max_batch, max_test_batch, S(compute), S(comm), world, rho,
-                               eps, wd);
+                               eps, wd, fp32);
            }),
            py::arg("buffers"), py::arg("max_batch"), py::arg("max_test_batch"), py::arg("compute_stream"),
-           py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"))
+           py::arg("comm_stream"), py::arg("world_size"), py::arg("rho"), py::arg("eps"), py::arg("weight_decay"),
+           py::arg("fp32") = false)
+      .def_property_readonly("fp32", &Engine::fp32)
       .def("attach_comm", &Engine::attach_comm)
       .def("attach_xgmi", &Engine::attach_xgmi)
       .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)

@@ -179,6 +179,46 @@ void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStre
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 
+// ---------------- fp32 step (--dtype fp32; f32_net.hip): f32-input MFMA GEMMs + VALU kernels
+struct F32Step {
+  // batch source: pre-gathered rows (idx = null, row = step * idx_step_stride + b) or dataset rows
+  // through the index vector; eval: the test split, idx = test_idx + first row, stride 0
+  const uint8_t* data_u8;
+  const int32_t* idx;
+  int64_t idx_step_stride;
+  const int32_t* labels;
+  const StepState* state;     // null in eval (step 0, no dropout)
+  const float* param;         // flat fp32 parameters
+  float* grad;                // flat fp32 gradient (every parameter written each step)
+  float* loss_log;            // [steps] mean loss per step (train)
+  float inv_batch;            // 1 / (B * world): DDP averaging folded into the loss gradient
+  // workspace (fp32 unless noted)
+  float* w2fwd;               // [9][32][64] conv2 weight, forward B operand
+  float* w2bwd;               // [9][64][32] conv2 weight, input-gradient B operand
+  float* a1;                  // [B][26][26][32] ReLU(conv1); then the conv1 pre-activation gradient
+  float* y2;                  // [B][24][24][64] conv2 pre-activation; then its gradient
+  float* p;                   // [B][9216] pooled + dropout, torch flatten order
+  uint8_t* pm;                // [B][9216] argmax (bits 0-1), dropout keep (2), pooled > 0 (3)
+  float* z1part;              // [f32_fc1_splits(B)][B][128]
+  float* h;                   // [B][128] fc1 activations after ReLU + dropout
+  float* dz1;                 // [B][128] gradient wrt the fc1 pre-activation
+  float* dl;                  // [B][16] gradient wrt the logits
+  float* loss_rows;           // [B] per-row NLL (train and eval)
+  int32_t* correct;           // eval: [B] argmax == label
+  float* c2part;              // [f32_conv2w_splits(B)][64][289] conv2 weight + bias partials
+  float* c1part;              // [f32_conv1w_splits(B)][32][10] conv1 weight + bias partials
+};
+constexpr int F32_MAX_SPLITS = 128;
+int f32_fc1_splits(int B);
+int f32_conv2w_splits(int B);
+int f32_conv1w_splits(int B);
+// prep + conv1 + conv2 + pool (+dropout) + fc1 + head (train: loss + logit / dz1 gradients; eval:
+// per-row NLL + hits)
+void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s);
+// fc2 / fc1-bias grads + loss log, fc1 weight grad, fc1 input grad (+ unpool), conv2 weight grad,
+// conv2 input grad (+ conv1 ReLU), conv1 weight grad, split-K reduce: every gradient of the step
+void launch_f32_backward(const F32Step& a, int B, hipStream_t s);
+
 // direct xGMI all-reduce (reduce-scatter + all-gather over IPC-mapped peer buckets; xgmi_allreduce.hip)
 constexpr int XGMI_MAX_RANKS = 8;          // one node
 constexpr int XGMI_MAX_WG = 512;           // flag slots per (stage, rank)

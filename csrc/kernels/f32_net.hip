@@ -1,0 +1,527 @@
+// fp32 training / eval step (--dtype fp32): the reference's own precision (mnist_ddp.py trains the
+// Net in fp32) on gfx950's f32-input matrix cores instead of stock torch ops.
+//
+// Replaces, for the fp32 mode: reference mnist_ddp.py:49-61 (forward), :71-72 (nll_loss +
+// backward) and :89-105 (test forward).  The bf16 engine (trunk_fwd.hip, fc_head.hip, conv_bwd.hip)
+// stays the performance path; this one keeps every operand in fp32.
+//
+// Design:
+//   * every GEMM-shaped op - conv2 forward (implicit im2col), fc1, fc1 weight / input gradients,
+//     conv2 weight (implicit im2col, split-K) / input gradients (implicit transposed conv), conv1
+//     weight gradient - is ONE LDS-tiled GEMM template on v_mfma_f32_16x16x4_f32 (exact f32: a
+//     k-ordered fma chain, no xf32 on CDNA4) whose operand loaders and epilogue are small policy
+//     structs: no im2col buffer, the gathers happen in the tile loads;
+//   * elementwise / per-row work (conv1 + ReLU, ReLU + max-pool + dropout, the fc head with
+//     log_softmax + NLL + their backward, bias sums) are VALU kernels;
+//   * dropout draws the same Philox-4x32-10 bytes as the bf16 engine (device_utils.h), so both
+//     engines drop the same units of the same step; every reduction runs in a fixed order
+//     (split-K partial slabs summed by one kernel), so the step is bitwise repeatable.
+// Layouts (fp32): a1 [B][26][26][32] (NHWC, ReLU applied; its storage is reused for the conv1
+// pre-activation gradient), y2 / dy2 [B][24][24][64] (conv2 pre-activation / its gradient, shared
+// storage), p [B][9216] torch flatten order, pm u8 [B][9216] (bits 0-1 argmax, 2 keep, 3 pooled > 0).
+#include "../include/device_utils.h"
+#include "../include/kernels.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace mnist {
+
+namespace {
+constexpr int BK = 16;                 // GEMM k-tile (4 MFMA k-steps of 4)
+constexpr int NPIX1 = H1 * H1;         // 676 conv1 output pixels
+constexpr int NPIX2 = H2 * H2;         // 576 conv2 output pixels
+constexpr int K2 = 9 * C1;             // 288 conv2 reduction length (tap, ci)
+constexpr int WG_N = C2 * K2 + C2;     // conv2 weight + bias gradient slab (18496)
+
+__device__ __forceinline__ const StepState* state_of(const F32Step& a) {
+  return a.state ? a.state : &g_zero_state;
+}
+
+// row b of the current step: pre-gathered rows (idx == null) or the dataset through the index vector
+__device__ __forceinline__ const uint8_t* image_row(const F32Step& a, int step, int b) {
+  const int64_t row = (int64_t)step * a.idx_step_stride + b;
+  const int64_t img = a.idx ? (int64_t)a.idx[row] : row;
+  return a.data_u8 + img * (IMG * IMG);
+}
+
+// ---------------------------------------------------------------------------------------------
+// GEMM template: C[M][N] = sum_k A(m, k) B(k, n) over k in [z*kc, min(K, (z+1)*kc)) (z = blockIdx.z).
+// Workgroup tile BM x BN (4 waves, each 32 x 32 = 2 x 2 tiles of 16 x 16), k-tile 16 staged in LDS
+// as [k][m] / [k][n] rows, so every MFMA operand read is 16 consecutive floats per 16-lane group.
+// The policy P provides M, N, K, kc, a(m, k), b(k, n), put(m, n, v, z), prepare() and whether A / B
+// are contiguous along k (A_KF / B_KF) - the tile-load thread mapping follows the contiguous axis.
+template <int BM, int BN, class P>
+__global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
+  static_assert((BM / 32) * (BN / 32) == 4, "4 waves of 32 x 32");
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256, WN = BN / 32;
+  __shared__ float As[BK][BM + 4];
+  __shared__ float Bs[BK][BN + 4];
+  p.prepare();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int k_lo = blockIdx.z * p.kc;
+  const int k_hi = min(p.K, k_lo + p.kc);
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = k_lo; k0 < k_hi; k0 += BK) {
+    float ra[EA], rb[EB];
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int x = tid + 256 * e;
+      const int m = P::A_KF ? x / BK : x % BM, k = P::A_KF ? x % BK : x / BM;
+      const int gm = m0 + m, gk = k0 + k;
+      ra[e] = (gm < p.M && gk < k_hi) ? p.a(gm, gk) : 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int x = tid + 256 * e;
+      const int n = P::B_KF ? x / BK : x % BN, k = P::B_KF ? x % BK : x / BN;
+      const int gn = n0 + n, gk = k0 + k;
+      rb[e] = (gn < p.N && gk < k_hi) ? p.b(gk, gn) : 0.0f;
+    }
+    __syncthreads();                              // the previous k-tile's reads are done
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int x = tid + 256 * e;
+      As[P::A_KF ? x % BK : x / BM][P::A_KF ? x / BK : x % BM] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int x = tid + 256 * e;
+      Bs[P::B_KF ? x % BK : x / BN][P::B_KF ? x / BK : x % BN] = rb[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = As[kk + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kk + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // C/D map of the 16 x 16 MFMA: column = lane & 15, row = 4 * (lane >> 4) + register
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m < p.M && n < p.N) p.put(m, n, acc[i][j][r], blockIdx.z);
+      }
+}
+
+template <int BM, int BN, class P>
+void gemm(const P& p, int splits, hipStream_t s) {
+  const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
+  hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, P>), grid, dim3(256), 0, s, p);
+}
+
+// ---- policies
+// conv2 forward: y2[(b, oy, ox)][co] = b2[co] + sum_(tap, ci) a1[b][oy+ky][ox+kx][ci] w2[co][ci][tap]
+struct PConv2Fwd {
+  static constexpr bool A_KF = true, B_KF = false;
+  int M, N, K, kc;
+  const float* a1;
+  const float* w2fwd;   // [tap][ci][co]
+  const float* b2;
+  float* y2;
+  __device__ void prepare() {}
+  __device__ float a(int m, int k) const {
+    const int b = m / NPIX2, pix = m - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
+    const int tap = k >> 5, ci = k & 31, ky = tap / 3, kx = tap - 3 * ky;
+    return a1[(((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci];
+  }
+  __device__ float b(int k, int n) const { return w2fwd[k * C2 + n]; }
+  __device__ void put(int m, int n, float v, int) const { y2[(int64_t)m * C2 + n] = v + b2[n]; }
+};
+
+// fc1 forward, split-K partial sums: z1part[z][b][o] = sum_(i in split z) p[b][i] w1[o][i]
+struct PFc1 {
+  static constexpr bool A_KF = true, B_KF = true;
+  int M, N, K, kc;
+  const float* p;
+  const float* w1;
+  float* z1part;
+  __device__ void prepare() {}
+  __device__ float a(int m, int k) const { return p[(int64_t)m * NFLAT + k]; }
+  __device__ float b(int k, int n) const { return w1[(int64_t)n * NFLAT + k]; }
+  __device__ void put(int m, int n, float v, int z) const { z1part[((int64_t)z * M + m) * NH + n] = v; }
+};
+
+// fc1 weight gradient: g[o][i] = sum_b dz1[b][o] p[b][i]
+struct PFc1W {
+  static constexpr bool A_KF = false, B_KF = false;
+  int M, N, K, kc;
+  const float* dz1;
+  const float* p;
+  float* g;
+  __device__ void prepare() {}
+  __device__ float a(int m, int k) const { return dz1[(int64_t)k * NH + m]; }
+  __device__ float b(int k, int n) const { return p[(int64_t)k * NFLAT + n]; }
+  __device__ void put(int m, int n, float v, int) const { g[(int64_t)m * NFLAT + n] = v; }
+};
+
+// fc1 input gradient dp[b][j] = sum_o dz1[b][o] w1[o][j], through dropout-1 and the max-pool +
+// ReLU backward in the epilogue: the 2 x 2 window's four conv2-output gradients (one non-zero)
+struct PFc1X {
+  static constexpr bool A_KF = true, B_KF = false;
+  int M, N, K, kc;
+  const float* dz1;
+  const float* w1;
+  const uint8_t* pm;
+  float* dy2;
+  const StepState* st;
+  float dscale;
+  __device__ void prepare() {
+    const StepState* s = st ? st : &g_zero_state;
+    dscale = (s->flags & STEP_FLAG_NO_DROPOUT) ? 1.0f : (1.0f / KEEP1);
+  }
+  __device__ float a(int m, int k) const { return dz1[(int64_t)m * NH + k]; }
+  __device__ float b(int k, int n) const { return w1[(int64_t)k * NFLAT + n]; }
+  __device__ void put(int m, int n, float v, int) const {
+    const int c = n / NPOOL, pos = n - c * NPOOL, py = pos / HP, px = pos - py * HP;
+    const uint32_t fl = pm[(int64_t)m * NFLAT + n];
+    const float g = ((fl & 12u) == 12u) ? v * dscale : 0.0f;    // kept by dropout, ReLU alive
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int y = 2 * py + (q >> 1), x = 2 * px + (q & 1);
+      dy2[(((int64_t)m * H2 + y) * H2 + x) * C2 + c] = ((int)(fl & 3u) == q) ? g : 0.0f;
+    }
+  }
+};
+
+// conv2 weight + bias gradient, split-K over the B*576 output pixels:
+// part[z][co][n] = sum_m dy2[m][co] im2col(a1)[m][n] (n < 288), sum_m dy2[m][co] (n = 288)
+struct PConv2W {
+  static constexpr bool A_KF = false, B_KF = false;
+  int M, N, K, kc;
+  const float* dy2;
+  const float* a1;
+  float* part;
+  __device__ void prepare() {}
+  __device__ float a(int m, int k) const { return dy2[(int64_t)k * C2 + m]; }
+  __device__ float b(int k, int n) const {
+    if (n == K2) return 1.0f;
+    const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
+    const int tap = n >> 5, ci = n & 31, ky = tap / 3, kx = tap - 3 * ky;
+    return a1[(((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci];
+  }
+  __device__ void put(int m, int n, float v, int z) const { part[((int64_t)z * C2 + m) * (K2 + 1) + n] = v; }
+};
+
+// conv2 input gradient (transposed conv) times the conv1 ReLU mask, in place over a1:
+// da1[(b, iy, ix)][ci] = [a1 > 0] sum_(tap, co) dy2[b][iy-ky][ix-kx][co] w2[co][ci][tap]
+struct PConv2X {
+  static constexpr bool A_KF = true, B_KF = false;
+  int M, N, K, kc;
+  const float* dy2;
+  const float* w2bwd;   // [tap][co][ci]
+  float* a1;
+  __device__ void prepare() {}
+  __device__ float a(int m, int k) const {
+    const int b = m / NPIX1, pix = m - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
+    const int tap = k >> 6, co = k & 63, ky = tap / 3, kx = tap - 3 * ky;
+    const int oy = iy - ky, ox = ix - kx;
+    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2) ? dy2[(((int64_t)b * H2 + oy) * H2 + ox) * C2 + co] : 0.0f;
+  }
+  __device__ float b(int k, int n) const { return w2bwd[k * C1 + n]; }
+  __device__ void put(int m, int n, float v, int) const {
+    float* q = a1 + (int64_t)m * C1 + n;
+    *q = (*q > 0.0f) ? v : 0.0f;
+  }
+};
+
+// conv1 weight + bias gradient, split-K over the B*676 pixels:
+// part[z][c][t] = sum_m da1[m][c] x_patch[m][t] (t < 9), sum_m da1[m][c] (t = 9)
+struct PConv1W {
+  static constexpr bool A_KF = false, B_KF = true;
+  int M, N, K, kc;
+  const float* da1;
+  F32Step s;
+  int step;
+  float* part;
+  __device__ void prepare() { step = state_of(s)->step; }
+  __device__ float a(int m, int k) const { return da1[(int64_t)k * C1 + m]; }
+  __device__ float b(int k, int n) const {
+    if (n == 9) return 1.0f;
+    const int b = k / NPIX1, pix = k - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
+    const int ky = n / 3, kx = n - 3 * ky;
+    return normalize_u8_alu(image_row(s, step, b)[(iy + ky) * IMG + ix + kx]);
+  }
+  __device__ void put(int m, int n, float v, int z) const { part[((int64_t)z * C1 + m) * 10 + n] = v; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// conv2 weight in the two GEMM B layouts: w2fwd[tap][ci][co], w2bwd[tap][co][ci]
+__global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= C2 * K2) return;
+  const int co = t / K2, r = t - co * K2, ci = r / 9, tap = r - 9 * ci;   // torch [co][ci][ky][kx]
+  const float w = a.param[OFF_CONV2_W + t];
+  a.w2fwd[(tap * C1 + ci) * C2 + co] = w;
+  a.w2bwd[(tap * C2 + co) * C1 + ci] = w;
+}
+
+// conv1 + bias + ReLU: one thread = one output pixel, 32 channels (the bf16 engine's fma order)
+__global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * NPIX1) return;
+  const int b = (int)(t / NPIX1), pix = (int)(t - (int64_t)b * NPIX1), y = pix / H1, x = pix - y * H1;
+  const uint8_t* src = image_row(a, state_of(a)->step, b) + y * IMG + x;
+  float xv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) xv[k] = normalize_u8_alu(src[(k / 3) * IMG + k % 3]);
+  const float* w = a.param + OFF_CONV1_W;
+  const float* bias = a.param + OFF_CONV1_B;
+  float4* dst = reinterpret_cast<float4*>(a.a1 + t * C1);
+#pragma unroll
+  for (int c4 = 0; c4 < C1 / 4; ++c4) {
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaxf(conv1_preact(xv, 3, w + (4 * c4 + j) * 9, bias[4 * c4 + j]), 0.0f);
+    dst[c4] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// ReLU + 2x2 max-pool (first max wins, as torch) + dropout(0.25): one thread = 16 consecutive
+// flat elements of one channel = one Philox block (the trunk's rule: counter rng_base + 2 step)
+template <bool TRAIN>
+__global__ __launch_bounds__(256) void f32_pool_kernel(F32Step a, int B) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * C2 * (NPOOL / 16)) return;
+  const int b = (int)(t / (C2 * (NPOOL / 16))), u = (int)(t - (int64_t)b * (C2 * (NPOOL / 16)));
+  const int c = u / (NPOOL / 16), j = u - c * (NPOOL / 16);
+  const int flat0 = c * NPOOL + 16 * j;
+  const StepState* st = state_of(a);
+  const bool drop = TRAIN && !(st->flags & STEP_FLAG_NO_DROPOUT);
+  u32x4 rw = {0u, 0u, 0u, 0u};
+  if (drop) rw = dropout_block(st->seed, st->rng_base + 2ull * (uint64_t)st->step, ((uint64_t)b * NFLAT + flat0) >> 4);
+  const float* y2 = a.y2 + (int64_t)b * NPIX2 * C2 + c;
+  float out[16];
+  uint32_t fl[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int pos = 16 * j + q, py = pos / HP, px = pos - py * HP;
+    float best = 0.0f;
+    int arg = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(y2[((2 * py + (r >> 1)) * H2 + 2 * px + (r & 1)) * C2], 0.0f);
+      if (r == 0 || v > best) { best = v; arg = r; }
+    }
+    bool keep = true;
+    if (TRAIN) keep = dropout_byte(rw, q) < KEEP1_THR8;
+    out[q] = keep ? (drop ? best * (1.0f / KEEP1) : best) : 0.0f;
+    fl[q >> 2] |= (uint32_t)(arg | (keep ? 4 : 0) | (best > 0.0f ? 8 : 0)) << (8 * (q & 3));
+  }
+  float4* dst = reinterpret_cast<float4*>(a.p + (int64_t)b * NFLAT + flat0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+  if (TRAIN) *reinterpret_cast<uint4*>(a.pm + (int64_t)b * NFLAT + flat0) = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+}
+
+__device__ __forceinline__ void log_softmax10_f32(const float* x, float* lp) {
+  float mx = x[0];
+#pragma unroll
+  for (int c = 1; c < NCLS; ++c) mx = fmaxf(mx, x[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) se += expf(x[c] - mx);
+  const float lse = logf(se);
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lp[c] = (x[c] - mx) - lse;
+}
+
+// fc1 bias + ReLU + dropout(0.5) + fc2 + log_softmax + NLL (+ backward to dz1): one wave = one row.
+// TRAIN writes h, dz1, dl = d loss / d logits (scaled by inv_batch = 1/(B*world)) and the row's
+// loss; eval writes the row's summed-NLL term and whether argmax (first max) == label.
+template <bool TRAIN>
+__global__ __launch_bounds__(256) void f32_head_kernel(F32Step a, int B, int S) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const StepState* st = state_of(a);
+  const int step = st->step;
+  const bool no_drop = !TRAIN || (st->flags & STEP_FLAG_NO_DROPOUT);
+  const uint64_t off = st->rng_base + 2ull * (uint64_t)step + 1ull;
+  const int64_t row = (int64_t)step * a.idx_step_stride + b;
+  const int y = a.labels[a.idx ? (int64_t)a.idx[row] : row];
+  const float* P = a.param;
+  float z[2], h[2];
+  bool keep[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = lane + 64 * j;
+    float s = 0.f;                                    // split-K partials in fixed order
+    for (int c = 0; c < S; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
+    z[j] = P[OFF_FC1_B + o] + s;
+    float hv = fmaxf(z[j], 0.0f);
+    keep[j] = true;
+    if (!no_drop) {
+      const u32x4 w = dropout_block(st->seed, off, ((uint64_t)b * NH + o) >> 4);
+      keep[j] = dropout_byte(w, o & 15) < KEEP2_THR8;
+      hv = keep[j] ? hv * (1.0f / KEEP2) : 0.0f;
+    }
+    h[j] = hv;
+  }
+  float logit[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c)
+    logit[c] = wave_sum(h[0] * P[OFF_FC2_W + c * NH + lane] + h[1] * P[OFF_FC2_W + c * NH + lane + 64]) +
+               P[OFF_FC2_B + c];
+  float lp[NCLS];
+  log_softmax10_f32(logit, lp);
+  if (!TRAIN) {
+    if (lane == 0) {
+      int arg = 0;
+#pragma unroll
+      for (int c = 1; c < NCLS; ++c) arg = lp[c] > lp[arg] ? c : arg;
+      a.loss_rows[b] = -lp[y];
+      a.correct[b] = arg == y ? 1 : 0;
+    }
+    return;
+  }
+  float dl[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {                    // nll(mean) + log_softmax backward
+    const float go = (c == y) ? -a.inv_batch : 0.0f;
+    dl[c] = go - expf(lp[c]) * (-a.inv_batch);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = lane + 64 * j;
+    float dh = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) dh = __builtin_fmaf(dl[c], P[OFF_FC2_W + c * NH + o], dh);
+    a.dz1[(int64_t)b * NH + o] = (keep[j] && z[j] > 0.0f) ? (no_drop ? dh : dh * (1.0f / KEEP2)) : 0.0f;
+    a.h[(int64_t)b * NH + o] = h[j];
+  }
+  if (lane < 16) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) v = (lane == c) ? dl[c] : v;
+    a.dl[(int64_t)b * 16 + lane] = v;
+  }
+  if (lane == 0) a.loss_rows[b] = -lp[y];
+}
+
+// fixed-order workgroup sum of 256 per-thread values (wave sums, then waves 0..3)
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// fc2 weight / bias, fc1 bias gradients and the step's mean loss: workgroup o = hidden unit o
+__global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
+  __shared__ float red[4];
+  const int o = blockIdx.x;
+  float acc[NCLS + 1];
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) acc[c] = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float hv = a.h[(int64_t)b * NH + o];
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) acc[c] = __builtin_fmaf(a.dl[(int64_t)b * 16 + c], hv, acc[c]);
+    acc[NCLS] += a.dz1[(int64_t)b * NH + o];
+  }
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) {
+    const float s = block_sum(acc[c], red);
+    if (threadIdx.x == 0) a.grad[c < NCLS ? OFF_FC2_W + c * NH + o : OFF_FC1_B + o] = s;
+  }
+  if (o != 0) return;
+  float d2[NCLS + 1];
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) d2[c] = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) d2[c] += a.dl[(int64_t)b * 16 + c];
+    d2[NCLS] += a.loss_rows[b];
+  }
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) {
+    const float s = block_sum(d2[c], red);
+    if (threadIdx.x == 0) {
+      if (c < NCLS) a.grad[OFF_FC2_B + c] = s;
+      else if (a.loss_log) a.loss_log[state_of(a)->step] = s / (float)B;
+    }
+  }
+}
+
+// split-K slabs -> the flat gradient in torch layouts (fixed slab order)
+__global__ __launch_bounds__(256) void f32_conv_reduce_kernel(F32Step a, int s2, int s1) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < WG_N) {
+    const int co = t / (K2 + 1), n = t - co * (K2 + 1);
+    float s = 0.f;
+    for (int z = 0; z < s2; ++z) s += a.c2part[((int64_t)z * C2 + co) * (K2 + 1) + n];
+    if (n < K2) a.grad[OFF_CONV2_W + co * K2 + (n & 31) * 9 + (n >> 5)] = s;
+    else a.grad[OFF_CONV2_B + co] = s;
+  } else if (t < WG_N + C1 * 10) {
+    const int u = t - WG_N, c = u / 10, n = u - c * 10;
+    float s = 0.f;
+    for (int z = 0; z < s1; ++z) s += a.c1part[((int64_t)z * C1 + c) * 10 + n];
+    if (n < 9) a.grad[OFF_CONV1_W + c * 9 + n] = s;
+    else a.grad[OFF_CONV1_B + c] = s;
+  }
+}
+
+inline int kchunk(int64_t K, int max_splits) {
+  const int64_t per = (K + max_splits - 1) / max_splits;
+  return (int)((per + BK - 1) / BK * BK);
+}
+inline int nsplit(int64_t K, int kc) { return (int)((K + kc - 1) / kc); }
+inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
+}  // namespace
+
+int f32_fc1_splits(int B) { return B <= 1024 ? 36 : 9; }
+int f32_conv2w_splits(int B) { return nsplit((int64_t)B * NPIX2, kchunk((int64_t)B * NPIX2, F32_MAX_SPLITS)); }
+int f32_conv1w_splits(int B) { return nsplit((int64_t)B * NPIX1, kchunk((int64_t)B * NPIX1, F32_MAX_SPLITS)); }
+
+void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
+  if (B < 1) throw std::runtime_error("f32 forward: empty batch");
+  hipLaunchKernelGGL(f32_prep_kernel, dim3(blocks(C2 * K2)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(f32_conv1_kernel, dim3(blocks((int64_t)B * NPIX1)), dim3(256), 0, s, a, B);
+  gemm<64, 64>(PConv2Fwd{B * NPIX2, C2, K2, K2, a.a1, a.w2fwd, a.param + OFF_CONV2_B, a.y2}, 1, s);
+  if (train)
+    hipLaunchKernelGGL(f32_pool_kernel<true>, dim3(blocks((int64_t)B * C2 * 9)), dim3(256), 0, s, a, B);
+  else
+    hipLaunchKernelGGL(f32_pool_kernel<false>, dim3(blocks((int64_t)B * C2 * 9)), dim3(256), 0, s, a, B);
+  const int s1 = f32_fc1_splits(B);
+  gemm<64, 64>(PFc1{B, NH, NFLAT, NFLAT / s1, a.p, a.param + OFF_FC1_W, a.z1part}, s1, s);
+  if (train)
+    hipLaunchKernelGGL(f32_head_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, s, a, B, s1);
+  else
+    hipLaunchKernelGGL(f32_head_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, s, a, B, s1);
+}
+
+void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(f32_fc_small_kernel, dim3(NH), dim3(256), 0, s, a, B);
+  gemm<64, 64>(PFc1W{NH, NFLAT, B, (B + BK - 1) / BK * BK, a.dz1, a.p, a.grad + OFF_FC1_W}, 1, s);
+  gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.param + OFF_FC1_W, a.pm, a.y2, a.state, 1.0f}, 1, s);
+  const int64_t k2 = (int64_t)B * NPIX2;
+  const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
+  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part}, s2, s);
+  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
+  const int64_t k1 = (int64_t)B * NPIX1;
+  const int kc1 = kchunk(k1, F32_MAX_SPLITS), s1 = nsplit(k1, kc1);
+  gemm<64, 64>(PConv1W{C1, 10, (int)k1, kc1, a.a1, a, 0, a.c1part}, s1, s);
+  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(blocks(WG_N + C1 * 10)), dim3(256), 0, s, a, s2, s1);
+}
+
+}  // namespace mnist

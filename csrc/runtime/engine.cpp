@@ -1,6 +1,7 @@
 #include "engine.h"
 #include "host_logic.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -18,15 +19,16 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 }  // namespace
 
 Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipStream_t compute,
-               hipStream_t comm, int world_size, float rho, float eps, float weight_decay)
+               hipStream_t comm, int world_size, float rho, float eps, float weight_decay, bool fp32)
     : buf_(buf), max_batch_(max_batch), max_test_batch_(max_test_batch), compute_(compute),
-      comm_stream_(comm), world_(world_size), rho_(rho), eps_(eps), wd_(weight_decay) {
+      comm_stream_(comm), world_(world_size), rho_(rho), eps_(eps), wd_(weight_decay), f32_(fp32) {
   if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   alloc_workspace();
+  if (f32_) alloc_workspace_f32();
 }
 
 Engine::~Engine() {
@@ -45,6 +47,7 @@ Engine::~Engine() {
   for (hipEvent_t e : {ev_fc_, ev_done_, ev_fork_, ev_join_})
     if (e) hipEventDestroy(e);
   if (ws_) hipFree(ws_);
+  if (ws32_) hipFree(ws32_);
 }
 
 void Engine::alloc_workspace() {
@@ -71,12 +74,54 @@ void Engine::alloc_workspace() {
   c1red_ = reinterpret_cast<float*>(base + L.c1red);
 }
 
+void Engine::alloc_workspace_f32() {
+  const int64_t M = max_batch_, Ma = max_batch_ > max_test_batch_ ? max_batch_ : max_test_batch_;
+  // fc1 split-K partials: 36 splits up to 1024 rows, 9 beyond (f32_fc1_splits), for any batch <= Ma
+  const int64_t z1rows = std::max<int64_t>(36 * std::min<int64_t>(Ma, 1024), 9 * Ma);
+  int64_t off = 0;
+  auto carve = [&](int64_t bytes) { int64_t o = off; off += ws_align256(bytes); return o; };
+  const int64_t o_w2f = carve(9 * C1 * C2 * 4), o_w2b = carve(9 * C1 * C2 * 4);
+  const int64_t o_a1 = carve(Ma * H1 * H1 * C1 * 4), o_y2 = carve(Ma * H2 * H2 * C2 * 4);
+  const int64_t o_p = carve(Ma * NFLAT * 4), o_pm = carve(Ma * NFLAT), o_z1 = carve(z1rows * NH * 4);
+  const int64_t o_h = carve(M * NH * 4), o_dz1 = carve(M * NH * 4), o_dl = carve(M * 16 * 4);
+  const int64_t o_loss = carve(M * 4);
+  const int64_t o_c2 = carve((int64_t)F32_MAX_SPLITS * C2 * (9 * C1 + 1) * 4);
+  const int64_t o_c1 = carve((int64_t)F32_MAX_SPLITS * C1 * 10 * 4);
+  HIP_OK(hipMalloc(&ws32_, off));
+  HIP_OK(hipMemset(ws32_, 0, off));
+  ws_bytes_ += off;
+  char* b = static_cast<char*>(ws32_);
+  F32Step& w = f32ws_;
+  w.w2fwd = reinterpret_cast<float*>(b + o_w2f);
+  w.w2bwd = reinterpret_cast<float*>(b + o_w2b);
+  w.a1 = reinterpret_cast<float*>(b + o_a1);
+  w.y2 = reinterpret_cast<float*>(b + o_y2);
+  w.p = reinterpret_cast<float*>(b + o_p);
+  w.pm = reinterpret_cast<uint8_t*>(b + o_pm);
+  w.z1part = reinterpret_cast<float*>(b + o_z1);
+  w.h = reinterpret_cast<float*>(b + o_h);
+  w.dz1 = reinterpret_cast<float*>(b + o_dz1);
+  w.dl = reinterpret_cast<float*>(b + o_dl);
+  w.loss_rows = reinterpret_cast<float*>(b + o_loss);
+  w.c2part = reinterpret_cast<float*>(b + o_c2);
+  w.c1part = reinterpret_cast<float*>(b + o_c1);
+}
+
+F32Step Engine::f32_args() const {
+  F32Step a = f32ws_;
+  a.param = buf_.param;
+  a.grad = buf_.grad;
+  a.loss_log = buf_.loss_log;
+  return a;
+}
+
 void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
   if (comm && comm->world_size() != world_) throw std::runtime_error("comm world size mismatch");
   comm_ = std::move(comm);
 }
 
 void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
+  if (x && f32_) throw std::runtime_error("engine: the fp32 step has no xGMI schedule (use RCCL)");
   if (x && x->world_size() != world_) throw std::runtime_error("xgmi world size mismatch");
   if (x && x->world_size() > 1 && !x->connected()) throw std::runtime_error("xgmi communicator not connected");
   if (x && x->numel() != PARAM_TOTAL) throw std::runtime_error("xgmi communicator must cover the flat gradient");
@@ -92,6 +137,8 @@ void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
 }
 
 void Engine::set_schedule(int s) {
+  if (f32_ && s != SERIAL && s != RCCL)
+    throw std::runtime_error("engine: the fp32 step runs the SERIAL or RCCL schedule only");
   if (s == SERIAL || s == OVERLAP) {
     if (world_ != 1 || comm_ || xgmi_)
       throw std::runtime_error("engine: the single-GPU schedules need world size 1 and no transport attached");
@@ -158,6 +205,10 @@ void Engine::enqueue_step(int batch, bool last) {
   // world times too small
   if (world_ > 1 && sched_ != RCCL && sched_ != XGMI)
     throw std::runtime_error("engine: world size > 1 needs the RCCL or XGMI schedule");
+  if (f32_) {
+    enqueue_step_f32(batch);
+    return;
+  }
   const int B = batch, Bp = round_up(B, 32);
   const int stride = idx_stride_;
   float* P = buf_.param;
@@ -365,6 +416,31 @@ void Engine::enqueue_step(int batch, bool last) {
   }
 }
 
+// fp32 step: forward, every gradient, (RCCL: one all-reduce of the whole flat gradient on the
+// compute stream), the whole Adadelta update (which advances the device step counter)
+void Engine::enqueue_step_f32(int batch) {
+  const bool pre = buf_.epoch_u8 != nullptr;
+  F32Step a = f32_args();
+  a.data_u8 = pre ? buf_.epoch_u8 : buf_.train_u8;
+  a.idx = pre ? nullptr : buf_.train_idx;
+  a.idx_step_stride = idx_stride_;
+  a.labels = pre ? buf_.epoch_labels : buf_.train_labels;
+  a.state = buf_.state;
+  a.inv_batch = ddp_head_inv_batch(batch, world_);
+  phase_begin("fwd");
+  launch_f32_forward(a, batch, true, compute_);
+  phase_end();
+  phase_begin("bwd");
+  launch_f32_backward(a, batch, compute_);
+  phase_end();
+  phase_begin("allreduce+update");
+  if (sched_ == RCCL) comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
+  AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
+                  buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, buf_.state};
+  launch_adadelta(ad, ADA_ALL, compute_);
+  phase_end();
+}
+
 void Engine::train_steps(int n, int batch, int stride) {
   if (batch < 1 || batch > max_batch_) throw std::runtime_error("batch exceeds engine capacity");
   idx_stride_ = stride;
@@ -517,6 +593,18 @@ void Engine::enqueue_eval(int n_total, int batch) {
   const float* P = buf_.param;
   for (int s = 0; s < n_total; s += batch) {
     const int B = (n_total - s) < batch ? (n_total - s) : batch;
+    if (f32_) {
+      F32Step a = f32_args();
+      a.data_u8 = buf_.test_u8;
+      a.idx = buf_.test_idx + s;
+      a.idx_step_stride = 0;
+      a.labels = buf_.test_labels;
+      a.state = nullptr;
+      a.loss_rows = buf_.test_loss_rows + s;
+      a.correct = buf_.test_correct + s;
+      launch_f32_forward(a, B, false, compute_);
+      continue;
+    }
     TrunkFwdArgs tf{buf_.test_u8, buf_.test_idx + s, 0, nullptr, P + OFF_CONV1_W, P + OFF_CONV1_B,
                     buf_.w2f, P + OFF_CONV2_B, nullptr, p_, nullptr, nullptr};
     launch_trunk_fwd(tf, B, false, compute_);

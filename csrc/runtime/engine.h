@@ -67,8 +67,10 @@ struct EngineBuffers {
 
 class Engine {
  public:
+  // fp32: the --dtype fp32 step (f32_net.hip: f32-input MFMA GEMMs, fp32 activations); SERIAL
+  // (single GPU) or RCCL (one all-reduce of the whole gradient before the update) schedules only
   Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipStream_t compute,
-         hipStream_t comm, int world_size, float rho, float eps, float weight_decay);
+         hipStream_t comm, int world_size, float rho, float eps, float weight_decay, bool fp32 = false);
   ~Engine();
 
   enum Schedule : int { SERIAL = 0, OVERLAP = 1, RCCL = 2, XGMI = 3 };
@@ -122,12 +124,15 @@ class Engine {
   void check_errors() const;                         // throws with a decoded message
   static std::string describe_xgmi_error(int code);
   int64_t workspace_bytes() const { return ws_bytes_; }
+  bool fp32() const { return f32_; }
 
   // single-op entry points used by the numerics tests / module API
   const EngineBuffers& buffers() const { return buf_; }
 
  private:
   void enqueue_step(int batch, bool last);
+  void enqueue_step_f32(int batch);
+  F32Step f32_args() const;
   bool side_schedule() const { return sched_ == OVERLAP || sched_ == XGMI; }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
@@ -135,6 +140,7 @@ class Engine {
   void side_worker();
   void enqueue_eval(int n_total, int batch);
   void alloc_workspace();
+  void alloc_workspace_f32();
 
   EngineBuffers buf_;
   int max_batch_, max_test_batch_;
@@ -176,6 +182,10 @@ class Engine {
   uint8_t* dyc_;                     // compact un-pooled gradient records (DYC_REC per pooled position)
   uint8_t* pmask_;
   float *z1part_, *loss_rows_, *c1part_, *w2part_, *fcpart_;
+  // fp32 mode workspace (F32Step's buffers)
+  bool f32_ = false;
+  void* ws32_ = nullptr;
+  F32Step f32ws_{};
   std::vector<hipGraphExec_t> graphs_;
   std::vector<hipGraph_t> graph_defs_;
 };

@@ -12,8 +12,9 @@ behaviour):
 * ``--bucket-cap-mb`` / ``--first-bucket-mb``: DDP gradient bucket sizing.
 * ``--engine {fused,module}``: native step engine vs the reference's module-level loop.
 * ``--dtype {bf16,fp32}``: bf16 = the MI355X kernels (bf16 MFMA operands, fp32 accumulation,
-  fp32 master weights / optimizer state / gradient all-reduce); fp32 = stock torch fp32 ops on
-  the GPU (module engine) for exact-parity debugging.
+  fp32 master weights / optimizer state / gradient all-reduce); fp32 = the reference's precision:
+  the fused engine's fp32 step (csrc/kernels/f32_net.hip, f32-input MFMA GEMMs; RCCL at N > 1),
+  or stock torch fp32 ops with ``--engine module``.
 * ``--dist-backend``: process-group backend override (``gloo`` + ``--allreduce xgmi`` needs no
   RCCL at all, e.g. several ranks on one GPU).
 * ``--check-sync``: all-gather a parameter checksum after every epoch (DDP desync detector).
@@ -60,7 +61,8 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
     g.add_argument('--synthetic-size', dest='synthetic_train_size', type=int, default=None,
                    help='alias of --synthetic-train-size')
     g.add_argument('--dtype', choices=['bf16', 'fp32'], default='bf16',
-                   help='bf16: MI355X MFMA kernels (default); fp32: torch fp32 ops (parity/debug, module engine)')
+                   help='bf16: MI355X bf16-MFMA kernels (default); fp32: the fp32 step (f32-input MFMA kernels; '
+                        'torch fp32 ops with --engine module)')
     g.add_argument('--check-sync', action='store_true', default=False,
                    help='verify parameters are identical on every rank after each epoch')
     g.add_argument('--engine', choices=['fused', 'module'], default=None,

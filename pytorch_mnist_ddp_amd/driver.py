@@ -101,7 +101,7 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
     device = torch.device(f"cuda:{gpu}" if use_cuda else "cpu") if ddp_script else \
         torch.device("cuda" if use_cuda else "cpu")
     engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
-    if not use_cuda or getattr(args, "dtype", "bf16") == "fp32":
+    if not use_cuda:
         engine = "module"
     # the HIP context + the native extension's code objects come up on a helper thread while this
     # one builds the data set and the model's CPU init (joined in _run_fused: "hip_init")
@@ -129,7 +129,7 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
         test_stream = RandomIndexStream(len(test_data)) if use_cuda else SequentialIndexStream(len(test_data))
 
     model = Net()
-    if getattr(args, "dtype", "bf16") == "fp32":     # stock torch fp32 ops: module engine only
+    if getattr(args, "dtype", "bf16") == "fp32":     # module engine: stock torch fp32 ops; fused: f32_net.hip
         model.compute_dtype = torch.float32
     if args.resume:
         load_state_dict(model, args.resume, map_location="cpu")
@@ -252,7 +252,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
-                           allreduce=allreduce, two_buckets=two_buckets)
+                           allreduce=allreduce, two_buckets=two_buckets,
+                           fp32=getattr(args, "dtype", "bf16") == "fp32")
     setup.mark("trainer")
     if distributed and rank == 0 and trainer.allreduce_timings:
         print(f"| gradient all-reduce: {trainer.allreduce} (schedule us/step: {trainer.allreduce_timings})",

@@ -82,13 +82,15 @@ class FusedTrainer:
     ``overlap`` (single GPU): the OVERLAP schedule (optimizer work on the comm stream) when the two
     streams pass the hand-off probe, else SERIAL.  ``xgmi_fuse``: the xGMI kernels apply Adadelta
     themselves (False = separate launches: the fused kernels' bitwise oracle).  ``probe_world1``
-    (tests): with a communicator at world 1, evaluate the xGMI candidate under "auto" too."""
+    (tests): with a communicator at world 1, evaluate the xGMI candidate under "auto" too.
+    ``fp32`` (``--dtype fp32``): the fp32 step of ``f32_net.hip`` (f32-input MFMA GEMMs, fp32
+    activations and gradient operands) in the SERIAL schedule, or RCCL at world > 1."""
 
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
                  two_buckets: bool = True, allreduce: str | None = None, overlap: bool = True,
-                 xgmi_fuse: bool = True, probe_world1: bool = False):
+                 xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False):
         C = native.load()
         self.C, self.ms = C, mstate
         # host seconds per setup phase (engine, xgmi_comm, stream_probe, validate.<transport>,
@@ -148,9 +150,10 @@ class FusedTrainer:
         # with --test-batch-size chunks: every eval kernel computes rows independently and the
         # losses / hits are summed once on the host): 3 launches instead of 3 per 1000 images
         self.eval_batch = self.n_test if 0 < self.n_test <= 16384 else max(self.TB, 1)
+        self.fp32 = bool(fp32)
         self.engine = C.Engine(bufs, self.B, max(self.eval_batch, self.TB, 1) if test is not None else 1,
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
-                               world_size, mstate.rho, mstate.eps, mstate.weight_decay)
+                               world_size, mstate.rho, mstate.eps, mstate.weight_decay, fp32=self.fp32)
         self.engine.set_bucket_split(two_buckets)
         self._graphs: dict[tuple[int, int], int] = {}        # captured chunks of the selected schedule
         self._graph_sets: dict[str, dict] = {}               # per transport (validation captures)
@@ -165,6 +168,8 @@ class FusedTrainer:
             allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
         if allreduce not in ("rccl", "xgmi", "auto"):
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
+        if self.fp32 and allreduce == "xgmi":
+            raise ValueError("the fp32 step all-reduces over RCCL only (--allreduce rccl or auto)")
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
         self.xgmi, self.grad_out = None, None
@@ -195,7 +200,7 @@ class FusedTrainer:
         # OVERLAP (default): the fc Adadelta step and conv2's reduce + update on the comm stream under
         # the conv backward (measured B = 200: 82.7 vs 85.2 us/step serial, then 70.8-71.2 with
         # conv2's part moved too); SERIAL when the streams share a hardware queue
-        self.overlap = bool(overlap) and self._probe_streams()
+        self.overlap = bool(overlap) and not self.fp32 and self._probe_streams()
         self.engine.set_schedule(C.SCHED_OVERLAP if self.overlap else C.SCHED_SERIAL)
 
     def _use_graph_set(self, name: str) -> None:
@@ -206,8 +211,8 @@ class FusedTrainer:
         from ..parallel.distributed import create_xgmi_comm, release_xgmi_comm
         C = self.C
         self.overlap = False
-        want_x = allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
-                                          and (self.world > 1 or probe_world1))
+        want_x = not self.fp32 and (allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
+                                                            and (self.world > 1 or probe_world1)))
         want_r = comm is not None and allreduce in ("rccl", "auto")
         x = None
         if want_x:
