@@ -263,11 +263,45 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     n_train = len(train_data)
     n_batches = num_batches(len(train_stream), args.batch_size)
     log_rank = (not distributed) or rank == 0
-    for epoch in range(1, args.epochs + 1):
+    # Epoch pipelining: the evaluation after epoch e is enqueued behind its training and read back
+    # while epoch e+1's first chunks run; its test line is printed (from train_epoch's before_log
+    # hook) before any train line of e+1, and the next epoch's sampler order is drawn on the host
+    # while the GPU works - the same lines, values and RNG draw order (train base seed, sampler
+    # permutation, test base seed [, test permutation], next epoch's train base seed, ...) as the
+    # reference's sequential loop, without a host sync and an idle GPU at every epoch boundary.
+    # --check-sync compares parameters after each epoch, which needs the sequential form.
+    pipelined = not (distributed and args.check_sync) and not args.profile
+
+    def next_indices(epoch):
         if distributed:
             train_stream.set_epoch(epoch)
         consume_loader_base_seed()          # iter(train_loader)
-        idx = train_stream.epoch_indices()
+        return train_stream.epoch_indices()
+
+    def finish(p):
+        """Epoch p["epoch"]'s test line, sync check and JSON record (its evaluation is complete or
+        completes here)."""
+        epoch, st, rec = p["epoch"], p["st"], p["rec"]
+        if p["handle"] is not None:
+            loss_sum, correct, n = p["handle"].result()
+            print(test_line(loss_sum / n, correct, n))
+            rec.update(test_loss=loss_sum / n, correct=correct)
+            setup.mark(f"epoch{epoch}_eval")
+        dev_s = st.device_time()
+        rec["device_train_s"] = dev_s
+        if dev_s:
+            rec["device_img_per_s"] = st.samples / dev_s
+            if pipelined:                     # host time is enqueue time here: report the device's
+                rec["host_train_s"], rec["train_s"] = rec["train_s"], dev_s
+        if distributed and args.check_sync:
+            from .parallel.ddp import assert_params_in_sync
+            trainer.synchronize()
+            assert_params_in_sync([ms.param])
+        _json_log(args.json_log, rec)
+
+    idx = next_indices(1)
+    pend = None
+    for epoch in range(1, args.epochs + 1):
         trainer.set_lr(lr)
 
         def log_fn(batch_idx, blen, loss, epoch=epoch):
@@ -275,9 +309,11 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             seen = (world if distributed else 1) * batch_idx * blen
             print(train_line(epoch, seen, n_train, batch_idx, n_batches, loss), flush=False)
 
+        hook = (lambda p=pend: finish(p)) if pend is not None else None
         with roctx_range(f"train_epoch_{epoch}", args.profile):
-            st = trainer.train_epoch(epoch, idx, args.log_interval,
-                                     dry_run=args.dry_run, log_fn=log_fn if log_rank else None)
+            st = trainer.train_epoch(epoch, idx, args.log_interval, dry_run=args.dry_run,
+                                     log_fn=log_fn if log_rank else None, sync=not pipelined, before_log=hook)
+        pend = None
         setup.mark(f"epoch{epoch}_train")
         if epoch == 1:                     # the trainer's phases include epoch 1's graph captures
             setup.update(trainer.setup, prefix="trainer.")
@@ -285,25 +321,24 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                                       "setup_info": setup.info, "allreduce": trainer.allreduce if distributed else None,
                                       "transport_report": trainer.transport_report or None})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
-               "img_per_s": st.samples / max(st.train_seconds, 1e-9), "device_train_s": st.device_seconds}
-        if st.device_seconds:
-            rec["device_img_per_s"] = st.samples / st.device_seconds
+               "img_per_s": st.samples / max(st.train_seconds, 1e-9)}
+        handle = None
         if log_rank:
             consume_loader_base_seed()      # iter(test_loader)
             if isinstance(test_stream, RandomIndexStream):
                 test_stream.epoch_indices()  # mnist.py CUDA path shuffles the test set: same RNG draw
             with roctx_range(f"eval_epoch_{epoch}", args.profile):
-                loss_sum, correct, n = trainer.evaluate()
-            print(test_line(loss_sum / n, correct, n))
-            rec.update(test_loss=loss_sum / n, correct=correct)
-            setup.mark(f"epoch{epoch}_eval")
-        if distributed and args.check_sync:
-            from .parallel.ddp import assert_params_in_sync
-            trainer.synchronize()
-            assert_params_in_sync([ms.param])
-        _json_log(args.json_log, rec)
+                handle = trainer.evaluate_async()
+        if epoch < args.epochs:
+            idx = next_indices(epoch + 1)   # host work under the evaluation / the epoch's tail
+        pend = {"epoch": epoch, "st": st, "rec": rec, "handle": handle}
+        if not pipelined:
+            finish(pend)
+            pend = None
         lr = lr * args.gamma                                   # scheduler.step()
-    trainer.synchronize()
+    if pend is not None:
+        finish(pend)
+    trainer.synchronize()                 # (raises on a device hand-off / xGMI stage timeout)
     setup.mark("train_done")
     _save(args, model_for_save, distributed, rank, ddp_script)
     setup.mark("saved")

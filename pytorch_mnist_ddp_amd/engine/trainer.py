@@ -56,6 +56,32 @@ class EpochStats:
     train_seconds: float
     losses: dict = field(default_factory=dict)   # batch_idx -> loss for logged steps
     device_seconds: float | None = None          # HIP-event time of the epoch's training work
+    events: tuple | None = None                  # (start, end) HIP events of that work (sync=False)
+
+    def device_time(self) -> float | None:
+        """Device seconds of the epoch's training work (waits for its end event when needed)."""
+        if self.device_seconds is None and self.events is not None:
+            self.events[1].synchronize()
+            self.device_seconds = self.events[0].elapsed_time(self.events[1]) / 1000.0
+        return self.device_seconds
+
+
+class EvalHandle:
+    """An enqueued evaluation (FusedTrainer.evaluate_async): per-row losses / hits land in pinned
+    buffers; ``result()`` waits for them and sums in float64 on the host (fixed order)."""
+
+    def __init__(self, event, rows, hits, n: int):
+        self.event, self.rows, self.hits, self.n = event, rows, hits, n
+        self._res = None
+
+    def result(self) -> tuple[float, int, int]:
+        if self._res is None:
+            if self.event is None:
+                self._res = (0.0, 0, 0)
+            else:
+                self.event.synchronize()
+                self._res = (float(self.rows.double().sum()), int(self.hits.sum()), self.n)
+        return self._res
 
 
 class TransportHang(RuntimeError):
@@ -477,13 +503,15 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------ training
     def train_epoch(self, epoch: int, idx: torch.Tensor, log_interval: int = 10, dry_run: bool = False,
-                    log_fn=None, sync: bool = True) -> EpochStats:
+                    log_fn=None, sync: bool = True, before_log=None) -> EpochStats:
         """Run one epoch over this rank's index vector ``idx``.
 
         ``log_fn(batch_idx, batch_len, loss)`` is called (in order) for every batch with
         ``batch_idx % log_interval == 0``; pass None to skip the per-chunk syncs entirely.
         ``sync=False`` returns as soon as the epoch is enqueued (``train_seconds`` is then the enqueue
         time): the caller overlaps host work - the next epoch's sampler order - with the GPU.
+        ``before_log()`` runs once, before the first ``log_fn`` call (or at the end): the driver
+        prints the previous epoch's test line there, after this epoch's first chunks are enqueued.
         """
         n = idx.numel()
         full, last = divmod(n, self.B)
@@ -501,8 +529,15 @@ class FusedTrainer:
         # host waits for that step (an event, not the whole stream), so the GPU never idles while the
         # host reads the loss and prints.  Lines come out in the same order with the same values.
         pending = []
+        hook = [before_log]
+
+        def run_hook():
+            if hook[0] is not None:
+                h, hook[0] = hook[0], None
+                h()
 
         def flush_one():
+            run_hook()
             ev, b_idx, blen = pending.pop(0)
             ev.synchronize()
             loss = float(self.loss_log[b_idx].item())
@@ -539,13 +574,14 @@ class FusedTrainer:
         ev1.record(self.compute)
         while pending:
             flush_one()
+        run_hook()
         dev_s = None
         if sync:
             self.compute.synchronize()
             if self.xgmi is not None or self.comm is not None or self.overlap:
                 self.check_errors()        # fail at the first bad epoch, not after the last one
             dev_s = ev0.elapsed_time(ev1) / 1000.0
-        return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged, dev_s)
+        return EpochStats(epoch, steps, min(n, steps * self.B), time.perf_counter() - t0, logged, dev_s, (ev0, ev1))
 
     # ------------------------------------------------------------------ raw step stream (bench)
     def start_stream(self, idx: torch.Tensor, gather: bool = True) -> None:
@@ -598,8 +634,13 @@ class FusedTrainer:
     # ------------------------------------------------------------------ evaluation
     def evaluate(self) -> tuple[float, int, int]:
         """Return (sum of per-sample NLL, correct, N) over the whole test split."""
+        return self.evaluate_async().result()
+
+    def evaluate_async(self) -> "EvalHandle":
+        """Enqueue the evaluation and its read-back; ``.result()`` waits for them (an event, not the
+        stream) and reduces on the host, so work enqueued after this call keeps the GPU busy."""
         if self.n_test == 0:
-            return 0.0, 0, 0
+            return EvalHandle(None, None, None, 0)
         # one batch = 3 launches: eager (a captured graph only pays when there are many batches)
         if self.use_graphs and self.n_test > self.eval_batch:
             if self._eval_graph is None:
@@ -613,10 +654,9 @@ class FusedTrainer:
         with torch.cuda.stream(self.compute):
             rows.copy_(self.test_loss_rows, non_blocking=True)
             hits.copy_(self.test_correct, non_blocking=True)
-        self.compute.synchronize()
-        loss_sum = float(rows.double().sum())
-        correct = int(hits.sum())
-        return loss_sum, correct, self.n_test
+            ev = torch.cuda.Event()
+            ev.record(self.compute)
+        return EvalHandle(ev, rows, hits, self.n_test)
 
     def synchronize(self) -> None:
         self.engine.synchronize()

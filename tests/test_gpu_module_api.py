@@ -198,6 +198,10 @@ def test_scripts_on_gpu(tmp_path):
     out = r.stdout
     assert "Not using distributed mode" in out and out.count("Test set: Average loss:") == 2
     assert "Train Epoch: 2 [2000/4000 (50%)]" in out and "Total cost time:" in out
+    # epoch pipelining (driver.py): every epoch's test line after its train lines, before the next's
+    kinds = [ln.split(":")[0].split(" [")[0] for ln in out.splitlines()
+             if ln.startswith(("Train Epoch", "Test set"))]
+    assert kinds == ["Train Epoch"] * 2 + ["Test set"] + ["Train Epoch"] * 2 + ["Test set"], kinds
     sd = torch.load(os.path.join(tmp_path, "mnist_cnn_.pt"), weights_only=True)
     assert sd["fc1.weight"].is_cuda and sd["fc1.weight"].dtype == torch.float32
     r = subprocess.run([sys.executable, os.path.join(ROOT, "mnist.py"), *common, "--engine", "module", "--dry-run"],
