@@ -451,18 +451,24 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
         w0 = time.perf_counter()
         sampler.set_epoch(1)
         idx = sampler.epoch_indices()
+        pending = None
         for epoch in range(1, args.epochs + 1):
             tr.set_lr(1.0 * (0.7 ** (epoch - 1)))
             tr.train_epoch(epoch, idx, sync=False)       # enqueued; the GPU runs while the host
+            if pending is not None:                      # reads the previous epoch's evaluation
+                ls, correct, n = pending.result()
+                acc = correct / max(1, n)
             if use_pg:                                   # per-epoch cross-rank fingerprint, on the
                 with torch.cuda.stream(tr.compute):      # device (compared after the run: no sync)
                     fps.append(params_fingerprint([ms.param]))
+            if rank == 0:
+                pending = tr.evaluate_async()
             if epoch < args.epochs:                      # draws the next epoch's sampler order
                 sampler.set_epoch(epoch + 1)
                 idx = sampler.epoch_indices()
-            if rank == 0:
-                ls, correct, n = tr.evaluate()
-                acc = correct / max(1, n)
+        if pending is not None:
+            ls, correct, n = pending.result()
+            acc = correct / max(1, n)
         tr.synchronize()
         if use_pg:
             barrier()
