@@ -126,8 +126,8 @@ def test_validation_fault_in_replayed_graph_is_named(cuda_device, tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=tmp_path, env=env)
     err = r.stdout + r.stderr
     assert r.returncode != 0, err[-3000:]
-    assert "failed its startup validation" in err, err[-3000:]
-    assert "timed out" in err and "rank " in err, err[-3000:]
+    assert "no gradient all-reduce passed its startup validation" in err, err[-3000:]
+    assert "[xgmi] startup validation failed" in err and "timed out" in err and "rank 2" in err, err[-3000:]
     assert "Train Epoch" not in r.stdout                         # nothing trained on the bad comm
 
 

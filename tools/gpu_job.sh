@@ -36,9 +36,13 @@ run_step() {
   case $kind in
     tests)
       [ $# -eq 0 ] && set -- tests
-      timeout -k 10 1500 python -u -m pytest "$@" -m gpu -x -v --timeout 170 --timeout-method thread \
+      # no -x: an assertion failure (rc 1) is reported and the job goes on; a timeout, abort or
+      # crash of the test process (124/134/137/139) still ends it
+      timeout -k 10 1500 python -u -m pytest "$@" -m gpu -v --timeout 170 --timeout-method thread \
         > gpurun_out/tests.log 2>&1; local rc=$?
-      tail -4 gpurun_out/tests.log; fatal $rc "tests $*";;
+      grep -E "^(FAILED|ERROR)" gpurun_out/tests.log | head -20; tail -2 gpurun_out/tests.log
+      [ $rc -eq 1 ] && { echo "tests: failures (rc 1), continuing"; return 0; }
+      fatal $rc "tests $*";;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; local rc=$?
       tail -1 gpurun_out/smoke.log; fatal $rc smoke;;
