@@ -187,8 +187,6 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default 50; --cpu: 10)")
     ap.add_argument("--batch-size", type=int, default=200, help="per-GPU batch (README config: 200)")
     ap.add_argument("--graph-steps", type=int, default=25, help="steps per captured hipGraph (0 = eager)")
-    ap.add_argument("--lead-steps", type=int, default=0,
-                    help="steps of the short graph the timed run opens with (0 = none)")
     ap.add_argument("--single-bucket", action="store_true", help="one all-reduce per step (no overlap)")
     ap.add_argument("--no-full-run", dest="full_run", action="store_false")
     ap.add_argument("--epochs", type=int, default=EPOCHS, help="epochs for the full-run wallclock")
@@ -358,7 +356,6 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                       two_buckets=not args.single_bucket, allreduce=args.allreduce,
                       fp32=args.dtype == "fp32")
     diag.tr = tr
-    tr.lead_steps = args.lead_steps
     phases.add("trainer", time.perf_counter() - t_tr)
 
     # flat index stream = consecutive DistributedSampler epochs, full batches only
@@ -532,7 +529,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
             "config": {"model": "mnist_cnn (reference Net: conv32-conv64-maxpool-fc128-fc10, 1.2M params)",
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
-                       "graph_steps": args.graph_steps, "lead_steps": args.lead_steps, "buckets": 1 if args.single_bucket else 2,
+                       "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
                        "warm_replay": bool(args.warm_replay), **comm_info},
             "params_in_sync": in_sync,
             "desync_epoch": desync_epoch,

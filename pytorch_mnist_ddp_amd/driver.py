@@ -86,12 +86,16 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
     setup = PhaseTimes(origin=t_start)
     args = cli.parse_args(ddp=ddp_script, argv=argv)
     args._ddp_script = ddp_script
-    use_cuda = not args.no_cuda and torch.cuda.is_available()
+    # device_count() reads the device list without initialising HIP (is_available() brings the
+    # runtime up: ~60 ms on the main thread inside the timer); the fused engine's HIP init runs on
+    # the prewarm thread instead, under the data build
+    use_cuda = not args.no_cuda and torch.cuda.device_count() > 0
     distributed, world, rank, gpu = False, 1, 0, 0
     args._setup = setup
     setup.mark("args")
     if ddp_script:
         from .parallel.distributed import init_distributed_mode
+        args._defer_set_device = use_cuda and (getattr(args, "engine", None) or "fused") == "fused"
         with setup.phase("pg_init"):
             init_distributed_mode(args)
         distributed = args.distributed
@@ -145,6 +149,8 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
 
 def _run_module(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world, rank,
                 gpu, ddp_script):
+    if distributed and device.type == "cuda" and getattr(args, "_defer_set_device", False):
+        torch.cuda.set_device(gpu)
     model = model.to(device)
     model_without_ddp = model
     if distributed:
@@ -222,6 +228,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                 raise pw.error
         else:
             _prewarm_body(device)
+        if distributed:
+            torch.cuda.set_device(gpu)       # (deferred by init_distributed_mode: runtime is up now)
     setup.mark("hip_native")
     t_model = time.perf_counter()
     ms = ModelState(model, device, lr=args.lr)

@@ -129,10 +129,6 @@ class FusedTrainer:
         self.world, self.rank = world_size, rank
         self.seed = int(seed)
         self.graph_steps = int(graph_steps)
-        # run_steps() opens with a short graph of this many steps: the GPU starts on it while the
-        # host is still submitting the big chunk behind it (a graph's packets only start once its
-        # launch call has submitted them all: ~6 us per step of host time).  0 = off.
-        self.lead_steps = 0
         self.flags = 0 if dropout else FLAG_NO_DROPOUT
         self.num_samples = int(num_samples)                 # per-rank samples per epoch
         self.steps_per_epoch = math.ceil(self.num_samples / self.B)
@@ -592,11 +588,9 @@ class FusedTrainer:
         self.rng_base += 2 * (idx.numel() // self.B)
 
     def _chunks(self, n: int) -> list[int]:
-        """Graph sizes ``run_steps(n)`` replays: an optional ``lead_steps`` graph, then
-        ``graph_steps`` each, the last one shorter."""
+        """Graph sizes ``run_steps(n)`` replays: ``graph_steps`` each, the last one shorter."""
         c = self.graph_steps if self.graph_steps > 0 else max(1, n)
-        lead = self.lead_steps if 0 < self.lead_steps < n and self.graph_steps > 0 else 0
-        return ([lead] if lead else []) + [min(c, n - lead - k) for k in range(0, n - lead, c)]
+        return [min(c, n - k) for k in range(0, n, c)]
 
     def precapture(self, n: int) -> None:
         """Capture every graph ``run_steps(n)`` will replay (capture executes nothing)."""

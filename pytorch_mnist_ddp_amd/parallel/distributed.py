@@ -33,7 +33,8 @@ from .hostcomm import get_hostcomm
 
 
 def init_distributed_mode(args) -> None:
-    use_cuda = not getattr(args, "no_cuda", False) and torch.cuda.is_available()
+    # device_count() does not bring the HIP runtime up (is_available() does, ~60 ms)
+    use_cuda = not getattr(args, "no_cuda", False) and torch.cuda.device_count() > 0
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
         args.rank = int(os.environ["RANK"])
         args.world_size = int(os.environ["WORLD_SIZE"])
@@ -53,7 +54,10 @@ def init_distributed_mode(args) -> None:
     if use_cuda and os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
         args.gpu = 0        # rehearsal knob: every rank on GPU 0 (needs --dist-backend gloo --allreduce xgmi)
     if use_cuda:
-        torch.cuda.set_device(args.gpu)
+        # the fused driver selects the device after its HIP prewarm thread has initialised the
+        # runtime (args._defer_set_device): the process group itself is lazy and touches no device
+        if not getattr(args, "_defer_set_device", False):
+            torch.cuda.set_device(args.gpu)
         args.dist_backend = getattr(args, "pg_backend", None) or "nccl"
     else:
         args.dist_backend = "gloo"
