@@ -87,6 +87,7 @@ def measure(args):
     tr.start_stream(stream, gather=True)
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
+    tr.warm_graphs(args.steps)                           # as bench.py: every timed graph has run once
     tr.run_steps(args.warmup)
     tr.synchronize()
     C.timeline_dump()                                    # discard the warmup's records
@@ -125,6 +126,15 @@ def analyse(recs, steps):
             "step_periods_us": [round((b - a) / 100.0, 1) for a, b in zip(starts, starts[1:])]}
     ends = [c[1] for launches in cl.values() for c in launches]
     span["window_us"] = round((max(ends) - starts[0]) / 100.0, 1)       # first trunk start -> last end
+    # the first replayed step (from an idle GPU, right after the graph launches): every launch that
+    # starts before the second trunk_fwd, relative to the first trunk_fwd start
+    first = []
+    for kid, launches in cl.items():
+        for s, e, w in launches:
+            if s < starts[1]:
+                first.append((round((s - starts[0]) / 100.0, 2), round((e - starts[0]) / 100.0, 2),
+                              NAMES[kid] if kid < len(NAMES) else str(kid)))
+    span["first_step"] = sorted(first)
     return table, span
 
 
@@ -160,7 +170,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=200)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph-steps", type=int, default=25)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-product", action="store_true")
@@ -180,6 +190,10 @@ def main() -> int:
                      f"{r['start_us']} | {r['end_us']} | {r['dur_us']} | {r['waves']} |")
     lines += ["", "Offsets are relative to the step's trunk_fwd start (first step excluded); every wave records"
               " its start / end with s_memrealtime (10 ns), a launch = the union of its waves.", ""]
+    lines += ["First replayed step (launches starting before the second trunk_fwd; us from the first trunk_fwd start):",
+              "", "| kernel | start us | end us |", "|---|---|---|"]
+    lines += [f"| {n} | {a} | {b} |" for a, b, n in span["first_step"]]
+    lines += [""]
     lines += ["- " + c for c in overlap_checks(table)]
     text = "\n".join(lines) + "\n"
     print(text)
