@@ -382,6 +382,15 @@ PYBIND11_MODULE(_C, m) {
 #else
   m.attr("TIMELINE") = false;
 #endif
+  m.def("preload_code_objects", []() {
+    preload_trunk();
+    preload_fc_head();
+    preload_conv_bwd();
+    preload_adadelta();
+    preload_comm();
+    preload_xgmi();
+    preload_f32();
+  }, py::call_guard<py::gil_scoped_release>(), "load every kernel translation unit's code object on the current device");
   m.def("roctx_push", [](const std::string& s) { roctx_push(s.c_str()); });
   m.def("roctx_pop", []() { roctx_pop(); });
 }

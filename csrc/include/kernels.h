@@ -179,6 +179,15 @@ void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStre
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 
+// code-object preload, one per kernel translation unit (hipFuncGetAttributes on one of its kernels)
+void preload_trunk();
+void preload_fc_head();
+void preload_conv_bwd();
+void preload_adadelta();
+void preload_comm();
+void preload_xgmi();
+void preload_f32();
+
 // ---------------- fp32 step (--dtype fp32; f32_net.hip): f32-input MFMA GEMMs + VALU kernels
 struct F32Step {
   // batch source: pre-gathered rows (idx = null, row = step * idx_step_stride + b) or dataset rows

@@ -186,8 +186,12 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
 def _prewarm_body(device) -> None:
     torch.cuda.init()
     torch.empty(1, device=device)            # the context (first allocation on the device)
+    # one 192 MB segment for the caching allocator: the model state, trainer buffers and datasets
+    # are then carved from it instead of each paying a hipMalloc on the main thread
+    torch.empty(192 << 20, dtype=torch.uint8, device=device)
     from .ops import native
-    native.load()                            # the _C extension: gfx950 code objects registered
+    C = native.load()                        # the _C extension: gfx950 code objects registered
+    C.preload_code_objects()                 # ... and loaded (else: at each one's first launch)
 
 
 class _Prewarm:
