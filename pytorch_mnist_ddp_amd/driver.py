@@ -185,6 +185,8 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
 
 def _prewarm_body(device) -> None:
     torch.cuda.init()
+    if device.index is not None:
+        torch.cuda.set_device(device)        # this thread's device (the preload below uses it)
     torch.empty(1, device=device)            # the context (first allocation on the device)
     # one 192 MB segment for the caching allocator: the model state, trainer buffers and datasets
     # are then carved from it instead of each paying a hipMalloc on the main thread
