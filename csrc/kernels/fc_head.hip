@@ -770,16 +770,20 @@ __global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B,
 
 
 
-void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
+void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s) {
+  const int S = fc_bwd_splits(B);
+  if (S <= 1) return;
+  constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;
+  hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
+}
+
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce) {
   const int S = fc_bwd_splits(B);
   if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
   const int grid = S + S * ROLE_A_WGS + fc_bwd_role_b_wgs(B);
   if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
   else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
-  if (S > 1) {
-    constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;
-    hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
-  }
+  if (reduce) launch_fc_grad_reduce(a, B, s);
 }
 
 // profiling aid: one role of fc_bwd on its own (0 = C, 1 = A, 2 = B)

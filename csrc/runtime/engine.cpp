@@ -256,8 +256,11 @@ void Engine::enqueue_step(int batch, bool last) {
   phase_end();
   FcBwdArgs fb{dz1_, p_, pmask_, buf_.w1t, h_bf_, dl_bf_, loss_rows_, buf_.state,
                buf_.grad, dyc_, buf_.loss_log, gscale, 1.0f / (float)B, fcpart_};
+  // B > 1024: the fc split partials are summed on the comm stream, ahead of the fc update /
+  // all-reduce that consumes them, instead of on the compute chain (SERIAL / one-bucket RCCL: here)
+  const bool fc_reduce_side = fc_bwd_splits(B) > 1 && (side || (sched_ == RCCL && two_buckets_));
   phase_begin("bwd_fc");
-  if (M) launch_fc_bwd(fb, B, Bp, compute_);
+  if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side);
   phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
@@ -303,6 +306,7 @@ void Engine::enqueue_step(int batch, bool last) {
     phase_end();
     phase_begin("allreduce_fc+update");
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
     launch_adadelta(ad, ADA_FC, comm_stream_);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
@@ -329,6 +333,7 @@ void Engine::enqueue_step(int batch, bool last) {
   phase_begin("allreduce_fc+update");
   if (S) {
     launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     if (!xg) {
       launch_adadelta(ad, ADA_FC, comm_stream_);
     } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused

@@ -87,6 +87,23 @@ def test_overlap_schedule_bitwise_equals_serial(cuda_device, graph_steps):
     assert lo == ls and co == cs
 
 
+@pytest.mark.parametrize("graph_steps", [0, 2])
+def test_overlap_schedule_large_batch_bitwise_equals_serial(cuda_device, graph_steps):
+    """B > 1024: fc_bwd's split partials are summed on the comm stream (ahead of the fc update) in
+    the OVERLAP schedule, on the compute stream in SERIAL - same bits, same logged losses."""
+    idx = torch.randperm(3000, generator=torch.Generator().manual_seed(9))
+    _, ms_o, to = _trainer(cuda_device, graph_steps=graph_steps, n_train=3000, B=1500, overlap=True)
+    _, ms_s, ts = _trainer(cuda_device, graph_steps=graph_steps, n_train=3000, B=1500, overlap=False)
+    assert to.overlap and not ts.overlap
+    for ep in (1, 2):
+        to.train_epoch(ep, idx)
+        ts.train_epoch(ep, idx)
+    torch.cuda.synchronize()
+    for name in ("param", "square_avg", "acc_delta", "grad", "w1", "w1t", "w2f", "w2d"):
+        assert torch.equal(getattr(ms_o, name), getattr(ms_s, name)), name
+    assert torch.equal(to.loss_log, ts.loss_log)
+
+
 def test_whole_split_eval_bitwise_equals_test_batch_chunks(cuda_device):
     """evaluate() runs the test split as one batch; per-row losses / hits must be bitwise the
     chunked (--test-batch-size 1000) ones."""
