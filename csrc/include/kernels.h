@@ -160,6 +160,10 @@ struct AdadeltaArgs {
   const int* hold_a;
   const int* hold_b;
   int* hold_err;
+  int hold_delta;             // hold until *hold_a >= *hold_b + hold_delta (adadelta_kernel; the
+                              // reduce kernel holds with delta 0)
+  int* signal_start;          // optional: the first workgroup adds 1 at kernel start (the previous
+                              // kernel on the stream has completed: a hand-off without a launch)
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
 void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
@@ -179,6 +183,9 @@ void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const 
 // device-counter stream hand-offs (engine DDP schedule 3)
 void launch_stream_signal(int* ctr, hipStream_t s);
 void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s, double timeout_s = 60.0);
+// signal then wait in one launch (*sig += 1; wait *a >= *b + delta)
+void launch_stream_signal_wait(int* sig, const int* a, const int* b, int delta, int* err, hipStream_t s,
+                               double timeout_s = 60.0);
 // dst[i] = src[i] * s (DDP bucket copy-in with the 1/world_size pre-division)
 void launch_scale_copy(float* dst, const float* src, int64_t n, float s, hipStream_t stream);
 

@@ -107,13 +107,26 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
   Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  bool done = false;
   if (region != ADA_CONV) {
-    if (bid < FC1_TILES) { fc1_tile<UPDATE>(a, ad, bid, ts); return; }
-    bid -= FC1_TILES;
-    if (bid == 0) { elementwise<UPDATE>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1); return; }
-    bid -= 1;
+    if (bid < FC1_TILES) {
+      fc1_tile<UPDATE>(a, ad, bid, ts);
+      done = true;
+    } else {
+      bid -= FC1_TILES;
+      if (bid == 0) {
+        elementwise<UPDATE>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1);
+        done = true;
+      }
+      bid -= 1;
+    }
   }
-  elementwise<UPDATE>(a, ad, OFF_CONV1_W, CONV_N, bid, CONV_WGS);
+  if (!done) elementwise<UPDATE>(a, ad, OFF_CONV1_W, CONV_N, bid, CONV_WGS);
+  // optional completion hold (single-GPU OVERLAP chain: the fc update completes only once the
+  // compute stream's dgrad has started, so conv2's reduce + update follows with no wait launch)
+  if (a.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a.hold_delta,
+                   a.hold_err);
 }
 
 // Single-GPU step tail in ONE launch: the fc-tile / fc-tail updates of adadelta_kernel next to the
@@ -129,6 +142,8 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
   __shared__ float4 red[256];
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (a.signal_start && bid == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   if (!conv_only) {
     const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
     if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }

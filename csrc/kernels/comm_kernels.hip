@@ -64,6 +64,31 @@ __global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* e
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
+// the previous kernel's hand-off signal and the next wait of the same stream in one launch
+__global__ void stream_signal_wait_kernel(int* sig, const int* a, const int* b, int delta, int* err,
+                                          uint64_t timeout_ticks) {
+  TL_SCOPE(TL_WAIT);
+  if (threadIdx.x != 0) return;
+  __hip_atomic_fetch_add(sig, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+void launch_stream_signal_wait(int* sig, const int* a, const int* b, int delta, int* err, hipStream_t s,
+                               double timeout_s) {
+  hipLaunchKernelGGL(stream_signal_wait_kernel, dim3(1), dim3(64), 0, s, sig, a, b, delta, err,
+                     (uint64_t)(timeout_s * 1e8));
+}
+
 void launch_stream_signal(int* ctr, hipStream_t s) {
   hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
 }

@@ -330,19 +330,36 @@ void Engine::enqueue_step(int batch, bool last) {
   phase_begin("bwd_conv_wgrad");
   if (M) launch_conv_wgrad(cbs, B, compute_);
   phase_end();
+  // OVERLAP (not in the traced profiling window, whose phase syncs would deadlock a hold): the comm
+  // chain's hand-offs ride on its update kernels - the fc update holds its completion until dgrad
+  // has started, conv2's reduce + update signals "fc update done" [1] at its start, and its own
+  // "conv2 update done" [3] is signalled by the next step's first comm launch, which then waits for
+  // that step's wgrad: one small launch per step instead of two waits and two signals
+  const bool chain = !xg && !trace_;
   phase_begin("allreduce_fc+update");
   if (S) {
-    launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    if (chain && comm_sig3_pending_)
+      launch_stream_signal_wait(sync_ + 3, sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    else
+      launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+    comm_sig3_pending_ = false;
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     if (!xg) {
-      launch_adadelta(ad, ADA_FC, comm_stream_);
+      AdadeltaArgs af = ad;
+      if (chain) {                              // completes once this step's dgrad has started
+        af.hold_a = sync_ + 4;
+        af.hold_b = sync_ + 3;
+        af.hold_delta = 1;
+        af.hold_err = sync_ + 2;
+      }
+      launch_adadelta(af, ADA_FC, comm_stream_);
     } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
       xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
     }
-    launch_stream_signal(sync_ + 1, comm_stream_);   // fc update of this step done
+    if (!chain) launch_stream_signal(sync_ + 1, comm_stream_);   // fc update of this step done
   }
   phase_end();
   side_pending_ = true;
@@ -372,16 +389,20 @@ void Engine::enqueue_step(int batch, bool last) {
     u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
     cb.w2d = w2d_cur;
     if (S) {
-      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+      if (!chain) launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
       if (xg) {
         XgmiConvPart p2;
         p2.lo = 0;
         p2.hi = RED_W2_PARTS;
         xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, comm_stream_, u2, p2);
       } else {
+        if (chain) u2.signal_start = sync_ + 1;   // the fc update (previous launch) is done
         launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
       }
-      launch_stream_signal(sync_ + 3, comm_stream_);
+      if (chain && !last)
+        comm_sig3_pending_ = true;                // signalled by the next step's first comm launch
+      else
+        launch_stream_signal(sync_ + 3, comm_stream_);
     }
     ConvBwdArgs cbd = cb;
     cbd.signal_ctr = sync_ + 4;
@@ -484,6 +505,7 @@ int Engine::capture_train(int n, int batch, int stride) {
 }
 
 void Engine::reset_host_state() {
+  comm_sig3_pending_ = false;
   enq_main_ = enq_side_ = true;
   skip_join_ = false;
   side_pending_ = false;
@@ -506,6 +528,7 @@ int Engine::capture_train_split(int n, int batch) {
   auto pass = [&](hipStream_t s, bool m, bool side, hipGraph_t* out) {
     side_pending_ = sp;
     w2d_in_alt_ = w2;
+    comm_sig3_pending_ = false;
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;
     enq_side_ = side;

@@ -8,7 +8,8 @@
 //   SERIAL   (single GPU, fallback)  C: trunk, fc1, head, fc_bwd, wgrad, dgrad, reduce+update(all)
 //   OVERLAP  (single GPU, default)   C: trunk(hold [1]>=[0]), fc1, head, fc_bwd, wgrad(+[0]),
 //                                       dgrad(+[4]), conv1 reduce+update(hold [3]>=[4])
-//                                    M: wait [0]: fc update, +[1]; wait [4]: conv2 reduce+update, +[3]
+//                                    M: (+[3] of the previous step) wait [0]: fc update (hold [4]>=[3]+1),
+//                                       conv2 reduce+update (+[1] at start); chunk end: +[3]
 //   RCCL     (DDP over RCCL)         C: trunk, fc1, head, fc_bwd -ev_fc-> wgrad, dgrad, conv reduce,
 //                                       (wait ev_done) all-reduce(conv), update(conv)
 //                                    M: (wait ev_fc) all-reduce(fc), update(fc) -ev_done->
@@ -157,6 +158,7 @@ class Engine {
   bool xgmi_fuse_update_ = true;
   bool side_pending_ = false;       // the previous step's fc update is not joined yet
   bool side_forked_ = false;        // comm stream already ordered after this chunk's start
+  bool comm_sig3_pending_ = false;  // OVERLAP chain: the last conv2 update's [3] signal is owed
   int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
                                     // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch
   bool enq_main_ = true, enq_side_ = true;   // split capture: which stream's pass enqueue_step feeds
