@@ -86,10 +86,11 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
     setup = PhaseTimes(origin=t_start)
     args = cli.parse_args(ddp=ddp_script, argv=argv)
     args._ddp_script = ddp_script
-    # device_count() reads the device list without initialising HIP (is_available() brings the
-    # runtime up: ~60 ms on the main thread inside the timer); the fused engine's HIP init runs on
-    # the prewarm thread instead, under the data build
-    use_cuda = not args.no_cuda and torch.cuda.device_count() > 0
+    # is_available() brings the HIP runtime up (~60 ms) and device_count() initialises amdsmi
+    # (~53 ms, measured under cProfile on the box), both on the main thread inside the timer; the
+    # device nodes tell the same here, and the fused engine's HIP init runs on the prewarm thread
+    # under the data build (a node without a usable GPU then fails there, loudly)
+    use_cuda = not args.no_cuda and gpu_present()
     distributed, world, rank, gpu = False, 1, 0, 0
     args._setup = setup
     setup.mark("args")
@@ -183,6 +184,17 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
     _save(args, model, distributed, rank, ddp_script)
 
 
+def gpu_present() -> bool:
+    """A GPU is visible to this process: the KFD + a DRM render node exist and HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES do not hide every device.  No runtime call."""
+    import glob
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() in ("", "-1"):
+            return False
+    return os.path.exists("/dev/kfd") and bool(glob.glob("/dev/dri/renderD*"))
+
+
 def _prewarm_body(device) -> None:
     torch.cuda.init()
     if device.index is not None:
@@ -191,6 +203,13 @@ def _prewarm_body(device) -> None:
     # one 192 MB segment for the caching allocator: the model state, trainer buffers and datasets
     # are then carved from it instead of each paying a hipMalloc on the main thread
     torch.empty(192 << 20, dtype=torch.uint8, device=device)
+    # torch's own kernels the model state / trainer construction launches (fill for each dtype,
+    # arange): their code objects load at first launch - 81 ms of torch.zeros on the main thread
+    # under cProfile before this
+    for dt in (torch.float32, torch.bfloat16, torch.int32, torch.int64, torch.uint8):
+        torch.zeros(4, dtype=dt, device=device)
+    torch.full((1,), 1.0, device=device)
+    torch.arange(4, dtype=torch.int32, device=device)
     from .ops import native
     C = native.load()                        # the _C extension: gfx950 code objects registered
     C.preload_code_objects()                 # ... and loaded (else: at each one's first launch)

@@ -33,15 +33,17 @@ from .hostcomm import get_hostcomm
 
 
 def init_distributed_mode(args) -> None:
-    # device_count() does not bring the HIP runtime up (is_available() does, ~60 ms)
-    use_cuda = not getattr(args, "no_cuda", False) and torch.cuda.device_count() > 0
+    # no runtime call on the main thread (driver.gpu_present: is_available() / device_count() cost
+    # ~60 / ~53 ms inside the reference timer)
+    from ..driver import gpu_present
+    use_cuda = not getattr(args, "no_cuda", False) and gpu_present()
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
         args.rank = int(os.environ["RANK"])
         args.world_size = int(os.environ["WORLD_SIZE"])
         args.gpu = int(os.environ.get("LOCAL_RANK", "0"))
     elif "SLURM_PROCID" in os.environ:
         args.rank = int(os.environ["SLURM_PROCID"])
-        ndev = torch.cuda.device_count() if use_cuda else 1
+        ndev = torch.cuda.device_count() if use_cuda else 1     # (SLURM launch only)
         args.gpu = args.rank % max(1, ndev)
     elif hasattr(args, "rank"):
         pass
