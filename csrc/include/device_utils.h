@@ -55,6 +55,23 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* row_lo, const uint16_t
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// 16-byte WRITE-THROUGH store (buffer_store_dwordx4 ... sc1): the line leaves this XCD's L2 with
+// the store instead of staying dirty there, so the kernel-end release has nothing of it to write
+// back - a dependent kernel boundary costs ~B / 6 TB/s more when the predecessor leaves B bytes
+// dirty (MI355X_MICROARCH.md 'boundary'; the step's wgrad slabs are 19 MB).  For data only a LATER
+// kernel reads; same cost as a plain 16-B store.
+__device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, u32x4 v) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, floatx4 v) {
+  store_wt16(base, byte_off, __builtin_bit_cast(u32x4, v));
+}
+__device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, uint4 v) {
+  store_wt16(base, byte_off, u32x4{v.x, v.y, v.z, v.w});
+}
+
 // Workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its global
 // loads and stores.  __syncthreads() is a workgroup fence + s_barrier, and the fence drains every
 // outstanding global access (vmcnt(0)) first - a prefetch issued before it lands before anyone

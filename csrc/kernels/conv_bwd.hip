@@ -745,13 +745,13 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
     for (int j = 0; j < 5; ++j)
       if (j < nn) {
         const int tile = (mt0 + i) * 18 + nt0 + j;
-        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = acc[i][j];
+        store_wt16(out, (int64_t)((tile * 64 + lane) * 4) * 4, acc[i][j]);   // slabs: write-through
       }
   // bias: column 0 of the ones-tile accumulators (every column holds the same row sums)
   if (ng == 2 && (lane & 15) == 0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + i) + 4 * (lane >> 4)) = accb[i];
+      store_wt16(out, (int64_t)(18432 + 16 * (mt0 + i) + 4 * (lane >> 4)) * 4, accb[i]);
   }
   WG_MARK(5);
 }
@@ -842,12 +842,12 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
         const floatx4 o = xch[((hw * 2 + i) * 9 + j) * 64 + lane];
         const floatx4 v = {acc[i][j][0] + o[0], acc[i][j][1] + o[1], acc[i][j][2] + o[2], acc[i][j][3] + o[3]};
         const int tile = (mt0 + i) * 18 + nt0 + j;
-        *reinterpret_cast<floatx4*>(out + (tile * 64 + lane) * 4) = v;
+        store_wt16(out, (int64_t)((tile * 64 + lane) * 4) * 4, v);           // slabs: write-through
       }
     if ((lane & 15) == 0) {
       const floatx4 o = xb[hw * 64 + lane];
       const floatx4 v = {mb[0] + o[0], mb[1] + o[1], mb[2] + o[2], mb[3] + o[3]};
-      *reinterpret_cast<floatx4*>(out + 18432 + 16 * (mt0 + bi) + 4 * (lane >> 4)) = v;
+      store_wt16(out, (int64_t)(18432 + 16 * (mt0 + bi) + 4 * (lane >> 4)) * 4, v);
     }
   }
 }

@@ -626,10 +626,9 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
-      if (b0 + bl < B) {
-        uint4* dst = reinterpret_cast<uint4*>(a.dyc + ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC);
-        dst[off] = reinterpret_cast<const uint4*>(recs)[cidx];
-      }
+      if (b0 + bl < B)        // write-through: the conv backward kernels read the records
+        store_wt16(a.dyc, ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC + off * 16,
+                   reinterpret_cast<const uint4*>(recs)[cidx]);
     }
     if (t + 1 < MR) lds_barrier();                     // pms / recs are rewritten by the next tile
   }
