@@ -71,6 +71,7 @@ __device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, f
 __device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, uint4 v) {
   store_wt16(base, byte_off, u32x4{v.x, v.y, v.z, v.w});
 }
+__device__ __forceinline__ floatx4 make_floatx4(const float4& v) { return floatx4{v.x, v.y, v.z, v.w}; }
 
 // Workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its global
 // loads and stores.  __syncthreads() is a workgroup fence + s_barrier, and the fence drains every
