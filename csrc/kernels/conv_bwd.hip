@@ -276,10 +276,15 @@ __device__ __forceinline__ float dgrad_xs_value(float xv) {
 }
 
 // Fixed-order sum of the 4 waves' conv1-gradient partials -> the item's c1part row (256 threads).
+// 80 lanes x 4 consecutive values, the same per-element sum order; 16-B write-through stores (read
+// by the conv reduce kernels only: 42 MB a step at B = 8192 no longer left dirty in L2)
 __device__ __forceinline__ void dgrad_red_reduce(const ConvBwdArgs& a, int strip, int b, const float* red, int ltid) {
-  for (int e = ltid; e < 320; e += 256) {
-    const float s = red[e] + red[e + 320] + red[e + 640] + red[e + 960];
-    a.c1part[((int64_t)b * 4 + strip) * 320 + e] = s;
+  if (ltid < 80) {
+    const float4* r4 = reinterpret_cast<const float4*>(red);
+    const float4 x0 = r4[ltid], x1 = r4[80 + ltid], x2 = r4[160 + ltid], x3 = r4[240 + ltid];
+    const floatx4 s = {x0.x + x1.x + x2.x + x3.x, x0.y + x1.y + x2.y + x3.y, x0.z + x1.z + x2.z + x3.z,
+                       x0.w + x1.w + x2.w + x3.w};
+    store_wt16(a.c1part, (((int64_t)b * 4 + strip) * 320 + 4 * ltid) * 4, s);
   }
 }
 
