@@ -382,6 +382,19 @@ PYBIND11_MODULE(_C, m) {
 #else
   m.attr("TIMELINE") = false;
 #endif
+  m.def("hip_prewarm", [](int device) {
+    // the HIP runtime + this process's context on `device` and every kernel TU's code object, with
+    // the GIL released (the driver's prewarm thread: the main thread keeps building data and model)
+    if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hip_prewarm: hipSetDevice failed");
+    (void)hipFree(nullptr);
+    preload_trunk();
+    preload_fc_head();
+    preload_conv_bwd();
+    preload_adadelta();
+    preload_comm();
+    preload_xgmi();
+    preload_f32();
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("device"));
   m.def("preload_code_objects", []() {
     preload_trunk();
     preload_fc_head();

@@ -94,6 +94,11 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
     distributed, world, rank, gpu = False, 1, 0, 0
     args._setup = setup
     setup.mark("args")
+    # the prewarm thread starts before the process-group init when this rank's device is already
+    # known from the launcher's environment (torchrun: LOCAL_RANK; no launcher: GPU 0)
+    fused = use_cuda and (getattr(args, "engine", None) or "fused") == "fused"
+    early = _early_device(ddp_script) if fused else None
+    args._prewarm = _start_prewarm(early) if early is not None else None
     if ddp_script:
         from .parallel.distributed import init_distributed_mode
         args._defer_set_device = use_cuda and (getattr(args, "engine", None) or "fused") == "fused"
@@ -110,7 +115,11 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
         engine = "module"
     # the HIP context + the native extension's code objects come up on a helper thread while this
     # one builds the data set and the model's CPU init (joined in _run_fused: "hip_init")
-    args._prewarm = _start_prewarm(device) if engine == "fused" else None
+    if args._prewarm is not None and (engine != "fused" or args._prewarm.device != device):
+        args._prewarm.join()                 # (a device guess that did not hold: start over)
+        args._prewarm = None
+    if args._prewarm is None and engine == "fused":
+        args._prewarm = _start_prewarm(device)
     # the fused engine's RCCL communicator initialises on a helper thread while data, model and
     # trainer are built (its bootstrap is the largest N > 1 startup cost inside the timer)
     args._pending_comm = None
@@ -195,14 +204,33 @@ def gpu_present() -> bool:
     return os.path.exists("/dev/kfd") and bool(glob.glob("/dev/dri/renderD*"))
 
 
-def _prewarm_body(device) -> None:
+def _prewarm_body(device, steps: dict | None = None) -> None:
+    """HIP runtime + context, code objects, torch's CUDA state, an allocator segment and the torch
+    kernels the model state / trainer construction use - everything the main thread would otherwise
+    pay on first touch inside the reference timer.  The native step runs with the GIL released."""
+    steps = {} if steps is None else steps
+    t = time.perf_counter()
+
+    def lap(name):
+        nonlocal t
+        now = time.perf_counter()
+        steps[name] = round(now - t, 4)
+        t = now
+
+    from .ops import native
+    C = native.load()                        # the _C extension (dlopen; no device work)
+    lap("native_load")
+    C.hip_prewarm(device.index if device.index is not None else torch.cuda.current_device())
+    lap("hip_runtime_context_code_objects")  # (GIL released: overlaps the main thread)
     torch.cuda.init()
     if device.index is not None:
-        torch.cuda.set_device(device)        # this thread's device (the preload below uses it)
-    torch.empty(1, device=device)            # the context (first allocation on the device)
+        torch.cuda.set_device(device)        # this thread's device
+    torch.empty(1, device=device)
+    lap("torch_cuda_init")
     # one 192 MB segment for the caching allocator: the model state, trainer buffers and datasets
     # are then carved from it instead of each paying a hipMalloc on the main thread
     torch.empty(192 << 20, dtype=torch.uint8, device=device)
+    lap("allocator_segment")
     # torch's own kernels the model state / trainer construction launches (fill for each dtype,
     # arange): their code objects load at first launch - 81 ms of torch.zeros on the main thread
     # under cProfile before this
@@ -210,22 +238,20 @@ def _prewarm_body(device) -> None:
         torch.zeros(4, dtype=dt, device=device)
     torch.full((1,), 1.0, device=device)
     torch.arange(4, dtype=torch.int32, device=device)
-    from .ops import native
-    C = native.load()                        # the _C extension: gfx950 code objects registered
-    C.preload_code_objects()                 # ... and loaded (else: at each one's first launch)
+    lap("torch_kernels")
 
 
 class _Prewarm:
     def __init__(self, device):
         import threading
-        self.device, self.error, self.seconds = device, None, None
+        self.device, self.error, self.seconds, self.steps = device, None, None, {}
         self._t = threading.Thread(target=self._run, name="hip-prewarm", daemon=True)
         self._t.start()
 
     def _run(self):
         t0 = time.perf_counter()
         try:
-            _prewarm_body(self.device)
+            _prewarm_body(self.device, self.steps)
         except BaseException as e:  # noqa: BLE001 - re-raised by the joining thread
             self.error = e
         self.seconds = time.perf_counter() - t0
@@ -236,6 +262,21 @@ class _Prewarm:
 
 def _start_prewarm(device):
     return _Prewarm(device)
+
+
+def _early_device(ddp_script: bool):
+    """This rank's device before init_distributed_mode, where the environment already fixes it:
+    mnist.py -> cuda (current device); mnist_ddp.py under torchrun -> cuda:LOCAL_RANK (cuda:0 with
+    MNIST_AMD_ONE_GPU=1); without a launcher -> cuda:0; SLURM (rank from the job) -> unknown."""
+    if not ddp_script:
+        return torch.device("cuda")
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        if os.environ.get("MNIST_AMD_ONE_GPU", "0") == "1":
+            return torch.device("cuda:0")
+        return torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}")
+    if "SLURM_PROCID" in os.environ:
+        return None
+    return torch.device("cuda:0")
 
 
 def _run_fused(args, model, device, train_data, test_data, train_stream, test_stream, distributed, world, rank,
@@ -249,6 +290,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         if pw is not None:
             pw.join()
             setup.add_info("prewarm_thread_s", pw.seconds)
+            setup.add_info("prewarm_steps_s", pw.steps)
             if pw.error is not None:
                 raise pw.error
         else:

@@ -54,7 +54,7 @@ class PhaseTimes:
 
     def __init__(self, origin: float | None = None):
         self.s: dict[str, float] = {}
-        self.info: dict[str, float] = {}   # seconds spent off the critical path (helper threads)
+        self.info: dict = {}   # seconds spent off the critical path (helper threads; sub-step dicts)
         # wall-clock marks in seconds since `origin` (time.time() of the reference timer's start):
         # where the non-phase time goes (epochs, evaluation, teardown)
         self.origin = time.time() if origin is None else origin
@@ -74,8 +74,11 @@ class PhaseTimes:
     def add(self, name: str, seconds: float) -> None:
         self.s[name] = self.s.get(name, 0.0) + seconds
 
-    def add_info(self, name: str, seconds: float | None) -> None:
-        if seconds is not None:
+    def add_info(self, name: str, seconds) -> None:
+        """seconds: a number, or a dict of sub-step seconds (kept as is)"""
+        if isinstance(seconds, dict):
+            self.info[name] = dict(seconds)
+        elif seconds is not None:
             self.info[name] = round(float(seconds), 4)
 
     def update(self, other: "PhaseTimes | dict", prefix: str = "") -> None:

@@ -70,7 +70,7 @@ def test_pipelined_epochs_keep_reference_print_and_rng_order(monkeypatch, capsys
     monkeypatch.setattr("pytorch_mnist_ddp_amd.engine.trainer.FusedTrainer", lambda *a, **k: fake)
     monkeypatch.setattr("pytorch_mnist_ddp_amd.engine.state.ModelState",
                         lambda model, device, lr=1.0: types.SimpleNamespace(param=torch.zeros(1)))
-    args = types.SimpleNamespace(_setup=PhaseTimes(), _prewarm=types.SimpleNamespace(join=lambda: None, seconds=0.0,
+    args = types.SimpleNamespace(_setup=PhaseTimes(), _prewarm=types.SimpleNamespace(join=lambda: None, seconds=0.0, steps={},
                                                                                     error=None),
                                  lr=1.0, gamma=0.7, allreduce="auto", graph_steps=None, log_interval=10,
                                  batch_size=2, test_batch_size=10, profile=False, profile_steps=0, epochs=3,
