@@ -3,6 +3,7 @@
 // (torch.cuda.Stream.cuda_stream): the runtime never includes libtorch headers, so it is immune
 // to torch C++ ABI details and compiles in seconds.
 #include <pybind11/pybind11.h>
+#include <chrono>
 #include <pybind11/stl.h>
 
 #include <stdexcept>
@@ -385,8 +386,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("hip_prewarm", [](int device) {
     // the HIP runtime + this process's context on `device` and every kernel TU's code object, with
     // the GIL released (the driver's prewarm thread: the main thread keeps building data and model)
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hip_prewarm: hipSetDevice failed");
     (void)hipFree(nullptr);
+    const auto t1 = clk::now();
     preload_trunk();
     preload_fc_head();
     preload_conv_bwd();
@@ -394,7 +398,15 @@ PYBIND11_MODULE(_C, m) {
     preload_comm();
     preload_xgmi();
     preload_f32();
+    const auto t2 = clk::now();
+    return std::make_pair(std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
   }, py::call_guard<py::gil_scoped_release>(), py::arg("device"));
+  m.def("memset_sync", [](uintptr_t ptr, int value, int64_t nbytes) {
+    // setup-time buffer initialisation without a torch fill kernel (whose code object would load on
+    // first launch inside the reference timer); synchronous
+    if (nbytes > 0 && hipMemset(reinterpret_cast<void*>(ptr), value, (size_t)nbytes) != hipSuccess)
+      throw std::runtime_error("memset_sync: hipMemset failed");
+  }, py::call_guard<py::gil_scoped_release>());
   m.def("preload_code_objects", []() {
     preload_trunk();
     preload_fc_head();

@@ -220,25 +220,22 @@ def _prewarm_body(device, steps: dict | None = None) -> None:
     from .ops import native
     C = native.load()                        # the _C extension (dlopen; no device work)
     lap("native_load")
-    C.hip_prewarm(device.index if device.index is not None else torch.cuda.current_device())
-    lap("hip_runtime_context_code_objects")  # (GIL released: overlaps the main thread)
+    # GIL released: the HIP runtime + context, then every kernel TU's code object
+    t_rt, t_co = C.hip_prewarm(device.index if device.index is not None else 0)
+    steps["hip_runtime_context"], steps["code_objects"] = round(t_rt, 4), round(t_co, 4)
+    lap("hip_prewarm_total")
     torch.cuda.init()
+    lap("torch_cuda_init")
     if device.index is not None:
         torch.cuda.set_device(device)        # this thread's device
     torch.empty(1, device=device)
-    lap("torch_cuda_init")
+    lap("torch_first_alloc")
     # one 192 MB segment for the caching allocator: the model state, trainer buffers and datasets
-    # are then carved from it instead of each paying a hipMalloc on the main thread
+    # are then carved from it instead of each paying a hipMalloc on the main thread.  (The setup
+    # paths launch no torch kernels at all - native.zeros / H2D copies - so no torch code object
+    # has to load inside the timer.)
     torch.empty(192 << 20, dtype=torch.uint8, device=device)
     lap("allocator_segment")
-    # torch's own kernels the model state / trainer construction launches (fill for each dtype,
-    # arange): their code objects load at first launch - 81 ms of torch.zeros on the main thread
-    # under cProfile before this
-    for dt in (torch.float32, torch.bfloat16, torch.int32, torch.int64, torch.uint8):
-        torch.zeros(4, dtype=dt, device=device)
-    torch.full((1,), 1.0, device=device)
-    torch.arange(4, dtype=torch.int32, device=device)
-    lap("torch_kernels")
 
 
 class _Prewarm:

@@ -138,18 +138,19 @@ class FusedTrainer:
         # ---- device-resident data
         self.train_u8 = train.images.reshape(len(train), -1).contiguous().to(dev)
         self.train_labels = train.targets.to(torch.int32).to(dev)
-        self.train_idx = torch.zeros(self.steps_per_epoch * self.B, dtype=torch.int32, device=dev)
+        z = native.zeros                                     # hipMemset: no torch fill kernel
+        self.train_idx = z(self.steps_per_epoch * self.B, torch.int32, dev)
         # device-side DataLoader: each epoch's rows pre-gathered in sampler order (Engine::gather_rows)
         self.epoch_u8 = torch.empty(self.steps_per_epoch * self.B, 784, dtype=torch.uint8, device=dev)
-        self.epoch_labels = torch.zeros(self.steps_per_epoch * self.B, dtype=torch.int32, device=dev)
-        self.loss_log = torch.zeros(max(self.steps_per_epoch, 1), dtype=torch.float32, device=dev)
+        self.epoch_labels = z(self.steps_per_epoch * self.B, torch.int32, dev)
+        self.loss_log = z(max(self.steps_per_epoch, 1), torch.float32, dev)
         self.n_test = len(test) if test is not None else 0
         if test is not None:
             self.test_u8 = test.images.reshape(self.n_test, -1).contiguous().to(dev)
             self.test_labels = test.targets.to(torch.int32).to(dev)
-            self.test_idx = torch.arange(self.n_test, dtype=torch.int32, device=dev)
-            self.test_loss_rows = torch.zeros(self.n_test, dtype=torch.float32, device=dev)
-            self.test_correct = torch.zeros(self.n_test, dtype=torch.int32, device=dev)
+            self.test_idx = torch.arange(self.n_test, dtype=torch.int32).to(dev)
+            self.test_loss_rows = z(self.n_test, torch.float32, dev)
+            self.test_correct = z(self.n_test, torch.int32, dev)
             # pinned landing buffers of the per-epoch evaluation read-back (allocated once: a pinned
             # allocation is a driver call inside every epoch of the reference's timer otherwise)
             self._eval_rows_h = torch.empty(self.n_test, dtype=torch.float32, pin_memory=True)
@@ -451,8 +452,10 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------ helpers
     def set_lr(self, lr: float) -> None:
+        # an H2D copy on the compute stream (stream-ordered with the epochs around it; the pageable
+        # source is staged before copy_ returns), not a fill kernel
         with torch.cuda.stream(self.compute):
-            self.ms.lr.fill_(float(lr))
+            self.ms.lr.copy_(torch.tensor([float(lr)], dtype=torch.float32))
 
     def _graph(self, n: int, batch: int) -> int:
         key = (n, batch)

@@ -71,3 +71,21 @@ def stream_handle(stream: "torch.cuda.Stream | None" = None) -> int:
 
 def ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else int(t.data_ptr())
+
+
+def zeros(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    """A zero-filled tensor; on the GPU by hipMemset instead of a torch fill kernel, whose code
+    object would otherwise load at first launch inside the reference timer (setup-time only:
+    synchronous)."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if t.is_cuda:
+        load().memset_sync(t.data_ptr(), 0, t.numel() * t.element_size())
+    else:
+        t.zero_()
+    return t
+
+
+def host_to_device(values, dtype: torch.dtype, device) -> torch.Tensor:
+    """A small device tensor from host values by one H2D copy (no device kernel)."""
+    return torch.tensor(values, dtype=dtype).to(device)
+
