@@ -72,6 +72,15 @@ __device__ __forceinline__ void store_wt16(const void* base, int64_t byte_off, u
   store_wt16(base, byte_off, u32x4{v.x, v.y, v.z, v.w});
 }
 __device__ __forceinline__ floatx4 make_floatx4(const float4& v) { return floatx4{v.x, v.y, v.z, v.w}; }
+// write-through only where it pays: small batches, whose kernels are short enough that the
+// kernel-end write-back of their dirty lines shows up as a gap (B = 200: 600 steps 70.2 -> 67.8
+// us/step); at B = 8192 the write-through stores cost more than the write-back they save (0.930 ->
+// 0.952 ms/step, same box: profiles/r4/ab/), so large batches keep plain stores
+template <class T>
+__device__ __forceinline__ void store16(bool wt, const void* base, int64_t byte_off, T v) {
+  if (wt) store_wt16(base, byte_off, v);
+  else *reinterpret_cast<T*>(static_cast<char*>(const_cast<void*>(base)) + byte_off) = v;
+}
 
 // Workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its global
 // loads and stores.  __syncthreads() is a workgroup fence + s_barrier, and the fence drains every

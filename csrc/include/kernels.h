@@ -7,6 +7,9 @@
 
 namespace mnist {
 
+// write-through (sc1) stores for batches up to this size (device_utils.h store16)
+constexpr int WT_MAX_B = 1024;
+
 // ---------------- forward ----------------
 struct TrunkFwdArgs {
   const uint8_t* data_u8;     // [N][784] raw dataset, HBM resident
@@ -160,6 +163,7 @@ struct AdadeltaArgs {
   const int* hold_a;
   const int* hold_b;
   int* hold_err;
+  int wt;                     // write-through parameter / state / shadow stores (engine: B <= WT_MAX_B)
   int hold_delta;             // hold until *hold_a >= *hold_b + hold_delta (adadelta_kernel; the
                               // reduce kernel holds with delta 0)
   int* signal_start;          // optional: the first workgroup adds 1 at kernel start (the previous

@@ -43,9 +43,9 @@ __device__ __forceinline__ void elementwise(const AdadeltaArgs& a, const Ada& ad
       ad.step(p.y, g.y, sq.y, ac.y);
       ad.step(p.z, g.z, sq.z, ac.z);
       ad.step(p.w, g.w, sq.w, ac.w);
-      store_wt16(a.param, e * 4, make_floatx4(p));        // write-through: read by later kernels
-      store_wt16(a.square_avg, e * 4, make_floatx4(sq));
-      store_wt16(a.acc_delta, e * 4, make_floatx4(ac));
+      store16(a.wt, a.param, e * 4, make_floatx4(p));        // write-through: read by later kernels
+      store16(a.wt, a.square_avg, e * 4, make_floatx4(sq));
+      store16(a.wt, a.acc_delta, e * 4, make_floatx4(ac));
     }
     if (e + 3 >= OFF_CONV2_W && e < OFF_CONV2_W + C2 * C1 * 9) {
       conv2_shadow(a, e, p.x);
@@ -82,20 +82,20 @@ __device__ __forceinline__ void fc1_tile(const AdadeltaArgs& a, const Ada& ad, i
       ad.step(p[j].y, g[j].y, sq[j].y, ac[j].y);
       ad.step(p[j].z, g[j].z, sq[j].z, ac[j].z);
       ad.step(p[j].w, g[j].w, sq[j].w, ac[j].w);
-      store_wt16(a.param, (e0 + 4 * j) * 4, make_floatx4(p[j]));   // write-through (later kernels)
-      store_wt16(a.square_avg, (e0 + 4 * j) * 4, make_floatx4(sq[j]));
-      store_wt16(a.acc_delta, (e0 + 4 * j) * 4, make_floatx4(ac[j]));
+      store16(a.wt, a.param, (e0 + 4 * j) * 4, make_floatx4(p[j]));   // write-through (later kernels)
+      store16(a.wt, a.square_avg, (e0 + 4 * j) * 4, make_floatx4(sq[j]));
+      store16(a.wt, a.acc_delta, (e0 + 4 * j) * 4, make_floatx4(ac[j]));
     }
     v[4 * j] = p[j].x; v[4 * j + 1] = p[j].y; v[4 * j + 2] = p[j].z; v[4 * j + 3] = p[j].w;
   }
   uint4 lo;
   lo.x = pack2bf(v[0], v[1]); lo.y = pack2bf(v[2], v[3]); lo.z = pack2bf(v[4], v[5]); lo.w = pack2bf(v[6], v[7]);
-  store_wt16(a.w1, ((int64_t)o * NFLAT + i0 + ic) * 2, lo);
+  store16(a.wt, a.w1, ((int64_t)o * NFLAT + i0 + ic) * 2, lo);
 #pragma unroll
   for (int j = 0; j < 8; ++j) ts[(ic + j) * TS + ol] = f2bf(v[j]);
   __syncthreads();
   const int il = t >> 3, oc = (t & 7) * 8;
-  store_wt16(a.w1t, ((int64_t)(i0 + il) * NH + 64 * ot + oc) * 2, *reinterpret_cast<const uint4*>(ts + il * TS + oc));
+  store16(a.wt, a.w1t, ((int64_t)(i0 + il) * NH + 64 * ot + oc) * 2, *reinterpret_cast<const uint4*>(ts + il * TS + oc));
 }
 }  // namespace
 

@@ -278,13 +278,14 @@ __device__ __forceinline__ float dgrad_xs_value(float xv) {
 // Fixed-order sum of the 4 waves' conv1-gradient partials -> the item's c1part row (256 threads).
 // 80 lanes x 4 consecutive values, the same per-element sum order; 16-B write-through stores (read
 // by the conv reduce kernels only: 42 MB a step at B = 8192 no longer left dirty in L2)
-__device__ __forceinline__ void dgrad_red_reduce(const ConvBwdArgs& a, int strip, int b, const float* red, int ltid) {
+__device__ __forceinline__ void dgrad_red_reduce(const ConvBwdArgs& a, int strip, int b, const float* red, int ltid,
+                                                 bool wt) {
   if (ltid < 80) {
     const float4* r4 = reinterpret_cast<const float4*>(red);
     const float4 x0 = r4[ltid], x1 = r4[80 + ltid], x2 = r4[160 + ltid], x3 = r4[240 + ltid];
     const floatx4 s = {x0.x + x1.x + x2.x + x3.x, x0.y + x1.y + x2.y + x3.y, x0.z + x1.z + x2.z + x3.z,
                        x0.w + x1.w + x2.w + x3.w};
-    store_wt16(a.c1part, (((int64_t)b * 4 + strip) * 320 + 4 * ltid) * 4, s);
+    store16(wt, a.c1part, (((int64_t)b * 4 + strip) * 320 + 4 * ltid) * 4, s);
   }
 }
 
@@ -434,7 +435,7 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
     }
   if constexpr (!STAG) {
     lds_barrier();
-    dgrad_red_reduce(a, strip, b, red, tid);
+    dgrad_red_reduce(a, strip, b, red, tid, a.c1_rows <= 4 * WT_MAX_B);   // (c1_rows = 4B)
   }
 }
 
@@ -750,13 +751,13 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
     for (int j = 0; j < 5; ++j)
       if (j < nn) {
         const int tile = (mt0 + i) * 18 + nt0 + j;
-        store_wt16(out, (int64_t)((tile * 64 + lane) * 4) * 4, acc[i][j]);   // slabs: write-through
+        store16(B <= WT_MAX_B, out, (int64_t)((tile * 64 + lane) * 4) * 4, acc[i][j]);   // slabs
       }
   // bias: column 0 of the ones-tile accumulators (every column holds the same row sums)
   if (ng == 2 && (lane & 15) == 0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      store_wt16(out, (int64_t)(18432 + 16 * (mt0 + i) + 4 * (lane >> 4)) * 4, accb[i]);
+      store16(B <= WT_MAX_B, out, (int64_t)(18432 + 16 * (mt0 + i) + 4 * (lane >> 4)) * 4, accb[i]);
   }
   WG_MARK(5);
 }
@@ -847,12 +848,12 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
         const floatx4 o = xch[((hw * 2 + i) * 9 + j) * 64 + lane];
         const floatx4 v = {acc[i][j][0] + o[0], acc[i][j][1] + o[1], acc[i][j][2] + o[2], acc[i][j][3] + o[3]};
         const int tile = (mt0 + i) * 18 + nt0 + j;
-        store_wt16(out, (int64_t)((tile * 64 + lane) * 4) * 4, v);           // slabs: write-through
+        store16(B <= WT_MAX_B, out, (int64_t)((tile * 64 + lane) * 4) * 4, v);   // slabs
       }
     if ((lane & 15) == 0) {
       const floatx4 o = xb[hw * 64 + lane];
       const floatx4 v = {mb[0] + o[0], mb[1] + o[1], mb[2] + o[2], mb[3] + o[3]};
-      store_wt16(out, (int64_t)(18432 + 16 * (mt0 + bi) + 4 * (lane >> 4)) * 4, v);
+      store16(B <= WT_MAX_B, out, (int64_t)(18432 + 16 * (mt0 + bi) + 4 * (lane >> 4)) * 4, v);
     }
   }
 }

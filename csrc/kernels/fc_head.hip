@@ -627,7 +627,7 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
     for (int k = 0; k < 3; ++k) {
       const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
       if (b0 + bl < B)        // write-through: the conv backward kernels read the records
-        store_wt16(a.dyc, ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC + off * 16,
+        store16(B <= WT_MAX_B, a.dyc, ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC + off * 16,
                    reinterpret_cast<const uint4*>(recs)[cidx]);
     }
     if (t + 1 < MR) lds_barrier();                     // pms / recs are rewritten by the next tile

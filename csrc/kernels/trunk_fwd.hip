@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
         const int grow = strip0 * STRIP + r;
         // write-through: the a1 copy is read by the backward kernels only (no dirty L2 lines for
         // the kernel-end release to write back)
-        store_wt16(a.a1_out, ((((int64_t)b * H1 + grow) * H1 + col) * C1 + c * 8) * 2, v);
+        store16((int)gridDim.y <= WT_MAX_B, a.a1_out, ((((int64_t)b * H1 + grow) * H1 + col) * C1 + c * 8) * 2, v);
       }
     }
   }
@@ -337,8 +337,8 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
     s1.x = pack2bf(o[8], o[9]);   s1.y = pack2bf(o[10], o[11]);
     s1.z = pack2bf(o[12], o[13]); s1.w = pack2bf(o[14], o[15]);
     const int64_t pb = ((int64_t)b * NFLAT + flat) * 2;           // write-through (read by later kernels)
-    store_wt16(a.p_out, pb, s0);
-    store_wt16(a.p_out, pb + 16, s1);
+    store16((int)gridDim.y <= WT_MAX_B, a.p_out, pb, s0);
+    store16((int)gridDim.y <= WT_MAX_B, a.p_out, pb + 16, s1);
   }
   PHASE_MARK(6);
   // DDP schedule 3: the kernel completes only once the comm stream's fc update of the previous step

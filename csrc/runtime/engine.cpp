@@ -265,6 +265,7 @@ void Engine::enqueue_step(int batch, bool last) {
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+  ad.wt = B <= WT_MAX_B;                          // write-through stores at small batches (store16)
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
