@@ -107,7 +107,14 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
         distributed = args.distributed
         if distributed:
             world, rank, gpu = args.world_size, args.rank, args.gpu
-    torch.manual_seed(args.seed)
+    if fused:
+        # the CPU generator only (model init, samplers, loader seeds: the reference's draws); the
+        # fused engine never uses torch's GPU RNG (dropout is in-kernel Philox), and a queued
+        # torch.cuda.manual_seed_all would make torch's CUDA init count devices through amdsmi
+        # (~53 ms on the prewarm thread, the startup's critical path)
+        torch.default_generator.manual_seed(args.seed)
+    else:
+        torch.manual_seed(args.seed)
     device = torch.device(f"cuda:{gpu}" if use_cuda else "cpu") if ddp_script else \
         torch.device("cuda" if use_cuda else "cpu")
     engine = getattr(args, "engine", None) or ("fused" if use_cuda else "module")
