@@ -157,33 +157,16 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
     spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hold_err);
 }
 
-// conv-bucket parts on their own (single-GPU OVERLAP: conv2's part on the comm stream, conv1's on
-// compute).  At most 80 VGPRs and 4 KB of LDS so a workgroup fits beside the persistent dgrad's two
-// resident workgroups per CU (2 x 70 KB LDS, 2 waves/SIMD x 216 VGPRs): conv2's part then runs under
-// conv2_dgrad from its start instead of waiting for dgrad workgroups to retire (in-kernel timeline:
-// it started 7.6 us into dgrad's 12.3 with the 98-VGPR combined kernel).
-__global__ __launch_bounds__(256, 6) void adadelta_conv_parts_kernel(AdadeltaArgs a, ConvBwdArgs c, int B, int bid0) {
-  TL_SCOPE(TL_RED_CONV2);
-  __shared__ float4 red[256];
-  if (a.state_inc && blockIdx.x == 0 && threadIdx.x == 0) a.state_inc->step += 1;
-  if (a.signal_start && blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  conv_reduce_update<8>(a, c, B, blockIdx.x + bid0, red);
-  if (a.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-    spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a.hold_delta,
-                   a.hold_err);
-}
-
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
   hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(FC1_TILES + 1 + RED_WGS), dim3(256), 0, s, a, c, B, 0, 0);
 }
 
 void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s) {
   if (lo < 0 || hi > RED_WGS || lo >= hi) throw std::runtime_error("adadelta_reduce: bad part range");
-  if (hi <= RED_W2_WGS)     // conv2 parts: the 80-VGPR kernel that fits beside dgrad
-    hipLaunchKernelGGL(adadelta_conv_parts_kernel, dim3(hi - lo), dim3(256), 0, s, a, c, B, lo);
-  else
-    hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(hi - lo), dim3(256), 0, s, a, c, B, 1, lo);
+  // (a 60-VGPR conv2-part kernel that fits beside the persistent dgrad's resident workgroups and so
+  // runs under dgrad from its start measured slower than this one, which waits for dgrad's
+  // one-item workgroups to retire: 600 steps 68.2-68.7 vs 67.1-67.8 us/step, same box)
+  hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(hi - lo), dim3(256), 0, s, a, c, B, 1, lo);
 }
 
 static int adadelta_grid(int region) {

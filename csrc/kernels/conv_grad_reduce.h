@@ -47,13 +47,9 @@ __device__ __forceinline__ int64_t conv_sink_index(int bid, int tid, int r) {
 // sum, as before) and issued before `pre()` - the caller's own loads (e.g. the optimizer state the
 // sink updates) - so the sums wait for the slabs alone: a branch-guarded load would end in vmcnt(0)
 // and split the kernel into dependent round trips.
-// NV: slab loads in flight per thread on the conv2 columns (16 = one round; 8 = two rounds in the
-// same summation order, bitwise equal, 32 fewer VGPRs: the 80-VGPR conv2 part beside dgrad)
-// (NV = 8 serves the conv2 parts only: the conv1 branch is compiled out)
-template <int NV = 16, class Pre, class Sink>
+template <class Pre, class Sink>
 __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Pre&& pre,
                                                   Sink&& sink) {
-  static_assert(NV == 16 || NV == 8, "loads in flight");
   const int tid = threadIdx.x;
   const float sc = a.grad_scale;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -62,23 +58,19 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
     const int col = bid * 16 + (tid & 15), sl = tid >> 4;          // float4 column, slab slice
     const float4* src = reinterpret_cast<const float4*>(a.w2part) + col;
     constexpr int S4 = W2PART_STRIDE / 4;
-    float4 t = z4;
+    float4 v[16];
 #pragma unroll
-    for (int h = 0; h < 16 / NV; ++h) {
-      float4 v[NV];
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int g = sl + 16 * (h * NV + k);
-        v[k] = src[(int64_t)(g < G ? g : 0) * S4];
-      }
-      if (h == 0 && NV == 16) pre();      // (NV = 8: after the tree, fewer live registers)
-#pragma unroll
-      for (int k = 0; k < NV; ++k)
-        if (sl + 16 * (h * NV + k) >= G) v[k] = z4;
-      if (h == 0) t = v[0];
-#pragma unroll
-      for (int k = (h == 0 ? 1 : 0); k < NV; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+    for (int k = 0; k < 16; ++k) {
+      const int g = sl + 16 * k;
+      v[k] = src[(int64_t)(g < G ? g : 0) * S4];
     }
+    pre();
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (sl + 16 * k >= G) v[k] = z4;
+    float4 t = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
     for (int g = sl + 256; g < G; g += 16) {          // G > 256 never happens today; kept general
       const float4 u = src[(int64_t)g * S4];
       t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
@@ -94,13 +86,12 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
       }
       __syncthreads();
     }
-    if (NV != 16) pre();
     if (sl == 0 && 4 * col < 18432 + C2) {
       const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
 #pragma unroll
       for (int r = 0; r < 4; ++r) sink(conv_sink_index(bid, tid, r), o[r]);
     }
-  } else if constexpr (NV == 16) {
+  } else {
     const int col = (bid - RED_W2_WGS) * 4 + (tid & 3), sl = tid >> 2;   // 80 float4 columns, 64 slices
     const int nslab = a.c1red ? C1_PRE_SLABS : a.c1_rows;
     const float4* src = reinterpret_cast<const float4*>(a.c1red ? a.c1red : a.c1part) + col;
@@ -143,7 +134,7 @@ __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, i
 
 template <class Sink>
 __device__ __forceinline__ void reduce_conv_grads(const ConvBwdArgs& a, int B, int bid, float4* red, Sink&& sink) {
-  reduce_conv_grads<16>(a, B, bid, red, [] {}, sink);
+  reduce_conv_grads(a, B, bid, red, [] {}, sink);
 }
 
 // bf16 shadows of one updated conv2.weight element: forward layout w2f [co][tap][ci] and dgrad
@@ -160,7 +151,6 @@ __device__ __forceinline__ void conv2_shadow(const AdadeltaArgs& a, int64_t e, f
 // Reduce part `bid` of the conv gradients and apply the Adadelta step to each finished element
 // (grad buffer, param, optimizer state, bf16 shadows).  The optimizer state of the <= 4 elements a
 // lane sinks is loaded before (and in flight with) the slab loads.
-template <int NV = 16>
 __device__ __forceinline__ void conv_reduce_update(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int bid,
                                                    float4* red) {
   float* gbuf = c.grad;
@@ -177,7 +167,7 @@ __device__ __forceinline__ void conv_reduce_update(const AdadeltaArgs& a, const 
     lr = *a.lr;
   };
   int k = 0;
-  reduce_conv_grads<NV>(c, B, bid, red, pre, [&](int64_t e, float g) {
+  reduce_conv_grads(c, B, bid, red, pre, [&](int64_t e, float g) {
     const Ada ad{a.rho, a.eps, a.weight_decay, lr};
     gbuf[e] = g;                        // the flat gradient buffer stays complete (p.grad views)
     float p = pp[k], sq = ps[k], acc = pa[k];
