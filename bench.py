@@ -106,6 +106,9 @@ def run_reference_script(world: int, batch: int, epochs: int, timeout: float = 9
         try:
             recs = [json.loads(ln) for ln in open(jlog) if ln.strip()]
             setups = [rc["setup_s"] for rc in recs if "setup_s" in rc]
+            infos = [rc["setup_info"] for rc in recs if rc.get("setup_info")]
+            if infos:                # helper-thread timings (prewarm steps, RCCL init) of the first rank logged
+                out["setup_info"] = infos[0]
             if setups:
                 keys = list(dict.fromkeys(k for st in setups for k in st))
                 out["setup_phases_s"] = {k: round(max(st.get(k, 0.0) for st in setups), 3) for k in keys}
