@@ -2,7 +2,6 @@
 #include "host_logic.h"
 
 #include <algorithm>
-#include <chrono>
 #include <stdexcept>
 #include <string>
 
@@ -28,7 +27,6 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-  if (const char* v = getenv("MNIST_AMD_SIDE_SPIN_US")) side_spin_us_ = atoi(v);   // A/B (temporary)
   alloc_workspace();
   if (f32_) alloc_workspace_f32();
 }
@@ -571,20 +569,9 @@ int Engine::capture_train_split(int n, int batch) {
 void Engine::side_worker() {
   std::unique_lock<std::mutex> lk(side_mu_);
   for (;;) {
-    if (side_spin_us_ > 0 && !side_stop_ && side_job_ == nullptr) {
-      // poll (no lock, no futex) for a while after the last job: the next replay's side launch then
-      // starts within a microsecond instead of after a thread wake-up
-      lk.unlock();
-      const auto t0 = std::chrono::steady_clock::now();
-      while (!side_flag_.load(std::memory_order_acquire) &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(side_spin_us_)) {
-      }
-      lk.lock();
-    }
     side_cv_.wait(lk, [this] { return side_stop_ || side_job_ != nullptr; });
     if (side_stop_) return;
     hipGraphExec_t job = side_job_;
-    side_flag_.store(false, std::memory_order_relaxed);
     lk.unlock();
     hipError_t e = hipGraphLaunch(job, comm_stream_);
     if (e == hipSuccess) e = hipEventRecord(ev_join_, comm_stream_);
@@ -617,7 +604,6 @@ void Engine::replay(int id) {
     if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
     side_job_ = side;
     side_done_ = false;
-    side_flag_.store(true, std::memory_order_release);
   }
   side_cv_.notify_all();
   const hipError_t em = hipGraphLaunch(graphs_[id], compute_);

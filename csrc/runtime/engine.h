@@ -25,7 +25,6 @@
 #include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <atomic>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -170,8 +169,6 @@ class Engine {
   std::condition_variable side_cv_;
   hipGraphExec_t side_job_ = nullptr;
   bool side_done_ = false, side_stop_ = false;
-  std::atomic<bool> side_flag_{false};        // a side job is posted (polled by the spinning worker)
-  int side_spin_us_ = 0;                      // worker polls this long after a job before sleeping
   hipError_t side_err_ = hipSuccess;
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
   void phase_begin(const char* name);
