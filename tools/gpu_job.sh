@@ -14,6 +14,7 @@
 #   ddpeq W B                  tools/ddp_equivalence.py --world W --same-device --batch B
 #   ab TAG "ENV=a" "ENV=b" ... -- [BENCH ARGS]   tools/ab_multi.sh
 #   py TAG SCRIPT [ARGS]       python -u SCRIPT ARGS -> gpurun_out/py_TAG.log
+#   sh TAG SCRIPT [ARGS]       bash SCRIPT ARGS -> gpurun_out/sh_TAG.log (e.g. tools/pmc.sh)
 #
 # usage (on the box): bash tools/gpu_job.sh "tests tests/test_gpu_xgmi.py" "bench exact --gpus 1 --steps 20 --warmup 5"
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -82,6 +83,10 @@ run_step() {
       local tag=$1; shift
       timeout -k 10 400 python -u "$@" > gpurun_out/py_$tag.log 2>&1; local rc=$?
       tail -40 gpurun_out/py_$tag.log; fatal $rc "py $tag";;
+    sh)
+      local tag=$1; shift
+      timeout -k 10 900 bash "$@" > gpurun_out/sh_$tag.log 2>&1; local rc=$?
+      tail -5 gpurun_out/sh_$tag.log; fatal $rc "sh $tag";;
     *)
       echo "unknown step kind '$kind'"; exit 2;;
   esac
