@@ -385,7 +385,7 @@ class FusedTrainer:
                 time.sleep(delay)
             run_chunk()
             wait()
-            result = ms.param.clone()
+            result = ms.param.cpu()                  # (host checks: no torch GPU kernel at startup)
             if not torch.isfinite(result).all():
                 why = f"rank {self.rank}: non-finite parameters"
         except TransportHang:

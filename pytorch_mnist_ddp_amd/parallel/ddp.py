@@ -320,6 +320,19 @@ def params_fingerprint(tensors) -> torch.Tensor:
     return torch.stack(parts).sum(0)
 
 
+def params_fingerprint_host(tensors) -> bytes:
+    """The same kind of fingerprint computed on the host from a D2H copy: startup paths use it so no
+    torch GPU kernel (and its first-launch code-object load) runs inside the reference timer."""
+    import numpy as np
+    b_sum = w_sum = 0
+    for t in tensors:
+        h = t.detach().reshape(-1).contiguous().cpu().numpy().view(np.int32).astype(np.int64)
+        w = np.arange(h.size, dtype=np.int64) % 8191 + 1
+        b_sum += int(h.sum())
+        w_sum += int((h * w).sum())
+    return f"{b_sum}:{w_sum}".encode()
+
+
 def assert_params_in_sync(tensors, group=None) -> None:
     """SURVEY §5.2 'DDP desync detector': every rank's parameters must be bitwise identical."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
