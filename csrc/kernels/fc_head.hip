@@ -52,23 +52,23 @@ __device__ __forceinline__ void fc1_tile(const uint16_t* __restrict__ p, const u
     B0[ks] = ld16(pb + ks * 32);
     B1[ks] = ld16(pb + 16 * NFLAT + ks * 32);
   }
+  // z1^T tiles (w1 fragments as the A operand): lane (m, kg) ends with outputs o = 32 wave + 4 kg
+  // + r (r = 0..3) of batch row m - 16 contiguous bytes of z1part, one 16-B store (write-through at
+  // small batches: only the head reads them) instead of four scattered 4-B stores
 #pragma unroll
   for (int t = 0; t < MR; ++t) {
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const bf16x8 a = valid[t] ? A[t][ks] : zero_frag();
-      acc0 = mfma16x16x32(a, B0[ks], acc0);
-      acc1 = mfma16x16x32(a, B1[ks], acc1);
+      acc0 = mfma16x16x32(B0[ks], a, acc0);
+      acc1 = mfma16x16x32(B1[ks], a, acc1);
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = (tile * MR + t) * 16 + 4 * kg + r;
-      if (b < B) {
-        float* dst = z1part + ((int64_t)chunk * B + b) * NH + 32 * wave + m;
-        dst[0] = acc0[r];
-        dst[16] = acc1[r];
-      }
+    const int b = (tile * MR + t) * 16 + m;
+    if (b < B) {
+      const int64_t e = ((int64_t)chunk * B + b) * NH + 32 * wave + 4 * kg;
+      store16(B <= WT_MAX_B, z1part, e * 4, acc0);
+      store16(B <= WT_MAX_B, z1part, (e + 16) * 4, acc1);
     }
   }
 }
@@ -504,31 +504,37 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
       if (ones) {
         acc[mt][0] = mfma16x16x32(A, onesfrag, acc[mt][0]);
       } else {
+        // dW1^T tiles (p fragments as the A operand): lane (l & 15, g) ends with columns
+        // i0 + 16 nt + 4 g + r (r = 0..3) of row o = 32 wave + 16 mt + (l & 15) - one 16-B store
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int nb = 16 * nt + 4 * pp;
           const bf16x8 Bf = tr_frag(ps + rlo * 64 + swz_row128(rlo, nb), ps + rhi * 64 + swz_row128(rhi, nb));
-          acc[mt][nt] = mfma16x16x32(A, Bf, acc[mt][nt]);
+          acc[mt][nt] = mfma16x16x32(Bf, A, acc[mt][nt]);
         }
       }
     }
   }
+  // S == 1: final (scaled) gradient (write-through at small batches: read by the fc update only);
+  // S > 1: unscaled partial in the same layout (fc_grad_reduce)
+  float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
+  const float sc = (S == 1) ? a.grad_scale : 1.0f;
+  if (ones) {
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = 32 * wave + 16 * mt + 4 * g + r;
-      // S == 1: final (scaled) gradient; S > 1: unscaled partial in the same layout (fc_grad_reduce)
-      float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
-      const float sc = (S == 1) ? a.grad_scale : 1.0f;
-      if (ones) {
-        if ((lane & 15) == 0) dst[OFF_FC1_B + o] = acc[mt][0][r] * sc;
-      } else {
+      for (int r = 0; r < 4; ++r)
+        if ((lane & 15) == 0) dst[OFF_FC1_B + 32 * wave + 16 * mt + 4 * g + r] = acc[mt][0][r] * sc;
+  } else {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          dst[OFF_FC1_W + (int64_t)o * NFLAT + i0 + 16 * nt + (lane & 15)] = acc[mt][nt][r] * sc;
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int o = 32 * wave + 16 * mt + (lane & 15);
+        const floatx4 v = {acc[mt][nt][0] * sc, acc[mt][nt][1] * sc, acc[mt][nt][2] * sc, acc[mt][nt][3] * sc};
+        store16(S == 1 && B <= WT_MAX_B, dst, (OFF_FC1_W + (int64_t)o * NFLAT + i0 + 16 * nt + 4 * g) * 4, v);
       }
-    }
+  }
 }
 
 // B: gradient into the conv trunk.  WG = 16 batch rows x 4 consecutive pooled positions x 64 channels
