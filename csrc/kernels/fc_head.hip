@@ -166,25 +166,24 @@ __global__ __launch_bounds__(256) void fc1_fwd_big_kernel(const uint16_t* __rest
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(A[i], Bf[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(Bf[j], A[i], acc[i][j]);   // z1^T tiles
     }
     if (st + 1 < F1B_STAGES) F1B_STORE(buf ^ 1);
     __syncthreads();
   }
 #undef F1B_FETCH
 #undef F1B_STORE
-  // C fragment: row = 4*(lane>>4) + r, col = lane & 15
+  // transposed C fragment: lane (m, kg) holds outputs o = wc + 16 j + 4 kg + r (r = 0..3) of batch
+  // row b = wr + 16 i + m - one 16-B store each (write-through up to WT_MAX_B: the head reads them)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int b = r0 + wr + 16 * i + m;
+    if (b < B) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = r0 + wr + 16 * i + 4 * kg + r;
-      if (b < B) {
-        float* dst = z1part + ((int64_t)split * B + b) * NH + wc + m;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[16 * j] = acc[i][j][r];
-      }
+      for (int j = 0; j < 4; ++j)
+        store16(B <= WT_MAX_B, z1part, (((int64_t)split * B + b) * NH + wc + 16 * j + 4 * kg) * 4, acc[i][j]);
     }
+  }
 }
 
 void launch_fc1_fwd(const uint16_t* p, const uint16_t* w1, float* z1part, int B, hipStream_t s) {

@@ -66,13 +66,16 @@ struct TrunkCfg {
                                                               // 20 mod 32 words -> conflict-free rows
   static constexpr int POOL_OFF = 0, POOL_BYTES = C2 * WIN_LD * 4;
   static constexpr int FLAG_OFF = W2S_OFF, FLAG_BYTES = C2 * WIN_LD;
+  // the workgroup's pmask words ([pooled position / 4][channel] uint32, a contiguous 3 KB per strip
+  // of the global layout) staged past the flags, then stored as whole 16-B lanes
+  static constexpr int PM_OFF = (FLAG_OFF + FLAG_BYTES + 15) / 16 * 16, PM_BYTES = NS * (WIN / 4) * C2 * 4;
   static constexpr int LDS = W2S_OFF + W2S_BYTES;             // 53504 | 80128
   static constexpr int C1_PIX = THREADS / 4;                  // conv1 pixels per pass (4 chunks each)
   static constexpr int C1_ITERS = (A1_ROWS * H1 + C1_PIX - 1) / C1_PIX;   // 5 | 4
   static_assert(CHUNKS * THREADS * 16 == W2S_BYTES, "weight chunking");
   static_assert(XS_OFF + XS_BYTES <= LDS, "input rows alias the parked weight chunks");
   static_assert(W1S_OFF % 16 == 0 && W1S_OFF + W1S_BYTES <= LDS, "conv1 weights alias the parked chunks");
-  static_assert(POOL_BYTES <= A1S_BYTES && FLAG_OFF + FLAG_BYTES <= LDS, "epilogue staging aliasing");
+  static_assert(POOL_BYTES <= A1S_BYTES && PM_OFF + PM_BYTES <= LDS, "epilogue staging aliasing");
   static_assert(NS != 1 || 3 * LDS <= 160 * 1024, "three strip workgroups per CU");
 };
 
@@ -325,11 +328,11 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
         if (keep) mk[k >> 2] |= 4u << (8 * (k & 3));
       }
       // pmask layout [b][pooled position / 4][channel][4] (mnist_common.h): fc_bwd role B reads one
-      // contiguous 256-B run per row and 4-position group instead of 4 bytes per 144-B stride
-      const int w0 = strip0 * WIN + j16;
+      // contiguous 256-B run per row and 4-position group instead of 4 bytes per 144-B stride.
+      // Staged in LDS (this thread's words are 256 B apart), stored below as 16-B lanes.
+      uint32_t* pm_s = reinterpret_cast<uint32_t*>(smem + K::PM_OFF);
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-        *reinterpret_cast<uint32_t*>(a.pmask_out + (int64_t)b * NFLAT + (((w0 >> 2) + q4) * C2 + n) * 4) = mk[q4];
+      for (int q4 = 0; q4 < 4; ++q4) pm_s[((j16 >> 2) + q4) * C2 + n] = mk[q4];
     }
     uint4 s0, s1;
     s0.x = pack2bf(o[0], o[1]);   s0.y = pack2bf(o[2], o[3]);
@@ -339,6 +342,14 @@ __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(Tr
     const int64_t pb = ((int64_t)b * NFLAT + flat) * 2;           // write-through (read by later kernels)
     store16((int)gridDim.y <= WT_MAX_B, a.p_out, pb, s0);
     store16((int)gridDim.y <= WT_MAX_B, a.p_out, pb + 16, s1);
+  }
+  if (TRAIN) {
+    // the workgroup's pmask region: NS x 3 KB contiguous from position group strip0 * WIN / 4
+    // (write-through at small batches, as p_out; one 16-B lane per thread)
+    lds_barrier();
+    if (tid < K::PM_BYTES / 16)
+      store16((int)gridDim.y <= WT_MAX_B, a.pmask_out, (int64_t)b * NFLAT + strip0 * (WIN / 4) * C2 * 4 + tid * 16,
+              reinterpret_cast<const uint4*>(smem + K::PM_OFF)[tid]);
   }
   PHASE_MARK(6);
   // DDP schedule 3: the kernel completes only once the comm stream's fc update of the previous step
