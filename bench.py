@@ -189,7 +189,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 600; --cpu: 200)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default 50; --cpu: 10)")
     ap.add_argument("--batch-size", type=int, default=200, help="per-GPU batch (README config: 200)")
-    ap.add_argument("--graph-steps", type=int, default=25, help="steps per captured hipGraph (0 = eager)")
+    ap.add_argument("--graph-steps", type=int, default=50, help="steps per captured hipGraph (0 = eager; 50 as the driver)")
     ap.add_argument("--single-bucket", action="store_true", help="one all-reduce per step (no overlap)")
     ap.add_argument("--no-full-run", dest="full_run", action="store_false")
     ap.add_argument("--epochs", type=int, default=EPOCHS, help="epochs for the full-run wallclock")

@@ -69,7 +69,7 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='fused: native step engine (GPU default); module: the reference loop over '
                         'Net/DDP/Adadelta (always used with --no-cuda)')
     g.add_argument('--graph-steps', type=int, default=None,
-                   help='training steps per captured HIP graph (default: log-interval; 0 = eager)')
+                   help='training steps per captured HIP graph (default 50; 0 = eager)')
     g.add_argument('--bucket-cap-mb', type=float, default=25.0,
                    help='DDP gradient bucket cap in MiB (default 25, as torch DDP)')
     g.add_argument('--first-bucket-mb', type=float, default=1.0,

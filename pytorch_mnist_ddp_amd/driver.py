@@ -30,6 +30,13 @@ from .utils.logging import test_line, total_time_line, train_line
 from .utils.profiling import PhaseTimes
 
 
+
+# training steps per captured chunk (both graphs of a chunk are launched together; a chunk boundary
+# costs a fork / join and a host hand-off): 600-step same-box sweep 25 / 50 / 100 -> 65.9 / 65.0-65.8 /
+# 65.1-65.2 us a step, and chunks cut at every 10-step log interval 1.4-2.2 us a step more than
+# 20-step chunks (profiles/r4/s2/ab/gs_sweep_*.txt); logged losses are read per chunk
+DEFAULT_GRAPH_STEPS = 50
+
 def _json_log(path, rec):
     if path:
         with open(path, "a") as f:
@@ -328,7 +335,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
     # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
     # (No torch.optim object: constructing one imports torch._dynamo, ~1.6 s inside the timed run.)
     lr = float(args.lr)
-    graph_steps = args.log_interval if args.graph_steps is None else args.graph_steps
+    graph_steps = DEFAULT_GRAPH_STEPS if args.graph_steps is None else args.graph_steps
     trainer = FusedTrainer(ms, train_data, test_data if (not distributed or rank == 0) else None,
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
