@@ -170,7 +170,10 @@ struct AdadeltaArgs {
                               // kernel on the stream has completed: a hand-off without a launch)
 };
 enum AdadeltaRegion { ADA_ALL = 0, ADA_FC = 1, ADA_CONV = 2 };
-void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s);
+// grid > 0 (ADA_FC only): that many workgroups walk the 577 fc tiles grid-stride (ADA_FC_LEAN_GRID:
+// the single-GPU overlapped update, which runs beside wgrad / dgrad with slack to spare)
+constexpr int ADA_FC_LEAN_GRID = 144;
+void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s, int grid = 0);
 // conv gradient slab reduce + the whole Adadelta update in one launch (serial single-GPU step tail)
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 // conv-only form restricted to reduce parts [lo, hi) (conv_grad_reduce.h partition)

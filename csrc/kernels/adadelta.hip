@@ -107,7 +107,16 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   bool done = false;
-  if (region != ADA_CONV) {
+  if (region == ADA_FC && gridDim.x < FC1_TILES + 1) {
+    // fc bucket on fewer workgroups than tiles (grid-stride): the overlapped single-GPU / RCCL update
+    // runs beside wgrad / dgrad and only has to finish before the next step's trunk_fwd ends
+    for (int t = bid; t < FC1_TILES + 1; t += gridDim.x) {
+      if (t < FC1_TILES) fc1_tile<UPDATE>(a, ad, t, ts);
+      else elementwise<UPDATE>(a, ad, OFF_FC1_B, FC_TAIL_N, 0, 1);
+      __syncthreads();                            // ts is rewritten by the next tile
+    }
+    done = true;
+  } else if (region != ADA_CONV) {
     if (bid < FC1_TILES) {
       fc1_tile<UPDATE>(a, ad, bid, ts);
       done = true;
@@ -175,8 +184,10 @@ static int adadelta_grid(int region) {
   return FC1_TILES + 1 + CONV_WGS;
 }
 
-void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s) {
-  hipLaunchKernelGGL(adadelta_kernel<true>, dim3(adadelta_grid(region)), dim3(256), 0, s, a, region);
+void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s, int grid) {
+  if (grid > 0 && (region != ADA_FC || grid > FC1_TILES + 1))
+    throw std::runtime_error("adadelta: a reduced grid is for the fc region only");
+  hipLaunchKernelGGL(adadelta_kernel<true>, dim3(grid > 0 ? grid : adadelta_grid(region)), dim3(256), 0, s, a, region);
 }
 
 void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s) {

@@ -351,7 +351,10 @@ void Engine::enqueue_step(int batch, bool last) {
         af.hold_delta = 1;
         af.hold_err = sync_ + 2;
       }
-      launch_adadelta(af, ADA_FC, comm_stream_);
+      // 144 workgroups instead of 577: the update has ~15 us of slack before the next step's trunk
+      // ends, and fewer co-resident waves leave wgrad / dgrad more of the CUs (600 steps, two boxes:
+      // 65.9 -> 65.2, 65.0-65.7 -> 64.4-64.9 us/step; 96 / 64 workgroups: 67.6 / 74-75)
+      launch_adadelta(af, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
     } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused
       xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
     } else {
