@@ -310,13 +310,18 @@ void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
 // fc bucket with the fc Adadelta step fused (two-shot).  The unit of work is a 64(o) x 32(i) tile
 // of fc1.weight (576 tiles) plus one pseudo-tile for the tail (fc1.b, fc2.w, fc2.b; 368 float4):
 // shard p = units [p*577/W, (p+1)*577/W).  Workgroup b owns units lo_p + b + m*G of every shard p
-// (G = grid, any size: the residency planner may shrink it).  Phase 1: WG b reduces its units of
-// shard r (rank order) into its output bucket; stage 1; phase 2: WG b gathers its units of EVERY
-// shard, two at a time (gathered sums + local optimizer state in flight together), applies Ada::step
-// with the gathered sums as gradients and writes param / square_avg / acc_delta plus the bf16 shadows
-// w1 [128][9216] and w1t [9216][128] (tile transposed through LDS) - exactly the adadelta kernel's
-// fc1 tile math, so bitwise equal to the all-reduce + separate update it replaces.  The fc branch
-// of the DDP step loses a launch and a 4.7 MB gradient re-read.
+// (G = grid, any size: the residency planner may shrink it).
+//   phase 1: WG b reduces its units of shard r (rank order) into its output bucket (the peers'
+//            phase-2 source) and applies the update to them at once - their gradients are final;
+//   stage 1;
+//   phase 2: WG b gathers its units of every OTHER shard (gathered sums + local optimizer state in
+//            flight together) and applies the update.
+// The update is exactly the adadelta kernel's fc1 tile math (Ada::step, param / square_avg /
+// acc_delta, bf16 shadows w1 [128][9216] and w1t [9216][128], the tile transposed through LDS), so the
+// result is bitwise that of the all-reduce + separate update it replaces.  Registers and LDS are kept
+// at the single-GPU update's scale (one unit per pass at W <= 2, 4.6 KB of LDS) so the kernel fits
+// beside the persistent conv2_dgrad's workgroups (2 x 216 VGPRs per SIMD, 150 KB of LDS per CU) -
+// at 103 VGPRs it did not, and dgrad ran 2 us longer beside it (world-1 in-kernel timeline).
 namespace {
 constexpr int FCU_TILES = 2 * (NFLAT / 32);                      // 576
 constexpr int FCU_UNITS = FCU_TILES + 1;                         // + tail
@@ -334,15 +339,64 @@ __device__ __forceinline__ int fcu_f4(int u, int h, int tid) {
   const int q = tid + 256 * h;                                   // tail: 368 float4
   return q < FCU_TAIL_F4 ? (int)(OFF_FC1_B / 4) + q : -1;
 }
+
+__device__ __forceinline__ void fcu_load_state(const XgmiArgs& a, const int q[2], float4 pr[2], float4 sq[2],
+                                               float4 ac[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (q[h] < 0) continue;
+    pr[h] = reinterpret_cast<const float4*>(a.ada.param)[q[h]];
+    sq[h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q[h]];
+    ac[h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q[h]];
+  }
+}
+
+// Unit u's update from its reduced gradients g (this lane's 2 float4; q = their bucket indices,
+// -1 past the tail).  Workgroup-uniform call: two LDS barriers around the w1t transpose in ts.
+__device__ __forceinline__ void fcu_update(const XgmiArgs& a, const Ada& ad, int u, int tid, const int q[2],
+                                           const f4 g[2], float4 pr[2], float4 sq[2], float4 ac[2], uint16_t* ts) {
+  float v8[8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (q[h] < 0) continue;
+    ad.step(pr[h].x, g[h].x, sq[h].x, ac[h].x);
+    ad.step(pr[h].y, g[h].y, sq[h].y, ac[h].y);
+    ad.step(pr[h].z, g[h].z, sq[h].z, ac[h].z);
+    ad.step(pr[h].w, g[h].w, sq[h].w, ac[h].w);
+    // write-through 16-B stores at small batches (AdadeltaArgs::wt, as the single-GPU update): the
+    // next step's kernels read these, and the kernel-end write-back of dirty lines is a step gap
+    store16(a.ada.wt, a.ada.param, (int64_t)q[h] * 16, make_floatx4(pr[h]));
+    store16(a.ada.wt, a.ada.square_avg, (int64_t)q[h] * 16, make_floatx4(sq[h]));
+    store16(a.ada.wt, a.ada.acc_delta, (int64_t)q[h] * 16, make_floatx4(ac[h]));
+    v8[4 * h] = pr[h].x; v8[4 * h + 1] = pr[h].y; v8[4 * h + 2] = pr[h].z; v8[4 * h + 3] = pr[h].w;
+  }
+  const bool tile = u < FCU_TILES;                               // workgroup-uniform
+  const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
+  if (tile) {                                                    // bf16 shadows of the fc1 tile
+    const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
+    uint4 lo4;
+    lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
+    lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
+    store16(a.ada.wt, a.ada.w1, ((int64_t)o * NFLAT + i0 + ic) * 2, lo4);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) ts[(ic + jj) * FCU_TS + ol] = f2bf(v8[jj]);
+  }
+  lds_barrier();
+  if (tile) {
+    const int il = tid >> 3, oc = (tid & 7) * 8;
+    store16(a.ada.wt, a.ada.w1t, ((int64_t)(32 * it + il) * NH + 64 * ot + oc) * 2,
+            *reinterpret_cast<const uint4*>(ts + il * FCU_TS + oc));
+  }
+  lds_barrier();                                                 // ts is rewritten by the next unit
+}
 }  // namespace
 
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_FC);
-  constexpr int PU = W <= 2 ? 2 : 1;                             // phase-1 units in flight per lane
-  constexpr int PG = 2;                                          // phase-2 units in flight per lane
+  constexpr int PG = W >= 4 ? 2 : 1;                             // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;
-  __shared__ __attribute__((aligned(16))) uint16_t ts[PG][32 * FCU_TS];
+  __shared__ __attribute__((aligned(16))) uint16_t ts[32 * FCU_TS];
   const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
   if (tid == 0) {
     const int e = a.ctr[b] + 1;
@@ -356,112 +410,93 @@ __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
   const int64_t bytes = a.nvec * 16;
   const __amdgpu_buffer_rsrc_t out = rsrc(a.out[r], bytes);
   if (!xgmi_stage(a, 0, b, e, XGMI_K_FC_FUSED)) return;
-  // ---- phase 1: my shard's units, rank-order sums -> my output
+  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
+  // ---- phase 1: my shard's units - rank-order sums -> my output (for the peers), then the update
   {
     __amdgpu_buffer_rsrc_t in[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) in[p] = rsrc(a.in[p], bytes);
     const int lo = fcu_lo(r, W), hi = fcu_lo(r + 1, W);
-    for (int u0 = lo + b; u0 < hi; u0 += PU * G) {
-      f4 v[PU][2][W];
-      int q[PU][2];
+    for (int u = lo + b; u < hi; u += G) {                       // workgroup-uniform
+      int q[2];
+      f4 g[2];
+      float4 pr[2], sq[2], ac[2];
 #pragma unroll
-      for (int j = 0; j < PU; ++j) {
-        const int u = u0 + j * G;
+      for (int h = 0; h < 2; ++h) q[h] = fcu_f4(u, h, tid);
+      fcu_load_state(a, q, pr, sq, ac);                          // local, in flight with the peer loads
+      if (W <= 2) {                                              // both halves' peer loads at once
+        f4 v[2][W];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int p = 0; p < W; ++p) v[h][p] = ld_sys(in[p], q[h] < 0 ? a.nvec : q[h]);   // -1: 0
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          q[j][h] = u < hi ? fcu_f4(u, h, tid) : -1;
+          g[h] = v[h][0];
 #pragma unroll
-          for (int p = 0; p < W; ++p) v[j][h][p] = ld_sys(in[p], q[j][h] < 0 ? a.nvec : q[j][h]);   // -1: 0
+          for (int p = 1; p < W; ++p) g[h] += v[h][p];
+        }
+      } else {                                                   // one half's W loads at a time
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f4 v[W];
+#pragma unroll
+          for (int p = 0; p < W; ++p) v[p] = ld_sys(in[p], q[h] < 0 ? a.nvec : q[h]);
+          g[h] = v[0];
+#pragma unroll
+          for (int p = 1; p < W; ++p) g[h] += v[p];
         }
       }
 #pragma unroll
-      for (int j = 0; j < PU; ++j)
+      for (int h = 0; h < 2; ++h)
+        if (q[h] >= 0) st_sys(out, q[h], g[h]);
+      fcu_update(a, ad, u, tid, q, g, pr, sq, ac, ts);
+    }
+  }
+  if constexpr (W > 1) {
+    if (!xgmi_stage(a, 1, b, e, XGMI_K_FC_FUSED)) return;
+    // ---- phase 2: items j over the other shards (p' = j mod (W-1) -> p, m = j / (W-1)): unit
+    // lo_p + b + m*G, which peer p's workgroup b reduced; consecutive items come from different
+    // peers' links.  Workgroup-uniform loop bounds (the LDS transpose needs the barriers).
+    const int M = ((FCU_UNITS + W - 1) / W + G - 1) / G;       // units per shard per WG (upper bound)
+    for (int j0 = 0; j0 < (W - 1) * M; j0 += PG) {
+      int uu[PG], q[PG][2];
+      f4 g[PG][2];
+      float4 pr[PG][2], sq[PG][2], ac[PG][2];
+#pragma unroll
+      for (int k = 0; k < PG; ++k) {
+        const int j = j0 + k, pp = j % (W - 1), m = j / (W - 1);
+        const int p = pp + (pp >= r ? 1 : 0);
+        const int u = fcu_lo(p, W) + b + m * G;
+        uu[k] = (j < (W - 1) * M && u < fcu_lo(p + 1, W)) ? u : -1;
+        if (uu[k] < 0) continue;
+        const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          f4 t = v[j][h][0];
-#pragma unroll
-          for (int p = 1; p < W; ++p) t += v[j][h][p];
-          if (q[j][h] >= 0) st_sys(out, q[j][h], t);
+          q[k][h] = fcu_f4(u, h, tid);
+          g[k][h] = ld_sys(src, q[k][h] < 0 ? a.nvec : q[k][h]);
         }
+        fcu_load_state(a, q[k], pr[k], sq[k], ac[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < PG; ++k)
+        if (uu[k] >= 0) fcu_update(a, ad, uu[k], tid, q[k], g[k], pr[k], sq[k], ac[k], ts);
     }
   }
-  if (!xgmi_stage(a, 1, b, e, XGMI_K_FC_FUSED)) return;
-  // ---- phase 2: items j = p + W*m (unit lo_p + b + m*G of shard p), PG per pass; consecutive items
-  // come from different shards, i.e. different peers' links.  Workgroup-uniform loop bounds (the
-  // LDS transpose needs the barriers).
-  const Ada ad{a.ada.rho, a.ada.eps, a.ada.weight_decay, *a.ada.lr};
-  const int M = ((FCU_UNITS + W - 1) / W + G - 1) / G;         // units per shard per WG (upper bound)
-  for (int j0 = 0; j0 < W * M; j0 += PG) {
-    int uu[PG], pp[PG];
-    f4 g[PG][2];
-    float4 pr[PG][2], sq[PG][2], ac[PG][2];
-#pragma unroll
-    for (int k = 0; k < PG; ++k) {
-      const int j = j0 + k, p = j % W, m = j / W;
-      const int u = fcu_lo(p, W) + b + m * G;
-      uu[k] = (j < W * M && u < fcu_lo(p + 1, W)) ? u : -1;
-      pp[k] = p;
-      if (uu[k] < 0) continue;
-      const __amdgpu_buffer_rsrc_t src = rsrc(a.out[p], bytes);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
-        if (q < 0) continue;
-        g[k][h] = ld_sys(src, q);
-        pr[k][h] = reinterpret_cast<const float4*>(a.ada.param)[q];
-        sq[k][h] = reinterpret_cast<const float4*>(a.ada.square_avg)[q];
-        ac[k][h] = reinterpret_cast<const float4*>(a.ada.acc_delta)[q];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < PG; ++k) {
-      const int u = uu[k];
-      if (u < 0) continue;
-      float v8[8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = fcu_f4(u, h, tid);
-        if (q < 0) continue;
-        float4 P = pr[k][h], S = sq[k][h], A = ac[k][h];
-        const f4 G4 = g[k][h];
-        ad.step(P.x, G4.x, S.x, A.x);
-        ad.step(P.y, G4.y, S.y, A.y);
-        ad.step(P.z, G4.z, S.z, A.z);
-        ad.step(P.w, G4.w, S.w, A.w);
-        reinterpret_cast<float4*>(a.ada.param)[q] = P;
-        reinterpret_cast<float4*>(a.ada.square_avg)[q] = S;
-        reinterpret_cast<float4*>(a.ada.acc_delta)[q] = A;
-        v8[4 * h] = P.x; v8[4 * h + 1] = P.y; v8[4 * h + 2] = P.z; v8[4 * h + 3] = P.w;
-      }
-      if (u < FCU_TILES) {                                        // bf16 shadows of the fc1 tile
-        const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
-        const int ol = tid >> 2, ic = (tid & 3) * 8, o = 64 * ot + ol, i0 = 32 * it;
-        uint4 lo4;
-        lo4.x = pack2bf(v8[0], v8[1]); lo4.y = pack2bf(v8[2], v8[3]);
-        lo4.z = pack2bf(v8[4], v8[5]); lo4.w = pack2bf(v8[6], v8[7]);
-        *reinterpret_cast<uint4*>(a.ada.w1 + (int64_t)o * NFLAT + i0 + ic) = lo4;
-        uint16_t* t = ts[k];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) t[(ic + jj) * FCU_TS + ol] = f2bf(v8[jj]);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PG; ++k) {
-      const int u = uu[k];
-      if (u < 0 || u >= FCU_TILES) continue;
-      const int ot = u / (NFLAT / 32), it = u - ot * (NFLAT / 32);
-      const int il = tid >> 3, oc = (tid & 7) * 8;
-      *reinterpret_cast<uint4*>(a.ada.w1t + (int64_t)(32 * it + il) * NH + 64 * ot + oc) =
-          *reinterpret_cast<const uint4*>(ts[k] + il * FCU_TS + oc);
-    }
-    __syncthreads();                                              // ts is rewritten by the next pass
-    (void)pp;
-  }
+  // optional completion hold (the XGMI comm chain, as the single-GPU fc update): the launch
+  // completes only once *hold_a >= *hold_b + hold_delta (this step's dgrad has started), so the
+  // conv2 part that follows on the comm stream needs no wait launch of its own
+  if (a.ada.hold_a && b == G - 1 && tid == 0)
+    spin_until_geq(a.ada.hold_a,
+                   __hip_atomic_load(a.ada.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a.ada.hold_delta,
+                   a.ada.hold_err);
 }
 
 int xgmi_fc_fused_workgroups(int world) {
+  // one workgroup per unit of this rank's shard (the residency planner may shrink it).  Not the
+  // single-GPU update's lean 144: this kernel's units wait on uncached / peer loads, so fewer
+  // workgroups lengthen the fc branch more than they relieve the conv backward (world 1, 600 steps:
+  // natural grid 68.5-68.9 us/step, 256 workgroups 69.7-70.8; before the slim kernel 144 was worse too)
   const int per = (FCU_UNITS + world - 1) / world;
   return per < XGMI_MAX_WG ? per : XGMI_MAX_WG;
 }
@@ -518,6 +553,10 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
     a.ctr[b] = e;
     s_epoch = e;
     s_err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // XGMI comm chain: "the previous launch on this stream (the fc all-reduce + update) is done",
+    // signalled by the first workgroup at its start instead of by a signal launch
+    if (b == 0 && a.ada.signal_start)
+      __hip_atomic_fetch_add(a.ada.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
   // (the reduce's first barrier orders the slot initialisation before any sink write)
   for (int k = 0; k < nvb; ++k) {

@@ -334,7 +334,10 @@ void Engine::enqueue_step(int batch, bool last) {
   // has started, conv2's reduce + update signals "fc update done" [1] at its start, and its own
   // "conv2 update done" [3] is signalled by the next step's first comm launch, which then waits for
   // that step's wgrad: one small launch per step instead of two waits and two signals
-  const bool chain = !xg && !trace_;
+  // XGMI (fused kernels) runs the same chain: the fc all-reduce + update holds its completion, the
+  // conv2 reduce + all-reduce + update signals [1] at its start (world-1 timeline: two hand-off launches
+  // a step fewer, conv2's part no longer queued behind them)
+  const bool chain = !trace_ && (!xg || xgmi_fuse_update_);
   phase_begin("allreduce_fc+update");
   if (S) {
     if (chain && comm_sig3_pending_)
@@ -356,7 +359,14 @@ void Engine::enqueue_step(int batch, bool last) {
       // 65.9 -> 65.2, 65.0-65.7 -> 64.4-64.9 us/step; 96 / 64 workgroups: 67.6 / 74-75)
       launch_adadelta(af, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
     } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused
-      xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, ad);
+      AdadeltaArgs af = ad;
+      if (chain) {                              // completes once this step's dgrad has started
+        af.hold_a = sync_ + 4;
+        af.hold_b = sync_ + 3;
+        af.hold_delta = 1;
+        af.hold_err = sync_ + 2;
+      }
+      xgmi_->allreduce_fc_fused(XGMI_CH_FC, comm_stream_, af);
     } else {
       xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
@@ -392,13 +402,13 @@ void Engine::enqueue_step(int batch, bool last) {
     cb.w2d = w2d_cur;
     if (S) {
       if (!chain) launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+      if (chain) u2.signal_start = sync_ + 1;     // the fc update (previous launch) is done
       if (xg) {
         XgmiConvPart p2;
         p2.lo = 0;
         p2.hi = RED_W2_PARTS;
         xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, comm_stream_, u2, p2);
       } else {
-        if (chain) u2.signal_start = sync_ + 1;   // the fc update (previous launch) is done
         launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
       }
       if (chain && !last)

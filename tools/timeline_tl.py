@@ -82,8 +82,23 @@ def measure(args):
         parts.append(idx[: (idx.numel() // B) * B])
         ep += 1
     stream = torch.cat(parts)[: total * B]
+    comm, kw = None, {}
+    if args.sched != "overlap":
+        # world-1 DDP production schedule: a one-rank process group (its store carries the RCCL uid)
+        # and the selected transport attached, exactly as bench.py --force-comm under torchrun
+        import socket
+        import torch.distributed as dist
+        from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comm
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("gloo", init_method="env://", world_size=1, rank=0)
+        if args.sched == "rccl":
+            comm = create_rccl_comm(1, 0, 0)
+        kw = dict(comm=comm, allreduce=args.sched)
     tr = FusedTrainer(ms, train, None, B, 1000, num_samples=max(total * B, 60000), seed=1,
-                      graph_steps=args.graph_steps)
+                      graph_steps=args.graph_steps, **kw)
     tr.start_stream(stream, gather=True)
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
@@ -141,14 +156,16 @@ def analyse(recs, steps):
 def overlap_checks(table):
     t = {r["kernel"]: r for r in table}
     out = []
-    if "ada_fc" in t and "conv2_wgrad" in t and "conv2_dgrad" in t:
-        r = t["ada_fc"]
-        out.append(f"fc Adadelta (comm stream) {r['start_us']:.1f}-{r['end_us']:.1f} us inside the conv backward "
+    fc = "ada_fc" if "ada_fc" in t else "xgmi_fc_fused"
+    c2 = "conv2 reduce+update" if "conv2 reduce+update" in t else "xgmi_conv2_fused"
+    if fc in t and "conv2_wgrad" in t and "conv2_dgrad" in t:
+        r = t[fc]
+        out.append(f"fc update {fc} (comm stream) {r['start_us']:.1f}-{r['end_us']:.1f} us inside the conv backward "
                    f"{t['conv2_wgrad']['start_us']:.1f}-{t['conv2_dgrad']['end_us']:.1f} us: "
                    f"{t['conv2_wgrad']['start_us'] <= r['start_us'] and r['end_us'] <= t['conv2_dgrad']['end_us']}")
-    if "conv2 reduce+update" in t and "conv2_dgrad" in t:
-        r = t["conv2 reduce+update"]
-        out.append(f"conv2 reduce+update (comm stream) {r['start_us']:.1f}-{r['end_us']:.1f} us under conv2_dgrad "
+    if c2 in t and "conv2_dgrad" in t:
+        r = t[c2]
+        out.append(f"conv2 part {c2} (comm stream) {r['start_us']:.1f}-{r['end_us']:.1f} us under conv2_dgrad "
                    f"{t['conv2_dgrad']['start_us']:.1f}-{t['conv2_dgrad']['end_us']:.1f} us: "
                    f"{r['start_us'] >= t['conv2_dgrad']['start_us'] and r['end_us'] <= t['conv2_dgrad']['end_us'] + 1.0}")
     return out
@@ -158,6 +175,9 @@ def product_period(args) -> float | None:
     """The same command's period with the product build (bench.py, host-timed)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup", str(args.warmup),
            "--batch-size", str(args.batch), "--graph-steps", str(args.graph_steps), "--no-full-run"]
+    if args.sched != "overlap":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes",
+               "1", "--nproc-per-node", "1"] + cmd[1:] + ["--force-comm", "--allreduce", args.sched]
     env = {k: v for k, v in os.environ.items() if k != "MNIST_AMD_TIMELINE"}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     for ln in r.stdout.splitlines():
@@ -173,6 +193,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph-steps", type=int, default=25)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--sched", choices=["overlap", "xgmi", "rccl"], default="overlap",
+                    help="overlap: single GPU; xgmi / rccl: the world-1 DDP production schedule")
     ap.add_argument("--no-product", action="store_true")
     args = ap.parse_args()
     recs, sched = measure(args)
