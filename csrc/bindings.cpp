@@ -345,6 +345,7 @@ PYBIND11_MODULE(_C, m) {
       .def("attach_xgmi", &Engine::attach_xgmi)
       .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)
       .def("set_bucket_split", &Engine::set_bucket_split)
+      .def("set_rccl_handoff", &Engine::set_rccl_handoff)
       .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("schedule", &Engine::schedule)
       .def("reset_counters", &Engine::reset_counters, py::call_guard<py::gil_scoped_release>())

@@ -236,7 +236,7 @@ void Engine::enqueue_step(int batch, bool last) {
   }
   // the previous step's fc update (comm stream) must be done before fc1_fwd reads w1: trunk_fwd
   // holds its completion for it (device counters, no extra launch)
-  if (side && side_pending_) {
+  if ((side || sched_ == RCCL) && side_pending_) {
     tf.wait_a = sync_ + 1;
     tf.wait_b = sync_ + 0;
     tf.wait_err = sync_ + 2;
@@ -297,18 +297,31 @@ void Engine::enqueue_step(int batch, bool last) {
     // the fc bucket (98.4 % of the bytes) forks onto the comm stream as soon as fc_bwd is done and
     // overlaps the conv backward; the conv bucket follows on compute after the join, so the one
     // communicator sees fc, conv in the same order on every rank and never two collectives at once.
+    // The join waits for the fc ALL-REDUCE only: the fc update runs after it on the comm stream
+    // (144 workgroups, beside dgrad and the conv tail) and is ordered before the next step's fc1_fwd
+    // by trunk_fwd's completion hold on device counters ([0] wgrad starts, [1] fc updates done), as in
+    // OVERLAP - at world > 1 the update is no longer on the path to the conv all-reduce.
     // (capture order matters: the graph executor keeps a fork's first-captured child on the
     // launching queue, so conv2 wgrad is enqueued before the comm branch)
     HIP_OK(hipEventRecord(ev_fc_, compute_));
+    ConvBwdArgs cbs = cb;
+    cbs.signal_ctr = sync_ + 0;                   // wgrad's start: this step's fc grads are final
     phase_begin("bwd_conv_wgrad");
-    launch_conv_wgrad(cb, B, compute_);
+    launch_conv_wgrad(cbs, B, compute_);
     phase_end();
     phase_begin("allreduce_fc+update");
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
-    launch_adadelta(ad, ADA_FC, comm_stream_);
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    if (rccl_handoff_) {
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      launch_adadelta(ad, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
+      launch_stream_signal(sync_ + 1, comm_stream_);  // fc update of this step done
+      side_pending_ = true;
+    } else {                                      // streams share a hardware queue: no counter holds
+      launch_adadelta(ad, ADA_FC, comm_stream_);
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    }
     phase_end();
     phase_begin("bwd_conv_dgrad");
     launch_conv_dgrad(cb, B, compute_);
@@ -319,6 +332,11 @@ void Engine::enqueue_step(int batch, bool last) {
     comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
     launch_adadelta(adc, ADA_CONV, compute_);
     phase_end();
+    if (last && rccl_handoff_) {                  // chunk end: the comm stream joins (fc update done)
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      side_pending_ = false;
+    }
     return;
   }
 

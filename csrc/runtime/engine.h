@@ -10,11 +10,12 @@
 //                                       dgrad(+[4]), conv1 reduce+update(hold [3]>=[4])
 //                                    M: (+[3] of the previous step) wait [0]: fc update (hold [4]>=[3]+1),
 //                                       conv2 reduce+update (+[1] at start); chunk end: +[3]
-//   RCCL     (DDP over RCCL)         C: trunk, fc1, head, fc_bwd -ev_fc-> wgrad, dgrad, conv reduce,
-//                                       (wait ev_done) all-reduce(conv), update(conv)
-//                                    M: (wait ev_fc) all-reduce(fc), update(fc) -ev_done->
+//   RCCL     (DDP over RCCL)         C: trunk(hold [1]>=[0]), fc1, head, fc_bwd -ev_fc-> wgrad(+[0]),
+//                                       dgrad, conv reduce, (wait ev_done) all-reduce(conv), update(conv)
+//                                    M: (wait ev_fc) all-reduce(fc) -ev_done->, update(fc), +[1]
 //                                    one communicator, collectives issued and run in step order fc ->
-//                                    conv (graph edges, no device counters): one graph per chunk
+//                                    conv (graph edges); the fc update is ordered by the counters
+//                                    (set_rccl_handoff; off: update(fc) before ev_done): one graph per chunk
 //   XGMI     (DDP over the direct xGMI kernels) the OVERLAP structure with the all-reduces fused in:
 //                                    M: fc all-reduce+update (xgmi_fc_fused), conv2 reduce+all-reduce+
 //                                    update; C: conv1 reduce+all-reduce+update (fuse off: separate
@@ -85,6 +86,10 @@ class Engine {
   // reduce / all-reduce / update launches (the A/B oracle of the fused kernels' bits).
   void set_xgmi_fuse_update(bool on) { xgmi_fuse_update_ = on; }
   void set_bucket_split(bool two_buckets) { two_buckets_ = two_buckets; }   // RCCL: 2 buckets or 1
+  // RCCL two-bucket schedule: the fc update after the join, ordered by device-counter holds (needs
+  // the compute / comm streams on distinct hardware queues: probe_stream_handoff); off = the update
+  // before the join (graph edges only)
+  void set_rccl_handoff(bool on) { rccl_handoff_ = on; }
   // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
   // hand-off counters and their error flag, so a schedule never inherits another's counts (e.g. an
   // aborted validation).  Detaching the xgmi communicator of the XGMI schedule unsets the schedule.
@@ -149,6 +154,7 @@ class Engine {
   int world_;
   float rho_, eps_, wd_;
   bool two_buckets_ = true;
+  bool rccl_handoff_ = false;
   int idx_stride_ = 0;
   int sched_ = SERIAL;
   std::shared_ptr<RcclComm> comm_;

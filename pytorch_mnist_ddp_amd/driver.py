@@ -208,14 +208,20 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
 
 
 def gpu_present() -> bool:
-    """A GPU is visible to this process: the KFD + a DRM render node exist and HIP_VISIBLE_DEVICES /
-    CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES do not hide every device.  No runtime call."""
+    """A GPU is usable by this process: torch is a ROCm build, the KFD + a DRM render node exist and
+    are accessible, and HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES do not
+    hide every device.  No runtime call (torch.cuda.is_available() brings HIP up: ~60 ms inside the
+    reference timer); a node that passes this and still has no usable GPU fails loudly in the
+    prewarm thread's runtime init."""
     import glob
+    if not getattr(torch.version, "hip", None):       # CPU-only (or non-ROCm) torch build
+        return False
     for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None and v.strip() in ("", "-1"):
             return False
-    return os.path.exists("/dev/kfd") and bool(glob.glob("/dev/dri/renderD*"))
+    nodes = glob.glob("/dev/dri/renderD*")
+    return os.access("/dev/kfd", os.R_OK | os.W_OK) and any(os.access(n, os.R_OK | os.W_OK) for n in nodes)
 
 
 def _prewarm_body(device, steps: dict | None = None) -> None:
@@ -343,8 +349,9 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                            fp32=getattr(args, "dtype", "bf16") == "fp32")
     setup.mark("trainer")
     if distributed and rank == 0 and trainer.allreduce_timings:
+        # stderr: stdout carries exactly the reference's line kinds
         print(f"| gradient all-reduce: {trainer.allreduce} (schedule us/step: {trainer.allreduce_timings})",
-              flush=True)
+              file=sys.stderr, flush=True)
     if args.profile:
         trainer.profile_left = args.profile_steps
     n_train = len(train_data)
@@ -375,6 +382,11 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             rec.update(test_loss=loss_sum / n, correct=correct)
             setup.mark(f"epoch{epoch}_eval")
         dev_s = st.device_time()
+        if pipelined:
+            # the epoch's work is complete (its end event): fail at the first bad epoch, as the
+            # sequential form does in train_epoch - a stream hand-off or xGMI stage timeout would
+            # otherwise surface only after the last epoch (two 4-byte reads)
+            trainer.check_errors()
         rec["device_train_s"] = dev_s
         if dev_s:
             rec["device_img_per_s"] = st.samples / dev_s
@@ -444,13 +456,38 @@ def _save(args, model, distributed, rank, ddp_script):
         save_state_dict(model, "mnist_cnn_.pt")
 
 
+def _fatal_exit(e: BaseException) -> None:
+    """A collective stuck on the device (``TransportHang``: ``fatal``) cannot be cancelled, and the
+    interpreter's teardown of the RCCL / HIP objects would wait for it: report, tell the other ranks
+    through the store, and leave without the runtime's teardown (as bench.py does)."""
+    print(f"FATAL: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+    try:
+        from .parallel.hostcomm import get_hostcomm
+        get_hostcomm().abort(f"{type(e).__name__}: {e}"[:300])
+    except Exception:  # noqa: BLE001 - no process group / store: nothing to tell
+        pass
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(3)
+
+
 def main_mnist(argv=None) -> int:
-    return run(argv, ddp_script=False)
+    try:
+        return run(argv, ddp_script=False)
+    except BaseException as e:  # noqa: BLE001
+        if getattr(e, "fatal", False):
+            _fatal_exit(e)
+        raise
 
 
 def main_mnist_ddp(argv=None) -> int:
     start = time.time()
-    rc = run(argv, ddp_script=True, t_start=start)
+    try:
+        rc = run(argv, ddp_script=True, t_start=start)
+    except BaseException as e:  # noqa: BLE001
+        if getattr(e, "fatal", False):
+            _fatal_exit(e)
+        raise
     print(total_time_line(time.time() - start))
     sys.stdout.flush()
     return rc

@@ -161,6 +161,9 @@ class FusedTrainer:
                        for _ in range(2)]
         self._idx_ev = [None, None]
         self._idx_k = 0
+        self._lr_h = [torch.empty(1, dtype=torch.float32, pin_memory=True) for _ in range(2)]   # set_lr
+        self._lr_ev = [None, None]
+        self._lr_k = 0
         bufs = mstate.buffers()
         p = native.ptr
         bufs.update(loss_log=p(self.loss_log), train_u8=p(self.train_u8), train_labels=p(self.train_labels),
@@ -238,10 +241,14 @@ class FusedTrainer:
                                                             and (self.world > 1 or probe_world1)))
         want_r = comm is not None and allreduce in ("rccl", "auto")
         x = None
+        # compute / comm streams on distinct hardware queues: the device-counter hand-offs of the
+        # XGMI schedule and of the RCCL schedule's fc update need it (one probe, every rank)
+        handoff = self._probe_streams() if (want_x or (want_r and two_buckets)) else False
+        self.engine.set_rccl_handoff(handoff)
         if want_x:
             with self.setup.phase("xgmi_comm"):
                 x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel())
-            if x is not None and not self._probe_streams():
+            if x is not None and not handoff:
                 if self.rank == 0:
                     print("[engine] compute/comm streams share a hardware queue: no xGMI schedule", flush=True)
                 release_xgmi_comm(x, self.world)
@@ -452,10 +459,21 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------ helpers
     def set_lr(self, lr: float) -> None:
-        # an H2D copy on the compute stream (stream-ordered with the epochs around it; the pageable
-        # source is staged before copy_ returns), not a fill kernel
+        """StepLR's new rate for the kernels (device scalar): an asynchronous H2D copy on the compute
+        stream from one of two pinned host scalars (stream-ordered with the epochs around it; no fill
+        kernel).  A pageable source would make copy_ block until the stream is idle - at every epoch
+        boundary of the pipelined driver.  Each pinned scalar is rewritten only after its previous
+        copy has run (event), as the index upload does."""
+        k = self._lr_k
+        self._lr_k ^= 1
+        if self._lr_ev[k] is not None:
+            self._lr_ev[k].synchronize()
+        self._lr_h[k][0] = float(lr)
         with torch.cuda.stream(self.compute):
-            self.ms.lr.copy_(torch.tensor([float(lr)], dtype=torch.float32))
+            self.ms.lr.copy_(self._lr_h[k], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.compute)
+        self._lr_ev[k] = ev
 
     def _graph(self, n: int, batch: int) -> int:
         key = (n, batch)

@@ -333,16 +333,17 @@ def params_fingerprint_host(tensors) -> bytes:
     return f"{b_sum}:{w_sum}".encode()
 
 
-def assert_params_in_sync(tensors, group=None) -> None:
-    """SURVEY §5.2 'DDP desync detector': every rank's parameters must be bitwise identical."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+def assert_params_in_sync(tensors) -> None:
+    """SURVEY §5.2 'DDP desync detector': every rank's parameters must be bitwise identical.
+
+    The fingerprints are computed on the host and compared over the c10d store (``hostcomm``), so
+    the check never creates a device communicator - on the nccl backend a ``dist.all_gather`` would
+    build ProcessGroupNCCL's RCCL communicator next to the engine's own."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
-    fp = params_fingerprint(tensors)
-    if dist.get_backend(group) != "nccl":
-        fp = fp.cpu()
-    allv = [torch.zeros_like(fp) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(allv, fp, group=group)
-    bad = [r for r, v in enumerate(allv) if not torch.equal(v, allv[0])]
+    from .hostcomm import get_hostcomm
+    allv = get_hostcomm().gather_strings(params_fingerprint_host(tensors).decode())
+    bad = [r for r, v in enumerate(allv) if v != allv[0]]
     if bad:
         raise RuntimeError(f"DDP desync: parameters on ranks {bad} differ from rank 0")
 

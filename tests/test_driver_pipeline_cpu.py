@@ -6,6 +6,8 @@ the evaluation of epoch e is only read back while epoch e+1 runs and e+1's sampl
 before that read-back."""
 import types
 
+import pytest
+
 import torch
 
 from pytorch_mnist_ddp_amd import driver
@@ -50,6 +52,9 @@ class _FakeTrainer:
 
     def synchronize(self):
         self.log.append(("sync",))
+
+    def check_errors(self):
+        self.log.append(("check",))
 
 
 def test_pipelined_epochs_keep_reference_print_and_rng_order(monkeypatch, capsys):
@@ -98,3 +103,34 @@ def test_pipelined_epochs_keep_reference_print_and_rng_order(monkeypatch, capsys
     assert [e[0] for e in ev] == ["train_enqueue", "train_enqueue", "eval_read", "train_enqueue", "eval_read",
                                   "eval_read"]
     assert [e[1] for e in log if e[0] == "lr"] == [1.0, 0.7, 0.49]
+    # fail fast: the device error flags are read at every epoch boundary, after that epoch's work
+    # (pipelined epochs used to surface a hand-off timeout only after the last epoch)
+    reads = [e[0] for e in log if e[0] in ("eval_read", "check")]
+    assert reads == ["eval_read", "check"] * 3
+
+
+def test_fatal_transport_hang_exits_without_teardown(monkeypatch, capsys):
+    """A TransportHang (a collective stuck on the device) in the real entry point leaves through
+    os._exit - the interpreter's teardown of RCCL / HIP objects would wait for the stuck kernel."""
+    from pytorch_mnist_ddp_amd.engine.trainer import TransportHang
+
+    def boom(*a, **k):
+        raise TransportHang("rank 0: RCCL schedule validation did not complete within 1 s")
+
+    exits = []
+
+    def fake_exit(code):
+        exits.append(code)
+        raise SystemExit(code)
+
+    monkeypatch.setattr(driver, "run", boom)
+    monkeypatch.setattr(driver.os, "_exit", fake_exit)
+    for entry in (driver.main_mnist_ddp, driver.main_mnist):
+        with pytest.raises(SystemExit):
+            entry([])
+    assert exits == [3, 3]
+    assert "FATAL: TransportHang" in capsys.readouterr().err
+    # an ordinary error still propagates (normal teardown)
+    monkeypatch.setattr(driver, "run", lambda *a, **k: (_ for _ in ()).throw(ValueError("x")))
+    with pytest.raises(ValueError):
+        driver.main_mnist_ddp([])

@@ -170,3 +170,27 @@ def test_bench_nccl_process_group_stays_lazy_w4(cuda_device, tmp_path):
     j = json.loads(lines[-1])
     assert j["n_gpus"] == 4 and j["params_in_sync"] is True and j["config"]["allreduce"] == "xgmi"
     assert "pg_init" in j["setup_phases_s"] and j["config"]["rccl_comms"] == 0
+
+
+@pytest.mark.timeout(300)
+def test_mnist_ddp_stdout_contract_nccl_check_sync_w2(cuda_device, tmp_path):
+    """``mnist_ddp.py`` at world 2 on the production ``nccl`` process group (lazy) with ``--check-sync``:
+    rank 0's stdout holds only the reference's line kinds (init line, train lines, test
+    lines, the timer - the transport line goes to stderr), and the per-epoch desync check runs over
+    the store: RCCL refuses two ranks on one GPU, so a torch collective on the nccl group (which
+    would build ProcessGroupNCCL's communicator) fails this test."""
+    W, n_train, B = 2, 8000, 200
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
+           "--batch-size", str(B), "--epochs", "2", "--synthetic", "--synthetic-train-size", str(n_train),
+           "--synthetic-test-size", "1000", "--allreduce", "xgmi", "--check-sync"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=tmp_path, env=_env())
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    kinds = (r"\| distributed init \(rank \d\): env://, local rank:\d, world size:2",
+             r"Train Epoch: \d+ \[\d+/\d+ \(\d+%\)\]\tLoss: [0-9.]+",
+             r"Test set: Average loss: [0-9.]+, Accuracy: \d+/\d+ \(\d+%\)",
+             r"Total cost time:[0-9.eE+-]+ ms", r"")
+    bad = [ln for ln in r.stdout.splitlines() if not any(re.fullmatch(k, ln) for k in kinds)]
+    assert not bad, bad[:10]
+    assert len(re.findall(r"Test set: Average loss", r.stdout)) == 2
+    assert "| gradient all-reduce: xgmi" in r.stderr
