@@ -417,6 +417,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     comm_info = {"allreduce": tr.allreduce,
                  "rccl_world": comm.world_size if comm is not None else None,
                  "rccl_comms": 1 if comm is not None else 0,
+                 "rccl_aborted": bool(comm.aborted) if comm is not None else None,
                  "allreduce_schedule_us": tr.allreduce_timings or None,
                  "transport_report": tr.transport_report or None,
                  "xgmi_validation": tr.xgmi_validation,

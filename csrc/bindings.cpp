@@ -228,18 +228,27 @@ PYBIND11_MODULE(_C, m) {
 
   // ---------------- communicator ----------------
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
-      .def(py::init([](py::bytes uid, int world, int rank, int device) {
+      .def(py::init([](py::bytes uid, int world, int rank, int device, double init_timeout_s) {
              std::string s = uid;
              std::shared_ptr<RcclComm> c;
              {
-               // ncclCommInitRank blocks for its bootstrap: let other Python threads run meanwhile
+               // the init waits for its bootstrap: let other Python threads run meanwhile
                // (distributed.PendingRcclComm overlaps it with data / model / trainer setup)
                py::gil_scoped_release nogil;
-               c = std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device);
+               c = std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device,
+                                              init_timeout_s);
              }
              return c;
            }),
-           py::arg("unique_id"), py::arg("world_size"), py::arg("rank"), py::arg("device"))
+           py::arg("unique_id"), py::arg("world_size"), py::arg("rank"), py::arg("device"),
+           py::arg("init_timeout_s") = 600.0)
+      .def("abort", [](RcclComm& c) {
+        py::gil_scoped_release nogil;
+        c.abort();
+      })
+      .def_property_readonly("aborted", &RcclComm::aborted)
+      .def_property_readonly("nonblocking", &RcclComm::nonblocking)
+      .def("async_error", &RcclComm::async_error)
       .def_static("available", &RcclComm::available)
       .def_static("version", &RcclComm::version)
       .def_static("unique_id", []() {
@@ -346,6 +355,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_rccl_handoff", &Engine::set_rccl_handoff)
+      .def("fault_hold", &Engine::fault_hold)
+      .def("fault_release", [](Engine& e, uintptr_t stream) { e.fault_release(S(stream)); })
       .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("schedule", &Engine::schedule)
       .def("reset_counters", &Engine::reset_counters, py::call_guard<py::gil_scoped_release>())

@@ -729,6 +729,19 @@ bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
 
 bool Engine::probe_stream_handoff(double timeout_s) { return probe_stream_pair(compute_, comm_stream_, timeout_s); }
 
+// fault injection (tests): the compute stream spins until fault_release (scratch counters
+// [12] released, [13] zero, [14] the hold's own timeout flag - never the engine's error flag [2])
+void Engine::fault_hold(double timeout_s) {
+  HIP_OK(hipMemsetAsync(sync_ + 12, 0, 4 * sizeof(int), compute_));
+  launch_stream_wait(sync_ + 12, sync_ + 13, 1, sync_ + 14, compute_, timeout_s);
+  HIP_OK(hipGetLastError());
+}
+
+void Engine::fault_release(hipStream_t s) {
+  launch_stream_signal(sync_ + 12, s);
+  HIP_OK(hipGetLastError());
+}
+
 std::pair<int, int> Engine::errors() const {
   int err = 0;
   HIP_OK(hipMemcpy(&err, sync_ + 2, sizeof(int), hipMemcpyDeviceToHost));

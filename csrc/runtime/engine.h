@@ -101,6 +101,10 @@ class Engine {
   // GPU_MAX_HW_QUEUES).  Each stream waits (spin kernel, `timeout_s`) for a signal enqueued on the
   // other afterwards; true if both hand-offs completed.  Eager, no graph; call before training.
   bool probe_stream_handoff(double timeout_s);
+  // fault injection (tests): hold the compute stream (a spinning one-workgroup kernel, `timeout_s`)
+  // until fault_release, launched on another stream, lets it go
+  void fault_hold(double timeout_s);
+  void fault_release(hipStream_t s);
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -165,7 +169,8 @@ class Engine {
   bool side_forked_ = false;        // comm stream already ordered after this chunk's start
   bool comm_sig3_pending_ = false;  // OVERLAP chain: the last conv2 update's [3] signal is owed
   int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
-                                    // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch
+                                    // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch,
+                                    // [12..15] fault-injection hold
   bool enq_main_ = true, enq_side_ = true;   // split capture: which stream's pass enqueue_step feeds
   bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
   std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null

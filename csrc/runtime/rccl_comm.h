@@ -20,7 +20,9 @@ class RcclComm {
   static std::string version();
   static std::vector<uint8_t> unique_id();
 
-  RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device);
+  // Non-blocking communicator where the RCCL exports ncclCommInitRankConfig / ncclCommAbort (the
+  // init is polled here and aborted after init_timeout_s), else a blocking ncclCommInitRank.
+  RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device, double init_timeout_s = 600.0);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -28,12 +30,22 @@ class RcclComm {
   // in-place sum all-reduce of fp32 (dtype 0) or bf16 (dtype 1) elements on `stream`
   void allreduce_sum(void* buf, int64_t count, int dtype, hipStream_t stream);
   void broadcast(void* buf, int64_t count, int dtype, int root, hipStream_t stream);
+  // ncclCommAbort: collectives stuck on the device return (RCCL's abort flag), the communicator is
+  // unusable afterwards (calls throw); idempotent
+  void abort();
+  bool aborted() const { return aborted_; }
+  bool nonblocking() const { return nonblocking_; }
+  int async_error() const;       // ncclCommGetAsyncError (0 = ncclSuccess, 7 = in progress)
   int world_size() const { return world_; }
   int rank() const { return rank_; }
 
  private:
+  // a call's result: ncclInProgress (non-blocking communicator) is polled to completion first
+  void finish(int r, const char* what, double timeout_s = 300.0);
+  void live(const char* what) const;
   void* comm_ = nullptr;
   int world_, rank_;
+  bool nonblocking_ = false, aborted_ = false;
 };
 
 // roctx ranges (no-ops when roctx is not loaded)

@@ -35,7 +35,16 @@ from .state import FLAG_NO_DROPOUT, ModelState
 # startup validation: timed replays of the chunk per candidate transport; host watchdog of the RCCL
 # schedule's replays (its first collectives also set up RCCL's channels and proxies)
 VALIDATE_TIMED = 2
-RCCL_WATCHDOG_S = float(os.environ.get("MNIST_AMD_RCCL_WATCHDOG", "120"))
+
+
+def rccl_watchdog_s() -> float:
+    """Host watchdog of the RCCL schedule's startup replays (``MNIST_AMD_RCCL_WATCHDOG``, s)."""
+    return float(os.environ.get("MNIST_AMD_RCCL_WATCHDOG", "120"))
+
+
+# after ncclCommAbort, how long the streams may take to drain (the engine's own device-counter holds
+# time out after 60 s, so a chunk whose RCCL kernels returned always drains within that)
+RCCL_DRAIN_S = 90.0
 
 
 def _fault_delay(kind: str, rank: int) -> float:
@@ -202,6 +211,7 @@ class FusedTrainer:
         self.xgmi_fuse = bool(xgmi_fuse)
         self.engine.set_xgmi_fuse_update(self.xgmi_fuse)
         self.transport_report: dict[str, dict] = {}           # candidate -> validation / us per step
+        self._fault_stall, self._fault_stream = False, None   # MNIST_AMD_FAULT=rccl_stall (tests)
         self.allreduce_timings: dict[str, float] = {}
         self.xgmi_validation = None
         self.allreduce = None
@@ -326,11 +336,49 @@ class FusedTrainer:
                 xgmi_broadcast_(x, self.ms.param, 0)
             elif self.comm is not None:
                 self.engine.broadcast_params(0)
-                self._wait_compute(RCCL_WATCHDOG_S, "RCCL parameter broadcast")
+                self._wait_compute(rccl_watchdog_s(), "RCCL parameter broadcast")
             else:
                 broadcast_(self.ms.param, 0)
             self.engine.refresh_shadows()
             torch.cuda.synchronize(self.device)
+
+    def _drain(self, timeout_s: float) -> bool:
+        """Both streams idle within ``timeout_s`` (events polled; never a blocking sync)."""
+        evs = []
+        for st in (self.compute, self.comm_stream):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+        t0 = time.perf_counter()
+        while not all(ev.query() for ev in evs):
+            if time.perf_counter() - t0 > timeout_s:
+                return False
+            time.sleep(0.001)
+        return True
+
+    def _abort_rccl(self, hang: "TransportHang | None" = None) -> float:
+        """Drop the RCCL candidate: ncclCommAbort (RCCL's device-side waits return), release an
+        injected test stall, wait for the streams to drain.  Returns the seconds that took; re-raises
+        ``hang`` (fatal) when the streams do not drain - then something is stuck for good."""
+        t0 = time.perf_counter()
+        if self.comm is not None:
+            self.comm.abort()
+        if self._fault_stall:
+            self.engine.fault_release(int(self._fault_stream.cuda_stream))
+            self._fault_stall = False
+        if not self._drain(RCCL_DRAIN_S):
+            if hang is not None:
+                raise hang
+            raise TransportHang(f"rank {self.rank}: the streams did not drain within {RCCL_DRAIN_S:.0f} s of "
+                                "aborting the RCCL communicator")
+        return time.perf_counter() - t0
+
+    def _drop_rccl(self) -> None:
+        """After a failed RCCL candidate: the engine no longer holds the (aborted) communicator and
+        the graphs captured with its collectives are never replayed."""
+        self.engine.attach_comm(None)
+        self.comm = None
+        self._graph_sets.pop("rccl", None)
 
     def _wait_compute(self, timeout_s: float, what: str) -> None:
         """Host watchdog on the compute stream (every chunk and step joins the comm stream into it)."""
@@ -349,12 +397,15 @@ class FusedTrainer:
         ``graph_steps`` steps that training replays (cached for training; eager steps when graphs are
         off), dropout off, on the live state, which is restored bit for bit afterwards.  Passes when
         no rank timed out (xGMI: STARTUP_TIMEOUT_S stage waits, read from device memory so the cached
-        graph picks up the run timeout afterwards; RCCL: a host watchdog of RCCL_WATCHDOG_S - a stuck
-        collective cannot be cancelled, so that raises TransportHang) and every rank holds the same
-        parameters afterwards.  Then the chunk is replayed ``VALIDATE_TIMED`` more times and timed:
-        the transport's µs per step (max over ranks) is the "auto" choice's measure.  The verdict is
-        collective and names every failing rank.  Fault injection for tests:
-        ``MNIST_AMD_FAULT=validate_delay:R:S`` holds rank R's replay back S seconds."""
+        graph picks up the run timeout afterwards; RCCL: a host watchdog of ``rccl_watchdog_s()``)
+        and every rank holds the same parameters afterwards.  A stuck RCCL replay is aborted
+        (ncclCommAbort: RCCL's device-side waits return, the streams drain) and the candidate dropped
+        on every rank - only streams that do not drain after that raise TransportHang (fatal).  Then
+        the chunk is replayed ``VALIDATE_TIMED`` more times and timed: the transport's µs per step
+        (max over ranks) is the "auto" choice's measure.  The verdict is collective and names every
+        failing rank.  Fault injection for tests: ``MNIST_AMD_FAULT=validate_delay:R:S`` holds rank
+        R's replay back S seconds; ``rccl_stall:R:S`` puts a device-side hold of up to S seconds in
+        front of rank R's first RCCL replay."""
         from ..parallel.distributed import (RUN_TIMEOUT_S, STARTUP_TIMEOUT_S, _max_over_ranks, gather_strings,
                                             params_fingerprint_equal)
         _t0 = time.perf_counter()
@@ -367,12 +418,19 @@ class FusedTrainer:
         idx = torch.arange(n * self.B, dtype=torch.int64) % max(1, len(train))
         delay = _fault_delay("validate_delay", self.rank)
         rccl = name == "rccl"
+        # MNIST_AMD_FAULT=rccl_stall:R:S (tests): rank R's first RCCL replay sits behind a device-side
+        # hold of up to S seconds - a collective that never completes, as seen by the host watchdog
+        stall = _fault_delay("rccl_stall", self.rank) if rccl else 0.0
         if self.xgmi is not None and not rccl:
             self.xgmi.set_timeout_seconds(STARTUP_TIMEOUT_S)
         why, us, result = "", None, None
 
         def run_chunk():
             eng.begin_epoch(self.seed, 0, 0, FLAG_NO_DROPOUT)
+            if stall and not self._fault_stall and not hung:
+                self._fault_stall = True
+                self._fault_stream = torch.cuda.Stream(device=self.device)
+                eng.fault_hold(stall)
             if self.use_graphs:
                 eng.replay(self._graph(n, self.B))
             else:
@@ -380,9 +438,10 @@ class FusedTrainer:
 
         def wait():
             if rccl:
-                self._wait_compute(RCCL_WATCHDOG_S, "RCCL schedule validation")
+                self._wait_compute(rccl_watchdog_s(), "RCCL schedule validation")
             eng.synchronize()                        # raises on a stage / hand-off timeout
 
+        hung = False                                 # this rank's RCCL replay was stuck and aborted
         try:
             self.upload_indices(idx)
             if self.use_graphs:
@@ -395,12 +454,22 @@ class FusedTrainer:
             result = ms.param.cpu()                  # (host checks: no torch GPU kernel at startup)
             if not torch.isfinite(result).all():
                 why = f"rank {self.rank}: non-finite parameters"
-        except TransportHang:
-            raise
+        except TransportHang as e:
+            if not rccl:
+                raise
+            # a stuck RCCL replay is no longer fatal: abort the communicator, let the streams drain,
+            # and report the candidate as failed (the xGMI candidate, validated first, stays usable)
+            took = self._abort_rccl(e)
+            hung = True
+            why = (f"rank {self.rank}: replay stuck for {rccl_watchdog_s():.0f} s, communicator aborted "
+                   f"after {rccl_watchdog_s() + took:.1f} s")
         except RuntimeError as e:
             why = f"rank {self.rank}: {e} (after {time.perf_counter() - _t0:.1f} s)"
         msgs = gather_strings(why, self.world)       # collective: every rank stops here together
         why = "; ".join(m for m in msgs if m)
+        if why and rccl and not hung:                # a peer's replay failed: this communicator goes too
+            self._abort_rccl()
+            hung = True
         if not why and self.world > 1 and not params_fingerprint_equal(result, world=self.world):
             why = "parameters differ across ranks after the validation chunk"
         if not why:
@@ -415,11 +484,19 @@ class FusedTrainer:
                 ev1.record(self.compute)
                 wait()
                 us = ev0.elapsed_time(ev1) * 1000.0 / (VALIDATE_TIMED * n)
-            except TransportHang:
-                raise
+            except TransportHang as e:
+                if not rccl:
+                    raise
+                took = self._abort_rccl(e)
+                hung = True
+                why = (f"rank {self.rank}: timed replay stuck for {rccl_watchdog_s():.0f} s, communicator aborted "
+                       f"after {rccl_watchdog_s() + took:.1f} s")
             except RuntimeError as e:
                 why = f"rank {self.rank}: timed replay: {e}"
             why = "; ".join(m for m in gather_strings(why, self.world) if m)
+            if why and rccl and not hung:
+                self._abort_rccl()
+                hung = True
             if not why:
                 us = _max_over_ranks(us, world=self.world)
         with torch.no_grad():
@@ -432,6 +509,8 @@ class FusedTrainer:
             self.xgmi.set_timeout_seconds(RUN_TIMEOUT_S)
         torch.cuda.synchronize(self.device)
         self.setup.add(f"validate.{name}", time.perf_counter() - _t0)
+        if hung:
+            self._drop_rccl()
         if why:
             return False, why, None
         how = f"graph replay of the {n}-step training chunk" if self.use_graphs else f"{n} eager steps"

@@ -115,3 +115,37 @@ def test_world_gt1_without_transport_refuses(cuda_device, monkeypatch):
     train = load_mnist(train=True, synthetic_data=True, synthetic_size=512, verbose=False)
     with pytest.raises(RuntimeError, match="no RCCL communicator"):
         FusedTrainer(ms, train, None, 64, 128, num_samples=512, world_size=2, rank=0, allreduce="xgmi")
+
+
+def test_stuck_rccl_candidate_is_aborted_and_xgmi_kept(cuda_device, monkeypatch):
+    """--allreduce auto where the RCCL candidate's validation replay never completes (an injected
+    device-side stall in front of it, MNIST_AMD_FAULT=rccl_stall): the host watchdog fires, the RCCL
+    communicator is aborted (ncclCommAbort) and dropped, the streams drain, and training continues on
+    the already-validated xGMI schedule - bitwise equal to --allreduce xgmi, no fatal exit."""
+    import torch
+    import torch.distributed as dist
+    from conftest import init_world1_pg
+    from pytorch_mnist_ddp_amd.parallel.distributed import create_rccl_comm
+    init_world1_pg("nccl", cuda_device)
+    try:
+        idx = torch.randperm(2000, generator=torch.Generator().manual_seed(4))
+        monkeypatch.setenv("MNIST_AMD_FAULT", "rccl_stall:0:60")
+        monkeypatch.setenv("MNIST_AMD_RCCL_WATCHDOG", "3")
+        comm = create_rccl_comm(1, 0, 0)
+        assert comm.nonblocking                      # ncclCommInitRankConfig(blocking = 0)
+        ms, t = _world1_trainer(cuda_device, comm, allreduce="auto", probe_world1=True)
+        rep = t.transport_report
+        assert rep["xgmi"]["ok"] and not rep["rccl"]["ok"], rep
+        assert "communicator aborted after" in rep["rccl"]["validation"], rep
+        assert comm.aborted and t.comm is None and t.allreduce == "xgmi"
+        assert ms.get_step() == 0
+        t.train_epoch(1, idx)
+        t.synchronize()
+        got = (ms.param.clone(), t.loss_log.clone())
+        monkeypatch.delenv("MNIST_AMD_FAULT")
+        ms2, t2 = _world1_trainer(cuda_device, None, allreduce="xgmi")
+        t2.train_epoch(1, idx)
+        t2.synchronize()
+        assert torch.equal(got[0], ms2.param) and torch.equal(got[1], t2.loss_log)
+    finally:
+        dist.destroy_process_group()
