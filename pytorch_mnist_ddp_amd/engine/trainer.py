@@ -34,7 +34,11 @@ from .state import FLAG_NO_DROPOUT, ModelState
 
 # startup validation: timed replays of the chunk per candidate transport; host watchdog of the RCCL
 # schedule's replays (its first collectives also set up RCCL's channels and proxies)
-VALIDATE_TIMED = 2
+# with two candidate transports ("auto" at world > 1) the validation replay is followed by this many
+# timed replays (the choice's measure, without first-replay costs); a single candidate is timed on
+# its validation replay alone (the startup inside the reference timer: each 50-step replay is ~15 ms
+# at world 2 in the one-GPU rehearsal)
+VALIDATE_TIMED = 1
 
 
 def rccl_watchdog_s() -> float:
@@ -257,7 +261,9 @@ class FusedTrainer:
         self.engine.set_rccl_handoff(handoff)
         if want_x:
             with self.setup.phase("xgmi_comm"):
-                x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel())
+                sub = {}
+                x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel(), timings=sub)
+                self.setup.add_info("xgmi_comm_steps_s", sub)
             if x is not None and not handoff:
                 if self.rank == 0:
                     print("[engine] compute/comm streams share a hardware queue: no xGMI schedule", flush=True)
@@ -273,7 +279,8 @@ class FusedTrainer:
             self.engine.set_schedule(C.SCHED_XGMI)
             self.xgmi = x
             self._use_graph_set("xgmi")
-            ok, why, us = self._validate("xgmi", train)
+            both = want_r                            # two candidates: time each beyond its first replay
+            ok, why, us = self._validate("xgmi", train, timed=both)
             if not ok and "differ" in why:
                 # wrong sums, no timeout: retry with system-scope release / acquire fences around every
                 # stage flag (the ordering rules R1-R4 of xgmi_allreduce.hip assume a memory model the
@@ -283,7 +290,7 @@ class FusedTrainer:
                 x.set_fences(True)
                 self._graph_sets["xgmi"] = {}
                 self._use_graph_set("xgmi")
-                ok, why2, us = self._validate("xgmi", train)
+                ok, why2, us = self._validate("xgmi", train, timed=both)
                 why = why2 if ok else f"{why}; fenced: {why2}"
             self.transport_report["xgmi"] = {"ok": ok, "validation": why, "us_per_step": us,
                                              "ordering": x.ordering}
@@ -297,7 +304,7 @@ class FusedTrainer:
         if want_r:
             self.engine.set_schedule(C.SCHED_RCCL)
             self._use_graph_set("rccl")
-            ok, why, us = self._validate("rccl", train)
+            ok, why, us = self._validate("rccl", train, timed=want_x)
             self.transport_report["rccl"] = {"ok": ok, "validation": why, "us_per_step": us}
         valid = {k: v["us_per_step"] for k, v in self.transport_report.items() if v.get("ok")}
         self.allreduce_timings = {k: round(v["us_per_step"], 2) for k, v in self.transport_report.items()
@@ -392,7 +399,7 @@ class FusedTrainer:
             time.sleep(0.0002)
 
     # ------------------------------------------------------------------ startup validation
-    def _validate(self, name: str, train: MNISTData) -> tuple[bool, str, float | None]:
+    def _validate(self, name: str, train: MNISTData, timed: bool = True) -> tuple[bool, str, float | None]:
         """Run the selected production schedule before training starts: the captured chunk graph of
         ``graph_steps`` steps that training replays (cached for training; eager steps when graphs are
         off), dropout off, on the live state, which is restored bit for bit afterwards.  Passes when
@@ -401,8 +408,9 @@ class FusedTrainer:
         and every rank holds the same parameters afterwards.  A stuck RCCL replay is aborted
         (ncclCommAbort: RCCL's device-side waits return, the streams drain) and the candidate dropped
         on every rank - only streams that do not drain after that raise TransportHang (fatal).  Then
-        the chunk is replayed ``VALIDATE_TIMED`` more times and timed: the transport's µs per step
-        (max over ranks) is the "auto" choice's measure.  The verdict is collective and names every
+        (``timed``: two candidates) the chunk is replayed ``VALIDATE_TIMED`` more times and timed: the
+        transport's µs per step (max over ranks) is the "auto" choice's measure; a single candidate is
+        timed on its validation replay.  The verdict is collective and names every
         failing rank.  Fault injection for tests: ``MNIST_AMD_FAULT=validate_delay:R:S`` holds rank
         R's replay back S seconds; ``rccl_stall:R:S`` puts a device-side hold of up to S seconds in
         front of rank R's first RCCL replay."""
@@ -449,8 +457,12 @@ class FusedTrainer:
             torch.cuda.synchronize(self.device)
             if delay:
                 time.sleep(delay)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(self.compute)
             run_chunk()
+            ev1.record(self.compute)
             wait()
+            us = ev0.elapsed_time(ev1) * 1000.0 / n
             result = ms.param.cpu()                  # (host checks: no torch GPU kernel at startup)
             if not torch.isfinite(result).all():
                 why = f"rank {self.rank}: non-finite parameters"
@@ -472,7 +484,9 @@ class FusedTrainer:
             hung = True
         if not why and self.world > 1 and not params_fingerprint_equal(result, world=self.world):
             why = "parameters differ across ranks after the validation chunk"
-        if not why:
+        if not why and not timed:
+            us = _max_over_ranks(us, world=self.world)
+        elif not why:
             # timed replays of the same chunk (state need not be restored in between: the numbers do
             # not matter, the schedule's time does)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -514,7 +528,8 @@ class FusedTrainer:
         if why:
             return False, why, None
         how = f"graph replay of the {n}-step training chunk" if self.use_graphs else f"{n} eager steps"
-        return True, f"ok ({how}, ranks bitwise equal, {VALIDATE_TIMED} timed replays)", us
+        clock = f"{VALIDATE_TIMED} timed replay(s)" if timed else "timed on the validation replay"
+        return True, f"ok ({how}, ranks bitwise equal, {clock})", us
 
     def reset_model(self, module) -> None:
         """Start over from ``module``'s parameters with fresh optimizer state (zero Adadelta

@@ -234,7 +234,8 @@ def ranks_share_a_device(device) -> bool:
 
 
 def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 3,
-                     verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None):
+                     verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None,
+                     timings: dict | None = None):
     """Direct xGMI all-reduce communicator over ``numel`` floats (csrc/runtime/xgmi_comm.h).
 
     The communicator owns its input / output buffers (``x.grad_in`` / ``x.grad_out``: zero-copy fp32
@@ -244,7 +245,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     agree on the outcome.  Returns the communicator, or ``None`` on every rank when any rank failed
     to map its peers or to verify (callers then keep the RCCL all-reduce).  ``co_ranks`` (default:
     measured with :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning
-    workgroups are resident."""
+    workgroups are resident.  ``timings`` (optional dict) receives host seconds per sub-step
+    (co_ranks, alloc, exchange, connect, verify): the N > 1 startup budget."""
     from torch.utils.dlpack import from_dlpack
 
     from ..ops import native
@@ -254,19 +256,33 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
         tag = str(_xgmi_seq)
     _xgmi_seq += 1
     dev = torch.device(device)
+    tm = timings if timings is not None else {}
+    t = time.perf_counter()
+
+    def lap(name):
+        nonlocal t
+        now = time.perf_counter()
+        tm[name] = round(tm.get(name, 0.0) + now - t, 4)
+        t = now
+
     if co_ranks is None:
         co_ranks = ranks_per_device(dev, world_size)
+    lap("co_ranks")
     x = None
     try:
         x = C.XgmiComm(world_size, rank, dev.index or 0, int(numel), channels, oneshot_max, co_ranks)
         x.grad_in = from_dlpack(x.dlpack("in"))
         x.grad_out = from_dlpack(x.dlpack("out"))
+        lap("alloc")
         if world_size > 1:
             store = dist.distributed_c10d._get_default_store()
             store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
             keys = [f"{_XGMI_KEY}/{tag}/{q}" for q in range(world_size)]
             store.wait(keys, timedelta(minutes=5))
-            x.connect([store.get(k) for k in keys])
+            recs = [store.get(k) for k in keys]
+            lap("exchange")
+            x.connect(recs)
+            lap("connect")
         ok = True
     except RuntimeError as e:
         print(f"[xgmi] rank {rank}: setup failed ({e})", flush=True)
@@ -274,8 +290,10 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     if not _all_ok(ok, world=world_size):
         release_xgmi_comm(x, world_size)
         return None
+    lap("agree")
     if verify:
         ok = _verify_xgmi(x, world_size, rank, x.grad_in, x.grad_out, channels)
+        lap("verify")
         if not _all_ok(ok, world=world_size):
             if rank == 0:
                 print("[xgmi] self-test failed: keeping the RCCL all-reduce", flush=True)
