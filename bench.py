@@ -197,7 +197,7 @@ def parse_args(argv=None):
     ap.add_argument("--force-comm", action="store_true",
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
-                    help="bf16: the bf16-MFMA step (default); fp32: the fp32 step (f32_net.hip, RCCL at N > 1)")
+                    help="bf16: the bf16-MFMA step (default); fp32: the fp32 step (f32_net.hip; RCCL or xGMI at N > 1)")
     ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
                     help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernels, or "
                          "auto (validate and time both production schedules at startup, keep the faster)")

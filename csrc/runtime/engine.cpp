@@ -121,7 +121,6 @@ void Engine::attach_comm(std::shared_ptr<RcclComm> comm) {
 }
 
 void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
-  if (x && f32_) throw std::runtime_error("engine: the fp32 step has no xGMI schedule (use RCCL)");
   if (x && x->world_size() != world_) throw std::runtime_error("xgmi world size mismatch");
   if (x && x->world_size() > 1 && !x->connected()) throw std::runtime_error("xgmi communicator not connected");
   if (x && x->numel() != PARAM_TOTAL) throw std::runtime_error("xgmi communicator must cover the flat gradient");
@@ -137,8 +136,7 @@ void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
 }
 
 void Engine::set_schedule(int s) {
-  if (f32_ && s != SERIAL && s != RCCL)
-    throw std::runtime_error("engine: the fp32 step runs the SERIAL or RCCL schedule only");
+  if (f32_ && s == OVERLAP) throw std::runtime_error("engine: the fp32 step has no OVERLAP schedule");
   if (s == SERIAL || s == OVERLAP) {
     if (world_ != 1 || comm_ || xgmi_)
       throw std::runtime_error("engine: the single-GPU schedules need world size 1 and no transport attached");
@@ -492,10 +490,17 @@ void Engine::enqueue_step_f32(int batch) {
   launch_f32_backward(a, batch, compute_);
   phase_end();
   phase_begin("allreduce+update");
-  if (sched_ == RCCL) comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
   AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, buf_.state};
-  launch_adadelta(ad, ADA_ALL, compute_);
+  if (sched_ == XGMI) {
+    // the whole flat gradient in one two-shot xGMI all-reduce (the producers wrote x->in()) with the
+    // Adadelta step fused into its gather phase (same per-element math as the separate update)
+    ad.grad = xgmi_->out();
+    xgmi_->allreduce(XGMI_CH_FC, 0, PARAM_TOTAL, compute_, &ad);
+  } else {
+    if (sched_ == RCCL) comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
+    launch_adadelta(ad, ADA_ALL, compute_);
+  }
   phase_end();
 }
 

@@ -70,7 +70,8 @@ struct EngineBuffers {
 class Engine {
  public:
   // fp32: the --dtype fp32 step (f32_net.hip: f32-input MFMA GEMMs, fp32 activations); SERIAL
-  // (single GPU) or RCCL (one all-reduce of the whole gradient before the update) schedules only
+  // (single GPU), RCCL (one all-reduce of the whole gradient before the update) or XGMI (one two-shot
+  // xGMI all-reduce of the whole gradient with the update fused) schedules, all on the compute stream
   Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipStream_t compute,
          hipStream_t comm, int world_size, float rho, float eps, float weight_decay, bool fp32 = false);
   ~Engine();
@@ -143,7 +144,7 @@ class Engine {
   void enqueue_step(int batch, bool last);
   void enqueue_step_f32(int batch);
   F32Step f32_args() const;
-  bool side_schedule() const { return sched_ == OVERLAP || sched_ == XGMI; }
+  bool side_schedule() const { return !f32_ && (sched_ == OVERLAP || sched_ == XGMI); }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
   void reset_host_state();

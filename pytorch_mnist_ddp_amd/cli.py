@@ -13,7 +13,7 @@ behaviour):
 * ``--engine {fused,module}``: native step engine vs the reference's module-level loop.
 * ``--dtype {bf16,fp32}``: bf16 = the MI355X kernels (bf16 MFMA operands, fp32 accumulation,
   fp32 master weights / optimizer state / gradient all-reduce); fp32 = the reference's precision:
-  the fused engine's fp32 step (csrc/kernels/f32_net.hip, f32-input MFMA GEMMs; RCCL at N > 1),
+  the fused engine's fp32 step (csrc/kernels/f32_net.hip, f32-input MFMA GEMMs; RCCL or xGMI at N > 1),
   or stock torch fp32 ops with ``--engine module``.
 * ``--dist-backend``: process-group backend override (``gloo`` + ``--allreduce xgmi`` needs no
   RCCL at all, e.g. several ranks on one GPU).

@@ -207,8 +207,6 @@ class FusedTrainer:
             allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
         if allreduce not in ("rccl", "xgmi", "auto"):
             raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
-        if self.fp32 and allreduce == "xgmi":
-            raise ValueError("the fp32 step all-reduces over RCCL only (--allreduce rccl or auto)")
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
         self.xgmi, self.grad_out = None, None
@@ -251,8 +249,8 @@ class FusedTrainer:
         from ..parallel.distributed import create_xgmi_comm, release_xgmi_comm
         C = self.C
         self.overlap = False
-        want_x = not self.fp32 and (allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
-                                                            and (self.world > 1 or probe_world1)))
+        want_x = allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
+                                         and (self.world > 1 or probe_world1))
         want_r = comm is not None and allreduce in ("rccl", "auto")
         x = None
         # compute / comm streams on distinct hardware queues: the device-counter hand-offs of the

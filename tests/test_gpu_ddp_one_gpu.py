@@ -194,3 +194,20 @@ def test_mnist_ddp_stdout_contract_nccl_check_sync_w2(cuda_device, tmp_path):
     assert not bad, bad[:10]
     assert len(re.findall(r"Test set: Average loss", r.stdout)) == 2
     assert "| gradient all-reduce: xgmi" in r.stderr
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W", [2, 8])
+def test_bench_fp32_xgmi_rehearsal(cuda_device, tmp_path, W):
+    """The fp32 step (the reference's precision) on the xGMI transport: ``bench.py --dtype fp32`` at
+    W ranks on one GPU (gloo + --allreduce xgmi, no RCCL) trains with every rank's parameters bitwise
+    equal, validated by replaying the captured fp32 chunk."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(W), "--steps", "10", "--warmup", "2",
+           "--no-full-run", "--dist-backend", "gloo", "--allreduce", "xgmi", "--dtype", "fp32",
+           "--batch-size", "64", "--graph-steps", "5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=tmp_path, env=_env())
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    j = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j["n_gpus"] == W and j["dtype"] == "fp32" and j["params_in_sync"] is True
+    assert j["config"]["allreduce"] == "xgmi" and j["config"]["schedule"] == "xgmi"
+    assert j["config"]["xgmi_validation"].startswith("ok (graph replay")
