@@ -267,6 +267,9 @@ PYBIND11_MODULE(_C, m) {
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm", py::dynamic_attr())
       .def(py::init([](int world, int rank, int device, int64_t numel, int channels, int64_t oneshot_max,
                        int co_ranks, double budget) {
+             // device allocation + memsets + a device sync: other Python threads run meanwhile
+             // (distributed.PendingXgmiComm overlaps the setup with the main thread's)
+             py::gil_scoped_release nogil;
              return std::make_shared<XgmiComm>(world, rank, device, numel, channels, oneshot_max, co_ranks,
                                                budget);
            }),
@@ -298,6 +301,7 @@ PYBIND11_MODULE(_C, m) {
           std::string s = r;
           v.emplace_back(s.begin(), s.end());
         }
+        py::gil_scoped_release nogil;   // one IPC import per peer
         c.connect(v);
       })
       .def("allreduce", [](XgmiComm& c, int channel, int64_t offset, int64_t count, uintptr_t stream) {

@@ -129,7 +129,7 @@ class FusedTrainer:
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
                  two_buckets: bool = True, allreduce: str | None = None, overlap: bool = True,
-                 xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False):
+                 xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False, xgmi_pending=None):
         C = native.load()
         self.C, self.ms = C, mstate
         # host seconds per setup phase (engine, xgmi_comm, stream_probe, validate.<transport>,
@@ -219,6 +219,7 @@ class FusedTrainer:
         self.allreduce = None
         import torch.distributed as _dist
         ddp = comm is not None or world_size > 1 or (allreduce == "xgmi" and _dist.is_initialized())
+        self._xgmi_pending = xgmi_pending        # distributed.PendingXgmiComm started by the caller
         if not ddp:
             self._setup_single_gpu(overlap)
         else:
@@ -257,10 +258,21 @@ class FusedTrainer:
         # XGMI schedule and of the RCCL schedule's fc update need it (one probe, every rank)
         handoff = self._probe_streams() if (want_x or (want_r and two_buckets)) else False
         self.engine.set_rccl_handoff(handoff)
-        if want_x:
+        pending, self._xgmi_pending = self._xgmi_pending, None
+        if pending is not None and not want_x:      # started by the caller, not a candidate after all
             with self.setup.phase("xgmi_comm"):
-                sub = {}
-                x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel(), timings=sub)
+                x = pending.result()
+                if x is not None:
+                    release_xgmi_comm(x, self.world)
+                x = None
+        if want_x:
+            with self.setup.phase("xgmi_comm"):   # (with a pending setup: the wait for its helper thread)
+                if pending is not None:
+                    x = pending.result()
+                    sub = dict(pending.timings, helper_thread_s=round(pending.seconds or 0.0, 4))
+                else:
+                    sub = {}
+                    x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel(), timings=sub)
                 self.setup.add_info("xgmi_comm_steps_s", sub)
             if x is not None and not handoff:
                 if self.rank == 0:

@@ -302,6 +302,43 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     return x
 
 
+class PendingXgmiComm:
+    """:func:`create_xgmi_comm` on a helper thread (its own host-collective channel), started as soon
+    as the HIP runtime is up: the buffer allocation, IPC export / exchange / peer mapping and the
+    self-test overlap the model build, the DDP wrap and the trainer's buffers on the main thread
+    (the N > 1 startup inside the reference timer).  ``result()`` joins and returns
+    the communicator (or None when it could not be built / verified, as create_xgmi_comm);
+    ``seconds`` / ``timings`` are the helper's."""
+
+    def __init__(self, world_size: int, rank: int, device, numel: int):
+        from .hostcomm import channel
+        self._hc = channel("xgmi_setup")
+        self._args = (world_size, rank, torch.device(device), int(numel))
+        self._comm, self._err, self.seconds, self.timings = None, None, None, {}
+        self._t = threading.Thread(target=self._run, name="xgmi-setup", daemon=True)
+        self._t.start()
+
+    def _run(self):
+        from .hostcomm import use_channel
+        t0 = time.perf_counter()
+        try:
+            world, rank, dev, numel = self._args
+            torch.cuda.set_device(dev)
+            with use_channel(self._hc):
+                self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings)
+        except BaseException as e:  # noqa: BLE001 - re-raised in result()
+            self._err = e
+        self.seconds = time.perf_counter() - t0
+
+    def result(self, timeout_s: float = 600.0):
+        self._t.join(timeout_s)
+        if self._t.is_alive():
+            raise RuntimeError(f"xGMI communicator setup did not finish within {timeout_s:.0f} s")
+        if self._err is not None:
+            raise self._err
+        return self._comm
+
+
 def release_xgmi_comm(x, world: int | None = None) -> None:
     """Collective teardown of an xGMI communicator: every rank unmaps its peers, then (host barrier)
     the buffers may be recycled by a later communicator of the same shape.  Call on every rank;

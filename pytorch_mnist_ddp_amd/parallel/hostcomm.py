@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import os
 import struct
+import threading
 import time
 from datetime import timedelta
 
@@ -38,13 +39,14 @@ class HostComm:
         return f"{self.prefix}/{seq}/{rank}"
 
     def abort(self, msg: str) -> None:
-        """Tell every rank's pending and future collectives that this job failed (``msg``)."""
+        """Tell every rank's pending and future collectives that this job failed (``msg``) - on
+        every channel (one abort key for all prefixes)."""
         if self.world > 1:
-            self.store.set(f"{self.prefix}/abort", str(msg).encode())
+            self.store.set(f"{_PREFIX}/abort", str(msg).encode())
 
     def _wait(self, keys: list[str], timeout_s: float) -> None:
         deadline = time.monotonic() + timeout_s
-        abort_key = f"{self.prefix}/abort"
+        abort_key = f"{_PREFIX}/abort"
         while True:
             try:
                 self.store.wait(keys, timedelta(seconds=min(1.0, max(0.05, deadline - time.monotonic()))))
@@ -102,15 +104,44 @@ class _World1(HostComm):
 
 _default: HostComm | None = None
 _default_pg = None
+_tls = threading.local()
+
+
+def channel(name: str) -> HostComm:
+    """A separate sequence of host collectives (own key prefix) over the default store, for a helper
+    thread whose collectives run concurrently with the main thread's: every rank issues each
+    channel's collectives in the same order, but the interleaving ACROSS channels differs between
+    ranks, so the two must never share one sequence counter."""
+    store = dist.distributed_c10d._get_default_store()
+    return HostComm(store, dist.get_rank(), dist.get_world_size(), prefix=f"{_PREFIX}/{name}")
+
+
+class use_channel:
+    """``with use_channel(hc):`` - this thread's get_hostcomm() returns ``hc``."""
+
+    def __init__(self, hc: HostComm):
+        self.hc = hc
+
+    def __enter__(self):
+        self.prev = getattr(_tls, "hc", None)
+        _tls.hc = self.hc
+        return self.hc
+
+    def __exit__(self, *exc):
+        _tls.hc = self.prev
 
 
 def get_hostcomm(world: int | None = None) -> HostComm:
     """The process's host collectives over the default process group's store (world 1 when no
     process group is initialised, or when the caller's job is a world of 1 - e.g. a single-rank
-    reference run inside a multi-rank tool's process group)."""
+    reference run inside a multi-rank tool's process group); a thread inside ``use_channel`` gets
+    its channel."""
     global _default, _default_pg
     if world == 1 or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return _World1()
+    hc = getattr(_tls, "hc", None)
+    if hc is not None:
+        return hc
     pg = dist.distributed_c10d._get_default_group()
     if _default is None or _default_pg is not pg:
         store = dist.distributed_c10d._get_default_store()

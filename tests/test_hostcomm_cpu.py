@@ -56,6 +56,32 @@ def _hc_worker(rank, world, port, q, mode):
             live = sum(store.check([hc._key(s, rank)]) for s in range(hc.seq))
             out.append(live)
             q.put((rank, out))
+        elif mode == "channels":
+            # a helper thread's channel and the main thread interleave their collectives differently
+            # on every rank (random sleeps): each sequence still pairs up with its peers'
+            import random
+            import threading
+            from pytorch_mnist_ddp_amd.parallel.hostcomm import channel, use_channel
+            rnd = random.Random(rank)
+            side = {}
+
+            def helper():
+                with use_channel(channel("helper")):
+                    got = []
+                    for i in range(8):
+                        time.sleep(rnd.random() * 0.02)
+                        got.append(get_hostcomm().gather_strings(f"h{i}r{rank}"))
+                    side["h"] = got
+
+            t = threading.Thread(target=helper)
+            t.start()
+            main = []
+            for i in range(8):
+                time.sleep(rnd.random() * 0.02)
+                main.append(hc.gather_strings(f"m{i}r{rank}"))
+            t.join(60)
+            q.put((rank, (main, side.get("h"))))
+            time.sleep(2.0)
         else:                                         # rank 1 fails, the others wait in a collective
             if rank == 1:
                 time.sleep(1.0)
@@ -103,3 +129,11 @@ def test_host_collective_abort_reaches_waiting_ranks():
         dt, msg = res[r].split("|", 1)
         assert "job aborted by a peer: rank 1 failed in trainer: boom" in msg
         assert float(dt) < 20.0                       # not the 120 s timeout
+
+
+def test_host_collective_channels_are_independent():
+    res = _run(3, "channels")
+    for r in range(3):
+        main, helper = res[r]
+        assert main == [[f"m{i}r{q}" for q in range(3)] for i in range(8)]
+        assert helper == [[f"h{i}r{q}" for q in range(3)] for i in range(8)]
