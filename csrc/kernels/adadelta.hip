@@ -106,6 +106,8 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
   Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
   int bid = blockIdx.x;
   if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (a.signal_start && bid == 0 && threadIdx.x == 0)      // the previous launch on the stream is done
+    __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   bool done = false;
   if (region == ADA_FC && gridDim.x < FC1_TILES + 1) {
     // fc bucket on fewer workgroups than tiles (grid-stride): the overlapped single-GPU / RCCL update

@@ -69,8 +69,10 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = k_lo; k0 < k_hi; k0 += BK) {
-    float ra[EA], rb[EB];
+  // register prefetch: the next k-tile's gathers are issued before this tile's MFMAs, so their
+  // latency hides under the matrix work instead of sitting between the two barriers
+  float ra[EA], rb[EB];
+  auto load = [&](int k0) {
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int x = tid + 256 * e;
@@ -85,7 +87,10 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
       const int gn = n0 + n, gk = k0 + k;
       rb[e] = (gn < p.N && gk < k_hi) ? p.b(gk, gn) : 0.0f;
     }
-    __syncthreads();                              // the previous k-tile's reads are done
+  };
+  if (k_lo < k_hi) load(k_lo);
+  for (int k0 = k_lo; k0 < k_hi; k0 += BK) {
+    lds_barrier();                                // the previous k-tile's reads are done
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int x = tid + 256 * e;
@@ -96,7 +101,8 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
       const int x = tid + 256 * e;
       Bs[P::B_KF ? x % BK : x / BN][P::B_KF ? x / BK : x % BN] = rb[e];
     }
-    __syncthreads();
+    lds_barrier();
+    if (k0 + BK < k_hi) load(k0 + BK);            // in flight under the MFMAs below
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       float av[2], bv[2];
