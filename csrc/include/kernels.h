@@ -221,6 +221,8 @@ struct F32Step {
   // workspace (fp32 unless noted)
   float* w2fwd;               // [9][32][64] conv2 weight, forward B operand
   float* w2bwd;               // [9][64][32] conv2 weight, input-gradient B operand
+  float* w1p;                 // [128][144][64] fc1 weight with its input index position-major
+                              // (pooled position, channel): the fc1 input-gradient B operand
   float* a1;                  // [B][26][26][32] ReLU(conv1); then the conv1 pre-activation gradient
   float* y2;                  // [B][24][24][64] conv2 pre-activation; then its gradient
   float* p;                   // [B][9216] pooled + dropout, torch flatten order

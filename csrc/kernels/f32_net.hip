@@ -181,12 +181,16 @@ struct PFc1W {
 };
 
 // fc1 input gradient dp[b][j] = sum_o dz1[b][o] w1[o][j], through dropout-1 and the max-pool +
-// ReLU backward in the epilogue: the 2 x 2 window's four conv2-output gradients (one non-zero)
+// ReLU backward in the epilogue: the 2 x 2 window's four conv2-output gradients (one non-zero).
+// N runs position-major (n = pos * 64 + c, B operand = the w1p copy): the 16 consecutive columns of
+// an MFMA output row are 16 channels of one pixel, so each of the four NHWC dy2 stores is a 64-byte
+// run (in torch order the lanes were 2 pixels = 512 B apart: 29.5 MB of scattered 4-byte stores,
+// 79.5 us of a 555 us step at B = 200)
 struct PFc1X {
   static constexpr bool A_KF = true, B_KF = false;
   int M, N, K, kc;
   const float* dz1;
-  const float* w1;
+  const float* w1p;
   const uint8_t* pm;
   float* dy2;
   const StepState* st;
@@ -196,10 +200,10 @@ struct PFc1X {
     dscale = (s->flags & STEP_FLAG_NO_DROPOUT) ? 1.0f : (1.0f / KEEP1);
   }
   __device__ float a(int m, int k) const { return dz1[(int64_t)m * NH + k]; }
-  __device__ float b(int k, int n) const { return w1[(int64_t)k * NFLAT + n]; }
+  __device__ float b(int k, int n) const { return w1p[(int64_t)k * NFLAT + n]; }
   __device__ void put(int m, int n, float v, int) const {
-    const int c = n / NPOOL, pos = n - c * NPOOL, py = pos / HP, px = pos - py * HP;
-    const uint32_t fl = pm[(int64_t)m * NFLAT + n];
+    const int c = n & (C2 - 1), pos = n >> 6, py = pos / HP, px = pos - py * HP;
+    const uint32_t fl = pm[(int64_t)m * NFLAT + c * NPOOL + pos];
     const float g = ((fl & 12u) == 12u) ? v * dscale : 0.0f;    // kept by dropout, ReLU alive
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -250,35 +254,24 @@ struct PConv2X {
   }
 };
 
-// conv1 weight + bias gradient, split-K over the B*676 pixels:
-// part[z][c][t] = sum_m da1[m][c] x_patch[m][t] (t < 9), sum_m da1[m][c] (t = 9)
-struct PConv1W {
-  static constexpr bool A_KF = false, B_KF = true;
-  int M, N, K, kc;
-  const float* da1;
-  F32Step s;
-  int step;
-  float* part;
-  __device__ void prepare() { step = state_of(s)->step; }
-  __device__ float a(int m, int k) const { return da1[(int64_t)k * C1 + m]; }
-  __device__ float b(int k, int n) const {
-    if (n == 9) return 1.0f;
-    const int b = k / NPIX1, pix = k - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
-    const int ky = n / 3, kx = n - 3 * ky;
-    return normalize_u8_alu(image_row(s, step, b)[(iy + ky) * IMG + ix + kx]);
-  }
-  __device__ void put(int m, int n, float v, int z) const { part[((int64_t)z * C1 + m) * 10 + n] = v; }
-};
-
 // ---------------------------------------------------------------------------------------------
-// conv2 weight in the two GEMM B layouts: w2fwd[tap][ci][co], w2bwd[tap][co][ci]
-__global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a) {
+// conv2 weight in the two GEMM B layouts: w2fwd[tap][ci][co], w2bwd[tap][co][ci] ...
+// ... and fc1.weight position-major for the fc1 input gradient: w1p[o][pos][c] = w1[o][c * 144 + pos]
+// (threads walk the destination: coalesced 16-B stores, gathered 4-B loads from L2)
+__global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a, int train) {
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= C2 * K2) return;
-  const int co = t / K2, r = t - co * K2, ci = r / 9, tap = r - 9 * ci;   // torch [co][ci][ky][kx]
-  const float w = a.param[OFF_CONV2_W + t];
-  a.w2fwd[(tap * C1 + ci) * C2 + co] = w;
-  a.w2bwd[(tap * C2 + co) * C1 + ci] = w;
+  if (t < C2 * K2) {
+    const int co = t / K2, r = t - co * K2, ci = r / 9, tap = r - 9 * ci;   // torch [co][ci][ky][kx]
+    const float w = a.param[OFF_CONV2_W + t];
+    a.w2fwd[(tap * C1 + ci) * C2 + co] = w;
+    a.w2bwd[(tap * C2 + co) * C1 + ci] = w;
+  }
+  const int u = t - ((C2 * K2 + 255) / 256) * 256;              // the w1p blocks follow
+  if (!train || u < 0 || u >= NH * NFLAT / 4) return;
+  const int o = u / (NFLAT / 4), j = 4 * (u - o * (NFLAT / 4)), pos = j >> 6, c = j & 63;
+  const float* src = a.param + OFF_FC1_W + (int64_t)o * NFLAT + pos;
+  *reinterpret_cast<float4*>(a.w1p + (int64_t)o * NFLAT + j) =
+      make_float4(src[c * NPOOL], src[(c + 1) * NPOOL], src[(c + 2) * NPOOL], src[(c + 3) * NPOOL]);
 }
 
 // conv1 + bias + ReLU: one thread = one output pixel, 32 channels (the bf16 engine's fma order)
@@ -367,12 +360,24 @@ __global__ __launch_bounds__(256) void f32_head_kernel(F32Step a, int B, int S) 
   const float* P = a.param;
   float z[2], h[2];
   bool keep[2];
+  float zs[2] = {0.f, 0.f};                           // split-K partials in fixed order, 24 loads in flight
+  for (int c0 = 0; c0 < S; c0 += 12) {
+    float v[12][2];
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        v[k][j] = c0 + k < S ? a.z1part[((int64_t)(c0 + k) * B + b) * NH + lane + 64 * j] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (c0 + k < S) zs[j] += v[k][j];
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int o = lane + 64 * j;
-    float s = 0.f;                                    // split-K partials in fixed order
-    for (int c = 0; c < S; ++c) s += a.z1part[((int64_t)c * B + b) * NH + o];
-    z[j] = P[OFF_FC1_B + o] + s;
+    z[j] = P[OFF_FC1_B + o] + zs[j];
     float hv = fmaxf(z[j], 0.0f);
     keep[j] = true;
     if (!no_drop) {
@@ -469,19 +474,79 @@ __global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
   }
 }
 
-// split-K slabs -> the flat gradient in torch layouts (fixed slab order)
+// conv1 weight + bias gradient (M = 32 channels, N = 9 taps + bias, K = B*676 pixels: far too thin
+// for the GEMM tile, whose 64 x 64 MFMA tiles were 92 % padding): workgroup g sums pixels
+// [g*P/G, (g+1)*P/G) on the VALU - thread = (pixel lane 0..7, channel), one coalesced 128-B da1
+// row per pixel, the 3x3 input patch as broadcast byte loads - then the 8 pixel lanes in fixed
+// order through LDS: part[g][c][0..9]
+__global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G) {
+  __shared__ float red[8][C1 * 10];
+  const int g = blockIdx.x, tid = threadIdx.x, c = tid & 31, pl = tid >> 5;
+  const int64_t P = (int64_t)B * NPIX1;
+  const int64_t lo = P * g / G, hi = P * (g + 1) / G;
+  const int step = state_of(a)->step;
+  float acc[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) acc[j] = 0.f;
+  for (int64_t m = lo + pl; m < hi; m += 8) {
+    const int b = (int)(m / NPIX1), pix = (int)(m - (int64_t)b * NPIX1), iy = pix / H1, ix = pix - iy * H1;
+    const uint8_t* src = image_row(a, step, b) + iy * IMG + ix;
+    const float d = a.a1[m * C1 + c];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] = __builtin_fmaf(d, normalize_u8_alu(src[(k / 3) * IMG + k % 3]), acc[k]);
+    acc[9] += d;
+  }
+#pragma unroll
+  for (int j = 0; j < 10; ++j) red[pl][c * 10 + j] = acc[j];
+  __syncthreads();
+  for (int e = tid; e < C1 * 10; e += 256) {
+    float s = red[0][e];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) s += red[q][e];
+    a.c1part[(int64_t)g * C1 * 10 + e] = s;
+  }
+}
+
+// split-K slabs -> the flat gradient in torch layouts (fixed order).  Workgroup = 64 output columns
+// x 4 slab phases: thread (column, q) sums slabs z = q, q+4, .. (8 loads in flight), then the 4
+// phases are added in order through LDS (was one thread per output walking all ~128 slabs: 31 us)
 __global__ __launch_bounds__(256) void f32_conv_reduce_kernel(F32Step a, int s2, int s1) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int t = blockIdx.x * 64 + col;
+  const float* src = nullptr;
+  int ns = 0, stride = 0;
   if (t < WG_N) {
     const int co = t / (K2 + 1), n = t - co * (K2 + 1);
-    float s = 0.f;
-    for (int z = 0; z < s2; ++z) s += a.c2part[((int64_t)z * C2 + co) * (K2 + 1) + n];
+    src = a.c2part + (int64_t)co * (K2 + 1) + n;
+    ns = s2;
+    stride = C2 * (K2 + 1);
+  } else if (t < WG_N + C1 * 10) {
+    src = a.c1part + (t - WG_N);
+    ns = s1;
+    stride = C1 * 10;
+  }
+  float s = 0.f;
+  for (int z0 = q; z0 < ns; z0 += 32) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int z = z0 + 4 * k;
+      v[k] = z < ns ? src[(int64_t)z * stride] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  red[q][col] = s;
+  __syncthreads();
+  if (q != 0 || !src) return;
+  s = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  if (t < WG_N) {
+    const int co = t / (K2 + 1), n = t - co * (K2 + 1);
     if (n < K2) a.grad[OFF_CONV2_W + co * K2 + (n & 31) * 9 + (n >> 5)] = s;
     else a.grad[OFF_CONV2_B + co] = s;
-  } else if (t < WG_N + C1 * 10) {
+  } else {
     const int u = t - WG_N, c = u / 10, n = u - c * 10;
-    float s = 0.f;
-    for (int z = 0; z < s1; ++z) s += a.c1part[((int64_t)z * C1 + c) * 10 + n];
     if (n < 9) a.grad[OFF_CONV1_W + c * 9 + n] = s;
     else a.grad[OFF_CONV1_B + c] = s;
   }
@@ -497,11 +562,13 @@ inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 int f32_fc1_splits(int B) { return B <= 1024 ? 36 : 9; }
 int f32_conv2w_splits(int B) { return nsplit((int64_t)B * NPIX2, kchunk((int64_t)B * NPIX2, F32_MAX_SPLITS)); }
-int f32_conv1w_splits(int B) { return nsplit((int64_t)B * NPIX1, kchunk((int64_t)B * NPIX1, F32_MAX_SPLITS)); }
+int f32_conv1w_splits(int B) { return F32_MAX_SPLITS; }
 
 void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
   if (B < 1) throw std::runtime_error("f32 forward: empty batch");
-  hipLaunchKernelGGL(f32_prep_kernel, dim3(blocks(C2 * K2)), dim3(256), 0, s, a);
+  // (training: + the position-major fc1 weight copy for the backward)
+  hipLaunchKernelGGL(f32_prep_kernel, dim3(blocks(C2 * K2) + (train ? blocks(NH * NFLAT / 4) : 0)), dim3(256), 0, s,
+                     a, train ? 1 : 0);
   hipLaunchKernelGGL(f32_conv1_kernel, dim3(blocks((int64_t)B * NPIX1)), dim3(256), 0, s, a, B);
   gemm<64, 64>(PConv2Fwd{B * NPIX2, C2, K2, K2, a.a1, a.w2fwd, a.param + OFF_CONV2_B, a.y2}, 1, s);
   if (train)
@@ -519,15 +586,14 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
 void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(f32_fc_small_kernel, dim3(NH), dim3(256), 0, s, a, B);
   gemm<64, 64>(PFc1W{NH, NFLAT, B, (B + BK - 1) / BK * BK, a.dz1, a.p, a.grad + OFF_FC1_W}, 1, s);
-  gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.param + OFF_FC1_W, a.pm, a.y2, a.state, 1.0f}, 1, s);
+  gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
   const int64_t k2 = (int64_t)B * NPIX2;
   const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
   gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part}, s2, s);
   gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
-  const int64_t k1 = (int64_t)B * NPIX1;
-  const int kc1 = kchunk(k1, F32_MAX_SPLITS), s1 = nsplit(k1, kc1);
-  gemm<64, 64>(PConv1W{C1, 10, (int)k1, kc1, a.a1, a, 0, a.c1part}, s1, s);
-  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(blocks(WG_N + C1 * 10)), dim3(256), 0, s, a, s2, s1);
+  const int s1 = f32_conv1w_splits(B);
+  hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
+  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3((WG_N + C1 * 10 + 63) / 64), dim3(256), 0, s, a, s2, s1);
 }
 
 // load this translation unit's gfx950 code object now (startup prewarm thread) instead of at its

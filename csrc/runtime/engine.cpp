@@ -23,7 +23,6 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
     : buf_(buf), max_batch_(max_batch), max_test_batch_(max_test_batch), compute_(compute),
       comm_stream_(comm), world_(world_size), rho_(rho), eps_(eps), wd_(weight_decay), f32_(fp32) {
   if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
-  if (const char* v = getenv("MNIST_AMD_CONV2_FIRST")) conv2_first_ = atoi(v) != 0;   // A/B (round 5)
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -81,7 +80,7 @@ void Engine::alloc_workspace_f32() {
   const int64_t z1rows = std::max<int64_t>(36 * std::min<int64_t>(Ma, 1024), 9 * Ma);
   int64_t off = 0;
   auto carve = [&](int64_t bytes) { int64_t o = off; off += ws_align256(bytes); return o; };
-  const int64_t o_w2f = carve(9 * C1 * C2 * 4), o_w2b = carve(9 * C1 * C2 * 4);
+  const int64_t o_w2f = carve(9 * C1 * C2 * 4), o_w2b = carve(9 * C1 * C2 * 4), o_w1p = carve((int64_t)NH * NFLAT * 4);
   const int64_t o_a1 = carve(Ma * H1 * H1 * C1 * 4), o_y2 = carve(Ma * H2 * H2 * C2 * 4);
   const int64_t o_p = carve(Ma * NFLAT * 4), o_pm = carve(Ma * NFLAT), o_z1 = carve(z1rows * NH * 4);
   const int64_t o_h = carve(M * NH * 4), o_dz1 = carve(M * NH * 4), o_dl = carve(M * 16 * 4);
@@ -95,6 +94,7 @@ void Engine::alloc_workspace_f32() {
   F32Step& w = f32ws_;
   w.w2fwd = reinterpret_cast<float*>(b + o_w2f);
   w.w2bwd = reinterpret_cast<float*>(b + o_w2b);
+  w.w1p = reinterpret_cast<float*>(b + o_w1p);
   w.a1 = reinterpret_cast<float*>(b + o_a1);
   w.y2 = reinterpret_cast<float*>(b + o_y2);
   w.p = reinterpret_cast<float*>(b + o_p);
@@ -355,68 +355,6 @@ void Engine::enqueue_step(int batch, bool last) {
   // conv2 reduce + all-reduce + update signals [1] at its start (world-1 timeline: two hand-off launches
   // a step fewer, conv2's part no longer queued behind them)
   const bool chain = !trace_ && (!xg || xgmi_fuse_update_);
-  if (!xg && chain && conv2_first_) {
-    // OVERLAP, conv2 first: the comm chain runs conv2's slab reduce + update as soon as dgrad has
-    // started (wgrad's slabs are final) and the fc update after it, so the step's tail (conv1's part,
-    // held until conv2's update is published) no longer waits behind the 20 us fc update; the fc
-    // update instead overlaps conv1's part and the next trunk_fwd, whose completion it must precede.
-    //   M: (+[1] of the previous step) wait [4] >= [3]+1, conv2 reduce+update, fc update (+[3] at start)
-    //   C: ..., wgrad(+[0]), dgrad(+[4]), conv1 reduce+update (hold [3] >= [4]); trunk holds [1] >= [0]
-    uint16_t* w2d_cur = w2d_in_alt_ ? w2d_alt_ : buf_.w2d;
-    AdadeltaArgs u2 = adc;
-    u2.state_inc = nullptr;
-    u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
-    cb.w2d = w2d_cur;
-    phase_begin("conv2+fc update");
-    if (S) {
-      if (comm_sig1_pending_)
-        launch_stream_signal_wait(sync_ + 1, sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
-      else
-        launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
-      comm_sig1_pending_ = false;
-      if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
-      launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
-      AdadeltaArgs af = ad;
-      af.signal_start = sync_ + 3;                // conv2's update (previous launch) is published
-      launch_adadelta(af, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
-      if (!last)
-        comm_sig1_pending_ = true;                // signalled by the next step's first comm launch
-      else
-        launch_stream_signal(sync_ + 1, comm_stream_);
-    }
-    phase_end();
-    side_pending_ = true;
-    ConvBwdArgs cbd = cb;
-    cbd.signal_ctr = sync_ + 4;
-    phase_begin("bwd_conv_dgrad");
-    if (M) launch_conv_dgrad(cbd, B, compute_);
-    phase_end();
-    phase_begin("conv1 reduce+update");
-    if (M) {
-      AdadeltaArgs u1 = adc;
-      u1.hold_a = sync_ + 3;
-      u1.hold_b = sync_ + 4;
-      u1.hold_err = sync_ + 2;
-      launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
-    }
-    phase_end();
-    w2d_in_alt_ = !w2d_in_alt_;
-    if (last && w2d_in_alt_) {
-      if (M)
-        HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
-                              compute_));
-      w2d_in_alt_ = false;
-    }
-    if (last) {
-      if (M && !skip_join_) {
-        HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-        HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-      }
-      side_pending_ = false;
-      side_forked_ = false;
-    }
-    return;
-  }
   phase_begin("allreduce_fc+update");
   if (S) {
     if (chain && comm_sig3_pending_)
@@ -604,7 +542,6 @@ int Engine::capture_train(int n, int batch, int stride) {
 
 void Engine::reset_host_state() {
   comm_sig3_pending_ = false;
-  comm_sig1_pending_ = false;
   enq_main_ = enq_side_ = true;
   skip_join_ = false;
   side_pending_ = false;
@@ -628,7 +565,6 @@ int Engine::capture_train_split(int n, int batch) {
     side_pending_ = sp;
     w2d_in_alt_ = w2;
     comm_sig3_pending_ = false;
-    comm_sig1_pending_ = false;
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;
     enq_side_ = side;

@@ -169,8 +169,6 @@ class Engine {
   bool side_pending_ = false;       // the previous step's fc update is not joined yet
   bool side_forked_ = false;        // comm stream already ordered after this chunk's start
   bool comm_sig3_pending_ = false;  // OVERLAP chain: the last conv2 update's [3] signal is owed
-  bool comm_sig1_pending_ = false;  // OVERLAP conv2-first chain: the last fc update's [1] signal is owed
-  bool conv2_first_ = false;        // OVERLAP comm chain order: conv2 part before the fc update
   int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
                                     // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch,
                                     // [12..15] fault-injection hold

@@ -327,7 +327,9 @@ class PendingXgmiComm:
             with use_channel(self._hc):
                 self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings)
         except BaseException as e:  # noqa: BLE001 - re-raised in result()
+            import traceback
             self._err = e
+            self._tb = traceback.format_exc()
         self.seconds = time.perf_counter() - t0
 
     def result(self, timeout_s: float = 600.0):
@@ -335,6 +337,8 @@ class PendingXgmiComm:
         if self._t.is_alive():
             raise RuntimeError(f"xGMI communicator setup did not finish within {timeout_s:.0f} s")
         if self._err is not None:
+            import sys
+            print(f"[xgmi] rank {self._args[1]}: setup thread failed:\n{self._tb}", file=sys.stderr, flush=True)
             raise self._err
         return self._comm
 
