@@ -434,6 +434,24 @@ PYBIND11_MODULE(_C, m) {
     auto sec = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
     return std::make_tuple(sec(t0, t1), sec(t1, t2), sec(t2, t3));
   }, py::call_guard<py::gil_scoped_release>(), py::arg("device"));
+  // physical identity of a device (PCI domain:bus:device.function + UUID) straight from the HIP
+  // runtime: callable from any thread, no amdsmi (torch.cuda.get_device_properties counts devices
+  // through amdsmi, and from a helper thread it refused a valid index on the box)
+  m.def("device_identity", [](int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, device) != hipSuccess)
+      throw std::runtime_error("device_identity: hipDeviceGetPCIBusId failed");
+    hipUUID uuid;
+    std::string u;
+    if (hipDeviceGetUuid(&uuid, device) == hipSuccess) {
+      static const char* hx = "0123456789abcdef";
+      for (int i = 0; i < 16; ++i) {
+        u += hx[((unsigned char)uuid.bytes[i]) >> 4];
+        u += hx[((unsigned char)uuid.bytes[i]) & 15];
+      }
+    }
+    return std::string(bus) + "|" + u;
+  });
   m.def("memset_sync", [](uintptr_t ptr, int value, int64_t nbytes) {
     // setup-time buffer initialisation without a torch fill kernel (whose code object would load on
     // first launch inside the reference timer); synchronous

@@ -234,9 +234,10 @@ struct F32Step {
   float* loss_rows;           // [B] per-row NLL (train and eval)
   int32_t* correct;           // eval: [B] argmax == label
   float* c2part;              // [f32_conv2w_splits(B)][64][289] conv2 weight + bias partials
-  float* c1part;              // [f32_conv1w_splits(B)][32][10] conv1 weight + bias partials
+  float* c1part;              // [F32_C1W_BLOCKS][32][10] conv1 weight + bias partials
 };
 constexpr int F32_MAX_SPLITS = 128;
+constexpr int F32_C1W_BLOCKS = 1024;         // conv1 weight-gradient workgroups (= partial slabs)
 int f32_fc1_splits(int B);
 int f32_conv2w_splits(int B);
 int f32_conv1w_splits(int B);

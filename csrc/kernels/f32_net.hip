@@ -49,14 +49,21 @@ __device__ __forceinline__ const uint8_t* image_row(const F32Step& a, int step, 
 // GEMM template: C[M][N] = sum_k A(m, k) B(k, n) over k in [z*kc, min(K, (z+1)*kc)) (z = blockIdx.z).
 // Workgroup tile BM x BN (4 waves, each 32 x 32 = 2 x 2 tiles of 16 x 16), k-tile 16 staged in LDS
 // as [k][m] / [k][n] rows, so every MFMA operand read is 16 consecutive floats per 16-lane group.
-// The policy P provides M, N, K, kc, a(m, k), b(k, n), put(m, n, v, z), prepare() and whether A / B
-// are contiguous along k (A_KF / B_KF) - the tile-load thread mapping follows the contiguous axis.
+// The policy P provides M, N, K, kc, put(m, n, v, z), prepare(), whether A / B are contiguous along
+// k (A_KF / B_KF), and the operands as 16-B vectors along their contiguous axis:
+//   a4(m, k) = A(m, k..k+3) when A_KF, else A(m..m+3, k);  b4(k, n) = B(k..k+3, n) when B_KF, else
+//   B(k, n..n+3)
+// so each gather (the implicit im2col / transposed-conv index math, its bounds test) serves 4
+// elements: the scalar form spent more VALU issue on addressing than the MFMAs took (the conv GEMMs
+// ran at 30-38 % of the f32 matrix peak).  Vector axes are 4-aligned (M, N, K multiples of 4 on
+// them, split-K chunks multiples of 16); a policy whose vector crosses its bound zero-fills itself.
 template <int BM, int BN, class P>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
   static_assert((BM / 32) * (BN / 32) == 4, "4 waves of 32 x 32");
-  constexpr int EA = BM * BK / 256, EB = BN * BK / 256, WN = BN / 32;
-  __shared__ float As[BK][BM + 4];
-  __shared__ float Bs[BK][BN + 4];
+  constexpr int NA = BM * BK / 4, NB = BN * BK / 4;            // float4s per operand tile
+  constexpr int EA = (NA + 255) / 256, EB = (NB + 255) / 256, WN = BN / 32;
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + 4];
   p.prepare();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -71,38 +78,47 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
 
   // register prefetch: the next k-tile's gathers are issued before this tile's MFMAs, so their
   // latency hides under the matrix work instead of sitting between the two barriers
-  float ra[EA], rb[EB];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      const int x = tid + 256 * e;
-      const int m = P::A_KF ? x / BK : x % BM, k = P::A_KF ? x % BK : x / BM;
-      const int gm = m0 + m, gk = k0 + k;
-      ra[e] = (gm < p.M && gk < k_hi) ? p.a(gm, gk) : 0.0f;
-    }
-#pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      const int x = tid + 256 * e;
-      const int n = P::B_KF ? x / BK : x % BN, k = P::B_KF ? x % BK : x / BN;
-      const int gn = n0 + n, gk = k0 + k;
-      rb[e] = (gn < p.N && gk < k_hi) ? p.b(gk, gn) : 0.0f;
-    }
-  };
-  if (k_lo < k_hi) load(k_lo);
+  float4 ra[EA], rb[EB];
+#define F32_GEMM_LOAD(K0)                                                                                    \
+  _Pragma("unroll") for (int e = 0; e < EA; ++e) {                                                          \
+    const int x = tid + 256 * e;                                                                            \
+    const int m = P::A_KF ? x / (BK / 4) : (x % (BM / 4)) * 4, k = P::A_KF ? (x % (BK / 4)) * 4 : x / (BM / 4); \
+    const int gm = m0 + m, gk = (K0) + k;                                                                   \
+    ra[e] = (x < NA && gm < p.M && gk < k_hi) ? p.a4(gm, gk) : make_float4(0.f, 0.f, 0.f, 0.f);             \
+  }                                                                                                         \
+  _Pragma("unroll") for (int e = 0; e < EB; ++e) {                                                          \
+    const int x = tid + 256 * e;                                                                            \
+    const int n = P::B_KF ? x / (BK / 4) : (x % (BN / 4)) * 4, k = P::B_KF ? (x % (BK / 4)) * 4 : x / (BN / 4); \
+    const int gn = n0 + n, gk = (K0) + k;                                                                   \
+    rb[e] = (x < NB && gn < p.N && gk < k_hi) ? p.b4(gk, gn) : make_float4(0.f, 0.f, 0.f, 0.f);            \
+  }
+  if (k_lo < k_hi) { F32_GEMM_LOAD(k_lo) }
   for (int k0 = k_lo; k0 < k_hi; k0 += BK) {
     lds_barrier();                                // the previous k-tile's reads are done
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int x = tid + 256 * e;
-      As[P::A_KF ? x % BK : x / BM][P::A_KF ? x / BK : x % BM] = ra[e];
+      if (x >= NA) continue;
+      if (P::A_KF) {
+        const int m = x / (BK / 4), k = (x % (BK / 4)) * 4;
+        As[k][m] = ra[e].x; As[k + 1][m] = ra[e].y; As[k + 2][m] = ra[e].z; As[k + 3][m] = ra[e].w;
+      } else {
+        *reinterpret_cast<float4*>(&As[x / (BM / 4)][(x % (BM / 4)) * 4]) = ra[e];
+      }
     }
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       const int x = tid + 256 * e;
-      Bs[P::B_KF ? x % BK : x / BN][P::B_KF ? x / BK : x % BN] = rb[e];
+      if (x >= NB) continue;
+      if (P::B_KF) {
+        const int n = x / (BK / 4), k = (x % (BK / 4)) * 4;
+        Bs[k][n] = rb[e].x; Bs[k + 1][n] = rb[e].y; Bs[k + 2][n] = rb[e].z; Bs[k + 3][n] = rb[e].w;
+      } else {
+        *reinterpret_cast<float4*>(&Bs[x / (BN / 4)][(x % (BN / 4)) * 4]) = rb[e];
+      }
     }
     lds_barrier();
-    if (k0 + BK < k_hi) load(k0 + BK);            // in flight under the MFMAs below
+    if (k0 + BK < k_hi) { F32_GEMM_LOAD(k0 + BK) }   // in flight under the MFMAs below
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       float av[2], bv[2];
@@ -145,12 +161,12 @@ struct PConv2Fwd {
   const float* b2;
   float* y2;
   __device__ void prepare() {}
-  __device__ float a(int m, int k) const {
+  __device__ float4 a4(int m, int k) const {
     const int b = m / NPIX2, pix = m - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
     const int tap = k >> 5, ci = k & 31, ky = tap / 3, kx = tap - 3 * ky;
-    return a1[(((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci];
+    return *reinterpret_cast<const float4*>(a1 + (((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci);
   }
-  __device__ float b(int k, int n) const { return w2fwd[k * C2 + n]; }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w2fwd + k * C2 + n); }
   __device__ void put(int m, int n, float v, int) const { y2[(int64_t)m * C2 + n] = v + b2[n]; }
 };
 
@@ -162,8 +178,8 @@ struct PFc1 {
   const float* w1;
   float* z1part;
   __device__ void prepare() {}
-  __device__ float a(int m, int k) const { return p[(int64_t)m * NFLAT + k]; }
-  __device__ float b(int k, int n) const { return w1[(int64_t)n * NFLAT + k]; }
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(p + (int64_t)m * NFLAT + k); }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w1 + (int64_t)n * NFLAT + k); }
   __device__ void put(int m, int n, float v, int z) const { z1part[((int64_t)z * M + m) * NH + n] = v; }
 };
 
@@ -175,8 +191,8 @@ struct PFc1W {
   const float* p;
   float* g;
   __device__ void prepare() {}
-  __device__ float a(int m, int k) const { return dz1[(int64_t)k * NH + m]; }
-  __device__ float b(int k, int n) const { return p[(int64_t)k * NFLAT + n]; }
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)k * NH + m); }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(p + (int64_t)k * NFLAT + n); }
   __device__ void put(int m, int n, float v, int) const { g[(int64_t)m * NFLAT + n] = v; }
 };
 
@@ -199,8 +215,8 @@ struct PFc1X {
     const StepState* s = st ? st : &g_zero_state;
     dscale = (s->flags & STEP_FLAG_NO_DROPOUT) ? 1.0f : (1.0f / KEEP1);
   }
-  __device__ float a(int m, int k) const { return dz1[(int64_t)m * NH + k]; }
-  __device__ float b(int k, int n) const { return w1p[(int64_t)k * NFLAT + n]; }
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)m * NH + k); }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w1p + (int64_t)k * NFLAT + n); }
   __device__ void put(int m, int n, float v, int) const {
     const int c = n & (C2 - 1), pos = n >> 6, py = pos / HP, px = pos - py * HP;
     const uint32_t fl = pm[(int64_t)m * NFLAT + c * NPOOL + pos];
@@ -222,12 +238,12 @@ struct PConv2W {
   const float* a1;
   float* part;
   __device__ void prepare() {}
-  __device__ float a(int m, int k) const { return dy2[(int64_t)k * C2 + m]; }
-  __device__ float b(int k, int n) const {
-    if (n == K2) return 1.0f;
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dy2 + (int64_t)k * C2 + m); }
+  __device__ float4 b4(int k, int n) const {
+    if (n >= K2) return make_float4(1.0f, 0.0f, 0.0f, 0.0f);      // the bias column (n = 288) + padding
     const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
     const int tap = n >> 5, ci = n & 31, ky = tap / 3, kx = tap - 3 * ky;
-    return a1[(((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci];
+    return *reinterpret_cast<const float4*>(a1 + (((int64_t)b * H1 + oy + ky) * H1 + ox + kx) * C1 + ci);
   }
   __device__ void put(int m, int n, float v, int z) const { part[((int64_t)z * C2 + m) * (K2 + 1) + n] = v; }
 };
@@ -241,13 +257,15 @@ struct PConv2X {
   const float* w2bwd;   // [tap][co][ci]
   float* a1;
   __device__ void prepare() {}
-  __device__ float a(int m, int k) const {
+  __device__ float4 a4(int m, int k) const {
     const int b = m / NPIX1, pix = m - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
     const int tap = k >> 6, co = k & 63, ky = tap / 3, kx = tap - 3 * ky;
     const int oy = iy - ky, ox = ix - kx;
-    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2) ? dy2[(((int64_t)b * H2 + oy) * H2 + ox) * C2 + co] : 0.0f;
+    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
+               ? *reinterpret_cast<const float4*>(dy2 + (((int64_t)b * H2 + oy) * H2 + ox) * C2 + co)
+               : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  __device__ float b(int k, int n) const { return w2bwd[k * C1 + n]; }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w2bwd + k * C1 + n); }
   __device__ void put(int m, int n, float v, int) const {
     float* q = a1 + (int64_t)m * C1 + n;
     *q = (*q > 0.0f) ? v : 0.0f;
@@ -475,10 +493,12 @@ __global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
 }
 
 // conv1 weight + bias gradient (M = 32 channels, N = 9 taps + bias, K = B*676 pixels: far too thin
-// for the GEMM tile, whose 64 x 64 MFMA tiles were 92 % padding): workgroup g sums pixels
-// [g*P/G, (g+1)*P/G) on the VALU - thread = (pixel lane 0..7, channel), one coalesced 128-B da1
-// row per pixel, the 3x3 input patch as broadcast byte loads - then the 8 pixel lanes in fixed
-// order through LDS: part[g][c][0..9]
+// for the GEMM tile, whose 64 x 64 MFMA tiles were 92 % padding): F32_C1W_BLOCKS workgroups, g sums
+// pixels [g*P/G, (g+1)*P/G) on the VALU - thread = (pixel lane 0..7, channel), a coalesced 128-B da1
+// row per pixel and the 3x3 input patch as broadcast byte loads, 4 pixels' loads in flight - then
+// the 8 pixel lanes in fixed order through LDS: part[g][c][0..9].  The work is 4.3 M (pixel,
+// channel) pairs of 10 FMAs: latency, not arithmetic - so ~1000 workgroups of a few pixels each
+// (128 workgroups of ~130 pixels per thread took 86 us)
 __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G) {
   __shared__ float red[8][C1 * 10];
   const int g = blockIdx.x, tid = threadIdx.x, c = tid & 31, pl = tid >> 5;
@@ -488,13 +508,26 @@ __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G
   float acc[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) acc[j] = 0.f;
-  for (int64_t m = lo + pl; m < hi; m += 8) {
-    const int b = (int)(m / NPIX1), pix = (int)(m - (int64_t)b * NPIX1), iy = pix / H1, ix = pix - iy * H1;
-    const uint8_t* src = image_row(a, step, b) + iy * IMG + ix;
-    const float d = a.a1[m * C1 + c];
+  constexpr int U = 4;
+  for (int64_t m0 = lo + pl; m0 < hi; m0 += 8 * U) {
+    float d[U], x[U][9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = __builtin_fmaf(d, normalize_u8_alu(src[(k / 3) * IMG + k % 3]), acc[k]);
-    acc[9] += d;
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + 8 * u;
+      const bool ok = m < hi;
+      const int64_t mm = ok ? m : lo;
+      const int b = (int)(mm / NPIX1), pix = (int)(mm - (int64_t)b * NPIX1), iy = pix / H1, ix = pix - iy * H1;
+      const uint8_t* src = image_row(a, step, b) + iy * IMG + ix;
+      d[u] = ok ? a.a1[mm * C1 + c] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) x[u][k] = normalize_u8_alu(src[(k / 3) * IMG + k % 3]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[k] = __builtin_fmaf(d[u], x[u][k], acc[k]);
+      acc[9] += d[u];
+    }
   }
 #pragma unroll
   for (int j = 0; j < 10; ++j) red[pl][c * 10 + j] = acc[j];
@@ -507,48 +540,66 @@ __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G
   }
 }
 
-// split-K slabs -> the flat gradient in torch layouts (fixed order).  Workgroup = 64 output columns
-// x 4 slab phases: thread (column, q) sums slabs z = q, q+4, .. (8 loads in flight), then the 4
-// phases are added in order through LDS (was one thread per output walking all ~128 slabs: 31 us)
+// split-K slabs -> the flat gradient in torch layouts (fixed order).
+//   blocks [0, RED2_BLOCKS): conv2 weight + bias, 64 output columns x 4 slab phases per workgroup:
+//     thread (column, q) sums slabs z = q, q+4, .. (8 loads in flight), the 4 phases added in order
+//     through LDS (was one thread per output walking all ~128 slabs: 31 us);
+//   the rest: conv1 weight + bias (F32_C1W_BLOCKS slabs), 4 outputs x 64 slab phases per workgroup,
+//     a fixed-order LDS tree over the 64 phases.
+constexpr int RED2_BLOCKS = (WG_N + 63) / 64;
+constexpr int RED1_BLOCKS = C1 * 10 / 4;
 __global__ __launch_bounds__(256) void f32_conv_reduce_kernel(F32Step a, int s2, int s1) {
-  __shared__ float red[4][64];
-  const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int t = blockIdx.x * 64 + col;
-  const float* src = nullptr;
-  int ns = 0, stride = 0;
-  if (t < WG_N) {
-    const int co = t / (K2 + 1), n = t - co * (K2 + 1);
-    src = a.c2part + (int64_t)co * (K2 + 1) + n;
-    ns = s2;
-    stride = C2 * (K2 + 1);
-  } else if (t < WG_N + C1 * 10) {
-    src = a.c1part + (t - WG_N);
-    ns = s1;
-    stride = C1 * 10;
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  if (blockIdx.x < RED2_BLOCKS) {
+    const int col = tid & 63, q = tid >> 6;
+    const int t = blockIdx.x * 64 + col;
+    const bool live = t < WG_N;
+    const int co = live ? t / (K2 + 1) : 0, n = live ? t - co * (K2 + 1) : 0;
+    const float* src = a.c2part + (int64_t)co * (K2 + 1) + n;
+    float s = 0.f;
+    for (int z0 = q; z0 < s2; z0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int z = z0 + 4 * k;
+        v[k] = z < s2 ? src[(int64_t)z * (C2 * (K2 + 1))] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    red[tid] = s;
+    __syncthreads();
+    if (q != 0 || !live) return;
+    s = ((red[col] + red[64 + col]) + red[128 + col]) + red[192 + col];
+    if (n < K2) a.grad[OFF_CONV2_W + co * K2 + (n & 31) * 9 + (n >> 5)] = s;
+    else a.grad[OFF_CONV2_B + co] = s;
+    return;
   }
+  const int o = (blockIdx.x - RED2_BLOCKS) * 4 + (tid & 3), q = tid >> 2;   // output, phase 0..63
+  const float* src = a.c1part + o;
   float s = 0.f;
-  for (int z0 = q; z0 < ns; z0 += 32) {
+  for (int z0 = q; z0 < s1; z0 += 64 * 8) {
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int z = z0 + 4 * k;
-      v[k] = z < ns ? src[(int64_t)z * stride] : 0.0f;
+      const int z = z0 + 64 * k;
+      v[k] = z < s1 ? src[(int64_t)z * (C1 * 10)] : 0.0f;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k];
   }
-  red[q][col] = s;
+  red[tid] = s;
   __syncthreads();
-  if (q != 0 || !src) return;
-  s = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
-  if (t < WG_N) {
-    const int co = t / (K2 + 1), n = t - co * (K2 + 1);
-    if (n < K2) a.grad[OFF_CONV2_W + co * K2 + (n & 31) * 9 + (n >> 5)] = s;
-    else a.grad[OFF_CONV2_B + co] = s;
-  } else {
-    const int u = t - WG_N, c = u / 10, n = u - c * 10;
-    if (n < 9) a.grad[OFF_CONV1_W + c * 9 + n] = s;
-    else a.grad[OFF_CONV1_B + c] = s;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {                 // fixed-order tree over the 64 phases
+    if (q < w) red[tid] = red[tid] + red[tid + 4 * w];
+    __syncthreads();
+  }
+  if (q == 0) {
+    const int c = o / 10, j = o - c * 10;
+    if (j < 9) a.grad[OFF_CONV1_W + c * 9 + j] = red[tid];
+    else a.grad[OFF_CONV1_B + c] = red[tid];
   }
 }
 
@@ -562,7 +613,7 @@ inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 int f32_fc1_splits(int B) { return B <= 1024 ? 36 : 9; }
 int f32_conv2w_splits(int B) { return nsplit((int64_t)B * NPIX2, kchunk((int64_t)B * NPIX2, F32_MAX_SPLITS)); }
-int f32_conv1w_splits(int B) { return F32_MAX_SPLITS; }
+int f32_conv1w_splits(int B) { return F32_C1W_BLOCKS; }
 
 void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
   if (B < 1) throw std::runtime_error("f32 forward: empty batch");
@@ -593,7 +644,7 @@ void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
   gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
   const int s1 = f32_conv1w_splits(B);
   hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
-  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3((WG_N + C1 * 10 + 63) / 64), dim3(256), 0, s, a, s2, s1);
+  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, s2, s1);
 }
 
 // load this translation unit's gfx950 code object now (startup prewarm thread) instead of at its

@@ -86,7 +86,7 @@ void Engine::alloc_workspace_f32() {
   const int64_t o_h = carve(M * NH * 4), o_dz1 = carve(M * NH * 4), o_dl = carve(M * 16 * 4);
   const int64_t o_loss = carve(M * 4);
   const int64_t o_c2 = carve((int64_t)F32_MAX_SPLITS * C2 * (9 * C1 + 1) * 4);
-  const int64_t o_c1 = carve((int64_t)F32_MAX_SPLITS * C1 * 10 * 4);
+  const int64_t o_c1 = carve((int64_t)F32_C1W_BLOCKS * C1 * 10 * 4);
   HIP_OK(hipMalloc(&ws32_, off));
   HIP_OK(hipMemset(ws32_, 0, off));
   ws_bytes_ += off;

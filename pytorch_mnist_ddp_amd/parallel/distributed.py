@@ -212,8 +212,8 @@ def xgmi_broadcast_(x, t: torch.Tensor, src: int = 0) -> None:
 
 
 def _device_identity(device) -> str:
-    p = torch.cuda.get_device_properties(torch.device(device))
-    return "|".join(str(getattr(p, k, "")) for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"))
+    from ..ops import native
+    return native.load().device_identity(torch.device(device).index or 0)
 
 
 def ranks_per_device(device, world: int | None = None) -> int:
