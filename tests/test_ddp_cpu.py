@@ -215,7 +215,8 @@ def _share_worker(rank, world, port, q):
             lambda d: _FakeProps("", bus=rank // 2),         # two ranks per GPU (rank 2 alone)
         ]
         for fake in cases:
-            torch.cuda.get_device_properties = fake
+            # (identity = PCI bus id | UUID from the HIP runtime: native device_identity)
+            D._device_identity = lambda d, f=fake: (lambda p: f"0000:{p.pci_bus_id:02x}:00.0|{p.uuid}")(f(d))
             out.append((D.ranks_share_a_device("cpu"), D.ranks_per_device("cpu")))
         q.put((rank, out))
     finally:
