@@ -292,25 +292,25 @@ __global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a, int train) {
       make_float4(src[c * NPOOL], src[(c + 1) * NPOOL], src[(c + 2) * NPOOL], src[(c + 3) * NPOOL]);
 }
 
-// conv1 + bias + ReLU: one thread = one output pixel, 32 channels (the bf16 engine's fma order)
+// conv1 + bias + ReLU: one thread = 4 channels of one output pixel (the bf16 engine's fma order);
+// 8 consecutive lanes cover a pixel's 32 channels, so each float4 store instruction writes 8 whole
+// pixels (1 KB contiguous; one thread per pixel wrote 64 lines in 16-B pieces per instruction)
 __global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)B * NPIX1) return;
-  const int b = (int)(t / NPIX1), pix = (int)(t - (int64_t)b * NPIX1), y = pix / H1, x = pix - y * H1;
+  if (t >= (int64_t)B * NPIX1 * 8) return;
+  const int64_t q = t >> 3;
+  const int c4 = (int)(t & 7);
+  const int b = (int)(q / NPIX1), pix = (int)(q - (int64_t)b * NPIX1), y = pix / H1, x = pix - y * H1;
   const uint8_t* src = image_row(a, state_of(a)->step, b) + y * IMG + x;
   float xv[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) xv[k] = normalize_u8_alu(src[(k / 3) * IMG + k % 3]);
   const float* w = a.param + OFF_CONV1_W;
   const float* bias = a.param + OFF_CONV1_B;
-  float4* dst = reinterpret_cast<float4*>(a.a1 + t * C1);
+  float o[4];
 #pragma unroll
-  for (int c4 = 0; c4 < C1 / 4; ++c4) {
-    float o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = fmaxf(conv1_preact(xv, 3, w + (4 * c4 + j) * 9, bias[4 * c4 + j]), 0.0f);
-    dst[c4] = make_float4(o[0], o[1], o[2], o[3]);
-  }
+  for (int j = 0; j < 4; ++j) o[j] = fmaxf(conv1_preact(xv, 3, w + (4 * c4 + j) * 9, bias[4 * c4 + j]), 0.0f);
+  reinterpret_cast<float4*>(a.a1 + q * C1)[c4] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // ReLU + 2x2 max-pool (first max wins, as torch) + dropout(0.25): one thread = 16 consecutive
@@ -319,8 +319,10 @@ template <bool TRAIN>
 __global__ __launch_bounds__(256) void f32_pool_kernel(F32Step a, int B) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)B * C2 * (NPOOL / 16)) return;
+  // lanes = channels: each y2 load instruction reads one pixel's 64 channels (256 contiguous bytes;
+  // with lanes walking positions of one channel every load touched 64 lines for 4 bytes each)
   const int b = (int)(t / (C2 * (NPOOL / 16))), u = (int)(t - (int64_t)b * (C2 * (NPOOL / 16)));
-  const int c = u / (NPOOL / 16), j = u - c * (NPOOL / 16);
+  const int c = u & (C2 - 1), j = u >> 6;
   const int flat0 = c * NPOOL + 16 * j;
   const StepState* st = state_of(a);
   const bool drop = TRAIN && !(st->flags & STEP_FLAG_NO_DROPOUT);
@@ -620,7 +622,7 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
   // (training: + the position-major fc1 weight copy for the backward)
   hipLaunchKernelGGL(f32_prep_kernel, dim3(blocks(C2 * K2) + (train ? blocks(NH * NFLAT / 4) : 0)), dim3(256), 0, s,
                      a, train ? 1 : 0);
-  hipLaunchKernelGGL(f32_conv1_kernel, dim3(blocks((int64_t)B * NPIX1)), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(f32_conv1_kernel, dim3(blocks((int64_t)B * NPIX1 * 8)), dim3(256), 0, s, a, B);
   gemm<64, 64>(PConv2Fwd{B * NPIX2, C2, K2, K2, a.a1, a.w2fwd, a.param + OFF_CONV2_B, a.y2}, 1, s);
   if (train)
     hipLaunchKernelGGL(f32_pool_kernel<true>, dim3(blocks((int64_t)B * C2 * 9)), dim3(256), 0, s, a, B);
