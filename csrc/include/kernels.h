@@ -247,6 +247,8 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s);
 // fc2 / fc1-bias grads + loss log, fc1 weight grad, fc1 input grad (+ unpool), conv2 weight grad,
 // conv2 input grad (+ conv1 ReLU), conv1 weight grad, split-K reduce: every gradient of the step
 void launch_f32_backward(const F32Step& a, int B, hipStream_t s);
+void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s);     // = the first half of it
+void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s);   // = the second half
 
 // direct xGMI all-reduce (reduce-scatter + all-gather over IPC-mapped peer buckets; xgmi_allreduce.hip)
 constexpr int XGMI_MAX_RANKS = 8;          // one node

@@ -636,9 +636,15 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
     hipLaunchKernelGGL(f32_head_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, s, a, B, s1);
 }
 
-void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
+// fc gradients (fc2 weight / bias, fc1 bias, fc1 weight): after these the fc update may start
+void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(f32_fc_small_kernel, dim3(NH), dim3(256), 0, s, a, B);
   gemm<64, 64>(PFc1W{NH, NFLAT, B, (B + BK - 1) / BK * BK, a.dz1, a.p, a.grad + OFF_FC1_W}, 1, s);
+}
+
+// the rest: fc1 input gradient (reads the w1p copy, not the fc1 parameters the update rewrites),
+// conv2 weight / input gradients, conv1 weight gradient, slab reduce
+void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s) {
   gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
   const int64_t k2 = (int64_t)B * NPIX2;
   const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
@@ -647,6 +653,11 @@ void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
   const int s1 = f32_conv1w_splits(B);
   hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
   hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, s2, s1);
+}
+
+void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {
+  launch_f32_backward_fc(a, B, s);
+  launch_f32_backward_conv(a, B, s);
 }
 
 // load this translation unit's gfx950 code object now (startup prewarm thread) instead of at its

@@ -137,7 +137,6 @@ void Engine::attach_xgmi(std::shared_ptr<XgmiComm> x) {
 }
 
 void Engine::set_schedule(int s) {
-  if (f32_ && s == OVERLAP) throw std::runtime_error("engine: the fp32 step has no OVERLAP schedule");
   if (s == SERIAL || s == OVERLAP) {
     if (world_ != 1 || comm_ || xgmi_)
       throw std::runtime_error("engine: the single-GPU schedules need world size 1 and no transport attached");
@@ -205,7 +204,7 @@ void Engine::enqueue_step(int batch, bool last) {
   if (world_ > 1 && sched_ != RCCL && sched_ != XGMI)
     throw std::runtime_error("engine: world size > 1 needs the RCCL or XGMI schedule");
   if (f32_) {
-    enqueue_step_f32(batch);
+    enqueue_step_f32(batch, last);
     return;
   }
   const int B = batch, Bp = round_up(B, 32);
@@ -474,8 +473,55 @@ void Engine::enqueue_step(int batch, bool last) {
 }
 
 // fp32 step: forward, every gradient, (RCCL: one all-reduce of the whole flat gradient on the
-// compute stream), the whole Adadelta update (which advances the device step counter)
-void Engine::enqueue_step_f32(int batch) {
+// compute stream), the whole Adadelta update (which advances the device step counter).
+// OVERLAP (single GPU): the fc update (98 % of the parameters) runs on the comm stream beside the
+// conv backward once the fc gradients are final; the next step's first kernel waits for it.
+//   C: (wait [1] >= [0]) forward, fc grads, +[0], conv grads, conv update (+step)
+//   M: wait [0] >= [1]+1, fc update, +[1]
+void Engine::enqueue_step_f32(int batch, bool last) {
+  if (sched_ == OVERLAP) {
+    const bool M = enq_main_, S = enq_side_;
+    if (!side_forked_) {
+      HIP_OK(hipEventRecord(ev_fc_, compute_));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+      side_forked_ = true;
+    }
+    const bool pre = buf_.epoch_u8 != nullptr;
+    F32Step a = f32_args();
+    a.data_u8 = pre ? buf_.epoch_u8 : buf_.train_u8;
+    a.idx = pre ? nullptr : buf_.train_idx;
+    a.idx_step_stride = idx_stride_;
+    a.labels = pre ? buf_.epoch_labels : buf_.train_labels;
+    a.state = buf_.state;
+    a.inv_batch = ddp_head_inv_batch(batch, world_);
+    AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
+                    buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+    if (M) {
+      if (side_pending_) launch_stream_wait(sync_ + 1, sync_ + 0, 0, sync_ + 2, compute_);
+      launch_f32_forward(a, batch, true, compute_);
+      launch_f32_backward_fc(a, batch, compute_);
+      launch_stream_signal(sync_ + 0, compute_);
+      launch_f32_backward_conv(a, batch, compute_);
+      AdadeltaArgs ac = ad;
+      ac.state_inc = buf_.state;
+      launch_adadelta(ac, ADA_CONV, compute_);
+    }
+    if (S) {
+      launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+      launch_adadelta(ad, ADA_FC, comm_stream_);
+      launch_stream_signal(sync_ + 1, comm_stream_);
+    }
+    side_pending_ = true;
+    if (last) {
+      if (M && !skip_join_) {
+        HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+        HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      }
+      side_pending_ = false;
+      side_forked_ = false;
+    }
+    return;
+  }
   const bool pre = buf_.epoch_u8 != nullptr;
   F32Step a = f32_args();
   a.data_u8 = pre ? buf_.epoch_u8 : buf_.train_u8;

@@ -142,9 +142,9 @@ class Engine {
 
  private:
   void enqueue_step(int batch, bool last);
-  void enqueue_step_f32(int batch);
+  void enqueue_step_f32(int batch, bool last);
   F32Step f32_args() const;
-  bool side_schedule() const { return !f32_ && (sched_ == OVERLAP || sched_ == XGMI); }
+  bool side_schedule() const { return sched_ == OVERLAP || (sched_ == XGMI && !f32_); }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
   void reset_host_state();

@@ -123,7 +123,8 @@ class FusedTrainer:
     themselves (False = separate launches: the fused kernels' bitwise oracle).  ``probe_world1``
     (tests): with a communicator at world 1, evaluate the xGMI candidate under "auto" too.
     ``fp32`` (``--dtype fp32``): the fp32 step of ``f32_net.hip`` (f32-input MFMA GEMMs, fp32
-    activations and gradient operands) in the SERIAL schedule, or RCCL at world > 1."""
+    activations and gradient operands) in the OVERLAP (fc update on the comm stream) or SERIAL schedule,
+    RCCL or XGMI at world > 1."""
 
     def __init__(self, mstate: ModelState, train: MNISTData, test: MNISTData | None, batch_size: int,
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
@@ -239,7 +240,7 @@ class FusedTrainer:
         # OVERLAP (default): the fc Adadelta step and conv2's reduce + update on the comm stream under
         # the conv backward (measured B = 200: 82.7 vs 85.2 us/step serial, then 70.8-71.2 with
         # conv2's part moved too); SERIAL when the streams share a hardware queue
-        self.overlap = bool(overlap) and not self.fp32 and self._probe_streams()
+        self.overlap = bool(overlap) and self._probe_streams()
         self.engine.set_schedule(C.SCHED_OVERLAP if self.overlap else C.SCHED_SERIAL)
 
     def _use_graph_set(self, name: str) -> None:

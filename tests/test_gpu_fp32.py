@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _trainer(dev, B, n_train, dropout, graph_steps=0, seed=1, n_test=0):
+def _trainer(dev, B, n_train, dropout, graph_steps=0, seed=1, n_test=0, overlap=False):
     torch.manual_seed(seed)
     net = Net()
     ref = copy.deepcopy(net)
@@ -33,8 +33,9 @@ def _trainer(dev, B, n_train, dropout, graph_steps=0, seed=1, n_test=0):
     te = load_mnist(synthetic_data=True, train=False, synthetic_size=n_test, verbose=False) if n_test else None
     ms = ModelState(net, dev, lr=1.0)
     t = FusedTrainer(ms, tr, te, B, 1000, num_samples=n_train, seed=seed, graph_steps=graph_steps,
-                     dropout=dropout, fp32=True)
-    assert t.fp32 and t.engine.fp32 and t.engine.schedule == t.C.SCHED_SERIAL
+                     dropout=dropout, fp32=True, overlap=overlap)
+    assert t.fp32 and t.engine.fp32
+    assert t.engine.schedule == (t.C.SCHED_OVERLAP if overlap else t.C.SCHED_SERIAL)
     return ref, ms, t, tr, te
 
 
@@ -116,6 +117,24 @@ def test_fp32_training_graphs_bitwise_equal_eager_and_converge(cuda_device):
     assert torch.equal(tg.loss_log, te.loss_log)
     l1, c1, _ = tg.evaluate()
     assert l1 < 0.5 * l0 and c1 / n > 0.75, (l0 / n, l1 / n, c1 / n)   # 30 steps: 2.30 -> 0.50, 83.7 %
+
+
+@pytest.mark.parametrize("graph_steps", [0, 4])
+def test_fp32_overlap_schedule_bitwise_equals_serial(cuda_device, graph_steps):
+    """The fp32 OVERLAP schedule (the fc update on the comm stream beside the conv backward, the next
+    step's first kernel held by device counters; split-captured chunks) trains bitwise like SERIAL."""
+    idx = torch.randperm(2000, generator=torch.Generator().manual_seed(5))
+    _, ms_o, to, _, _ = _trainer(cuda_device, 200, 2000, dropout=True, graph_steps=graph_steps, overlap=True)
+    _, ms_s, ts, _, _ = _trainer(cuda_device, 200, 2000, dropout=True, graph_steps=graph_steps)
+    for ep in (1, 2):
+        to.train_epoch(ep, idx)
+        ts.train_epoch(ep, idx)
+    to.synchronize()
+    ts.synchronize()
+    assert torch.equal(ms_o.param, ms_s.param)
+    assert torch.equal(ms_o.square_avg, ms_s.square_avg) and torch.equal(ms_o.acc_delta, ms_s.acc_delta)
+    assert torch.equal(to.loss_log, ts.loss_log)
+    assert ms_o.get_step() == ms_s.get_step()
 
 
 def test_mnist_ddp_dtype_fp32_runs_fused_fp32(cuda_device, tmp_path):
