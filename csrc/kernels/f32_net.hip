@@ -22,13 +22,15 @@
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <stdexcept>
 
 namespace mnist {
 
 namespace {
-constexpr int BK = 16;                 // GEMM k-tile (4 MFMA k-steps of 4)
+constexpr int BK = 16;                 // split-K chunk granularity (the GEMM k-tile is 16 or 32)
 constexpr int NPIX1 = H1 * H1;         // 676 conv1 output pixels
 constexpr int NPIX2 = H2 * H2;         // 576 conv2 output pixels
 constexpr int K2 = 9 * C1;             // 288 conv2 reduction length (tap, ci)
@@ -57,7 +59,7 @@ __device__ __forceinline__ const uint8_t* image_row(const F32Step& a, int step, 
 // elements: the scalar form spent more VALU issue on addressing than the MFMAs took (the conv GEMMs
 // ran at 30-38 % of the f32 matrix peak).  Vector axes are 4-aligned (M, N, K multiples of 4 on
 // them, split-K chunks multiples of 16); a policy whose vector crosses its bound zero-fills itself.
-template <int BM, int BN, class P>
+template <int BM, int BN, int BK, class P>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
   static_assert((BM / 32) * (BN / 32) == 4, "4 waves of 32 x 32");
   constexpr int NA = BM * BK / 4, NB = BN * BK / 4;            // float4s per operand tile
@@ -145,10 +147,22 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
       }
 }
 
+// k-tile: 16 (4 MFMA k-steps per barrier pair) or 32 (MNIST_AMD_F32_KT=32, A/B knob)
+inline int f32_ktile() {
+  static const int kt = [] {
+    const char* v = getenv("MNIST_AMD_F32_KT");
+    return v && atoi(v) == 32 ? 32 : 16;
+  }();
+  return kt;
+}
+
 template <int BM, int BN, class P>
 void gemm(const P& p, int splits, hipStream_t s) {
   const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, P>), grid, dim3(256), 0, s, p);
+  if (f32_ktile() == 32)
+    hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, 32, P>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, 16, P>), grid, dim3(256), 0, s, p);
 }
 
 // ---- policies
