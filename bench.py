@@ -333,10 +333,12 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
         if args.allreduce != "xgmi":       # the RCCL communicator initialises while data / model build
             with phases.phase("rccl_comm_start"):
                 pending = start_rccl_comm(world, rank, local)
-    xgmi_pending = None
+    xgmi_pending = streams = None
     if world > 1 and args.allreduce != "rccl":   # so does the xGMI communicator (helper thread)
+        from pytorch_mnist_ddp_amd.engine.trainer import make_streams
         from pytorch_mnist_ddp_amd.ops import native
         from pytorch_mnist_ddp_amd.parallel.distributed import PendingXgmiComm
+        streams = make_streams(dev)              # (the trainer's streams before the thread's)
         with phases.phase("xgmi_comm_start"):
             xgmi_pending = PendingXgmiComm(world, rank, dev, int(native.load().PARAM_TOTAL))
 
@@ -363,7 +365,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
                       comm=comm, seed=args.seed, graph_steps=args.graph_steps,
                       two_buckets=not args.single_bucket, allreduce=args.allreduce,
-                      fp32=args.dtype == "fp32", xgmi_pending=xgmi_pending)
+                      fp32=args.dtype == "fp32", xgmi_pending=xgmi_pending, streams=streams)
     diag.tr = tr
     phases.add("trainer", time.perf_counter() - t_tr)
 

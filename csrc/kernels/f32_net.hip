@@ -17,8 +17,9 @@
 //     engines drop the same units of the same step; every reduction runs in a fixed order
 //     (split-K partial slabs summed by one kernel), so the step is bitwise repeatable.
 // Layouts (fp32): a1 [B][26][26][32] (NHWC, ReLU applied; its storage is reused for the conv1
-// pre-activation gradient), y2 / dy2 [B][24][24][64] (conv2 pre-activation / its gradient, shared
-// storage), p [B][9216] torch flatten order, pm u8 [B][9216] (bits 0-1 argmax, 2 keep, 3 pooled > 0).
+// pre-activation gradient), y2 [B][24][24][64] (conv2 pre-activation; its storage then holds the
+// compact gradient wrt the conv2 output, DyCompact), p [B][9216] torch flatten order, pm u8 [B][9216]
+// (bits 0-1 argmax, 2 keep, 3 pooled > 0).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
@@ -210,12 +211,32 @@ struct PFc1W {
   __device__ void put(int m, int n, float v, int) const { g[(int64_t)m * NFLAT + n] = v; }
 };
 
+// The gradient wrt the conv2 output (the max-pool backward input) is kept COMPACT: per image and
+// pooled position the 64 pooled gradients (already dropout-scaled and ReLU-masked, fp32) and the 64
+// argmax routes (2x2 window code, one byte each), both position-major - dyp [B][144][64] fp32 and
+// rt [B][144][64] u8, in the (dead) y2 storage.  The dense dy2[b][y][x][c] = (rt == window code of
+// (y, x)) ? dyp : 0 is decoded inside the conv2 gradient GEMMs' operand loads (4 channels at once),
+// so the 75 %-zero dense tensor (29.5 MB at B = 200) is never written or read.
+struct DyCompact {
+  const float* dyp;
+  const uint8_t* rt;
+  __device__ DyCompact(const float* y2, int B) : dyp(y2), rt(reinterpret_cast<const uint8_t*>(y2 + (int64_t)B * NFLAT)) {}
+  // dy2[b][oy][ox][c..c+3]
+  __device__ __forceinline__ float4 load4(int b, int oy, int ox, int c) const {
+    const int64_t i = ((int64_t)b * NPOOL + (oy >> 1) * HP + (ox >> 1)) * C2 + c;
+    const float4 g = *reinterpret_cast<const float4*>(dyp + i);
+    const uint32_t r = *reinterpret_cast<const uint32_t*>(rt + i);
+    const uint32_t q = (uint32_t)(((oy & 1) << 1) | (ox & 1));
+    return make_float4((r & 0xffu) == q ? g.x : 0.0f, ((r >> 8) & 0xffu) == q ? g.y : 0.0f,
+                       ((r >> 16) & 0xffu) == q ? g.z : 0.0f, (r >> 24) == q ? g.w : 0.0f);
+  }
+};
+
 // fc1 input gradient dp[b][j] = sum_o dz1[b][o] w1[o][j], through dropout-1 and the max-pool +
-// ReLU backward in the epilogue: the 2 x 2 window's four conv2-output gradients (one non-zero).
-// N runs position-major (n = pos * 64 + c, B operand = the w1p copy): the 16 consecutive columns of
-// an MFMA output row are 16 channels of one pixel, so each of the four NHWC dy2 stores is a 64-byte
-// run (in torch order the lanes were 2 pixels = 512 B apart: 29.5 MB of scattered 4-byte stores,
-// 79.5 us of a 555 us step at B = 200)
+// ReLU masks in the epilogue, stored compact (DyCompact).  N runs position-major (n = pos * 64 + c,
+// B operand = the w1p copy): the 16 consecutive columns of an MFMA output row are 16 channels of
+// one position, so each store is a 64-B (gradient) / 16-B (route) run.  (The dense NHWC dy2 written
+// in torch order took 79.5 us of a 555 us step at B = 200; dense position-major 24 us.)
 struct PFc1X {
   static constexpr bool A_KF = true, B_KF = false;
   int M, N, K, kc;
@@ -232,14 +253,12 @@ struct PFc1X {
   __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)m * NH + k); }
   __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w1p + (int64_t)k * NFLAT + n); }
   __device__ void put(int m, int n, float v, int) const {
-    const int c = n & (C2 - 1), pos = n >> 6, py = pos / HP, px = pos - py * HP;
+    const int c = n & (C2 - 1), pos = n >> 6;
     const uint32_t fl = pm[(int64_t)m * NFLAT + c * NPOOL + pos];
     const float g = ((fl & 12u) == 12u) ? v * dscale : 0.0f;    // kept by dropout, ReLU alive
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int y = 2 * py + (q >> 1), x = 2 * px + (q & 1);
-      dy2[(((int64_t)m * H2 + y) * H2 + x) * C2 + c] = ((int)(fl & 3u) == q) ? g : 0.0f;
-    }
+    const int64_t i = ((int64_t)m * NPOOL + pos) * C2 + c;       // compact form (DyCompact)
+    dy2[i] = g;
+    reinterpret_cast<uint8_t*>(dy2 + (int64_t)M * NFLAT)[i] = (uint8_t)(fl & 3u);
   }
 };
 
@@ -248,11 +267,15 @@ struct PFc1X {
 struct PConv2W {
   static constexpr bool A_KF = false, B_KF = false;
   int M, N, K, kc;
-  const float* dy2;
+  const float* dy2;     // compact (DyCompact)
   const float* a1;
   float* part;
+  int B;
   __device__ void prepare() {}
-  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dy2 + (int64_t)k * C2 + m); }
+  __device__ float4 a4(int m, int k) const {
+    const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
+    return DyCompact(dy2, B).load4(b, oy, ox, m);
+  }
   __device__ float4 b4(int k, int n) const {
     if (n >= K2) return make_float4(1.0f, 0.0f, 0.0f, 0.0f);      // the bias column (n = 288) + padding
     const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
@@ -267,17 +290,17 @@ struct PConv2W {
 struct PConv2X {
   static constexpr bool A_KF = true, B_KF = false;
   int M, N, K, kc;
-  const float* dy2;
+  const float* dy2;     // compact (DyCompact)
   const float* w2bwd;   // [tap][co][ci]
   float* a1;
+  int B;
   __device__ void prepare() {}
   __device__ float4 a4(int m, int k) const {
     const int b = m / NPIX1, pix = m - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
     const int tap = k >> 6, co = k & 63, ky = tap / 3, kx = tap - 3 * ky;
     const int oy = iy - ky, ox = ix - kx;
-    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
-               ? *reinterpret_cast<const float4*>(dy2 + (((int64_t)b * H2 + oy) * H2 + ox) * C2 + co)
-               : make_float4(0.f, 0.f, 0.f, 0.f);
+    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2) ? DyCompact(dy2, B).load4(b, oy, ox, co)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w2bwd + k * C1 + n); }
   __device__ void put(int m, int n, float v, int) const {
@@ -318,7 +341,7 @@ __global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
   const uint8_t* src = image_row(a, state_of(a)->step, b) + y * IMG + x;
   float xv[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) xv[k] = normalize_u8_alu(src[(k / 3) * IMG + k % 3]);
+  for (int k = 0; k < 9; ++k) xv[k] = normalize_u8(src[(k / 3) * IMG + k % 3]);   // (LUT: the same bits)
   const float* w = a.param + OFF_CONV1_W;
   const float* bias = a.param + OFF_CONV1_B;
   float o[4];
@@ -510,39 +533,46 @@ __global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
 
 // conv1 weight + bias gradient (M = 32 channels, N = 9 taps + bias, K = B*676 pixels: far too thin
 // for the GEMM tile, whose 64 x 64 MFMA tiles were 92 % padding): F32_C1W_BLOCKS workgroups, g sums
-// pixels [g*P/G, (g+1)*P/G) on the VALU - thread = (pixel lane 0..7, channel), a coalesced 128-B da1
-// row per pixel and the 3x3 input patch as broadcast byte loads, 4 pixels' loads in flight - then
-// the 8 pixel lanes in fixed order through LDS: part[g][c][0..9].  The work is 4.3 M (pixel,
-// channel) pairs of 10 FMAs: latency, not arithmetic - so ~1000 workgroups of a few pixels each
-// (128 workgroups of ~130 pixels per thread took 86 us)
+// pixels [g*P/G, (g+1)*P/G) on the VALU.  Each image the range touches is normalised once into LDS
+// (the 784 inputs through the constant LUT: bitwise the fp32 divisions), then thread = (pixel lane
+// 0..7, channel) takes a coalesced 128-B da1 row per pixel and its 3x3 patch as LDS broadcast reads,
+// 4 pixels' loads in flight; the 8 pixel lanes are added in fixed order through LDS:
+// part[g][c][0..9].  (One thread per channel doing its own 64-bit index math and 9 IEEE-division
+// normalisations per pixel: 40 us at B = 200.)
 __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G) {
   __shared__ float red[8][C1 * 10];
+  __shared__ float img[IMG * IMG];
   const int g = blockIdx.x, tid = threadIdx.x, c = tid & 31, pl = tid >> 5;
-  const int64_t P = (int64_t)B * NPIX1;
-  const int64_t lo = P * g / G, hi = P * (g + 1) / G;
+  const int P = B * NPIX1;                                       // < 2^31 for any batch the engine takes
+  const int lo = (int)((int64_t)P * g / G), hi = (int)((int64_t)P * (g + 1) / G);
   const int step = state_of(a)->step;
   float acc[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) acc[j] = 0.f;
-  constexpr int U = 4;
-  for (int64_t m0 = lo + pl; m0 < hi; m0 += 8 * U) {
-    float d[U], x[U][9];
+  for (int b = lo / NPIX1; b * NPIX1 < hi; ++b) {               // workgroup-uniform
+    const uint8_t* src = image_row(a, step, b);
+    __syncthreads();                                             // the previous image's reads are done
+    for (int i = tid; i < IMG * IMG; i += 256) img[i] = normalize_u8(src[i]);
+    __syncthreads();
+    const int p0 = max(lo, b * NPIX1), p1 = min(hi, (b + 1) * NPIX1);
+    constexpr int U = 4;
+    for (int m0 = p0 + pl; m0 < p1; m0 += 8 * U) {
+      float d[U];
+      int off[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t m = m0 + 8 * u;
-      const bool ok = m < hi;
-      const int64_t mm = ok ? m : lo;
-      const int b = (int)(mm / NPIX1), pix = (int)(mm - (int64_t)b * NPIX1), iy = pix / H1, ix = pix - iy * H1;
-      const uint8_t* src = image_row(a, step, b) + iy * IMG + ix;
-      d[u] = ok ? a.a1[mm * C1 + c] : 0.0f;
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + 8 * u;
+        const bool ok = m < p1;
+        const int pix = (ok ? m : p0) - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
+        off[u] = iy * IMG + ix;
+        d[u] = ok ? a.a1[(int64_t)(ok ? m : p0) * C1 + c] : 0.0f;
+      }
 #pragma unroll
-      for (int k = 0; k < 9; ++k) x[u][k] = normalize_u8_alu(src[(k / 3) * IMG + k % 3]);
-    }
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc[k] = __builtin_fmaf(d[u], x[u][k], acc[k]);
-      acc[9] += d[u];
+        for (int k = 0; k < 9; ++k) acc[k] = __builtin_fmaf(d[u], img[off[u] + (k / 3) * IMG + k % 3], acc[k]);
+        acc[9] += d[u];
+      }
     }
   }
 #pragma unroll
@@ -662,8 +692,8 @@ void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s) {
   gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
   const int64_t k2 = (int64_t)B * NPIX2;
   const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
-  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part}, s2, s);
-  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
+  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part, B}, s2, s);
+  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1, B}, 1, s);
   const int s1 = f32_conv1w_splits(B);
   hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
   hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, s2, s1);

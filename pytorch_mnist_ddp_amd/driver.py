@@ -316,8 +316,12 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         if distributed:
             torch.cuda.set_device(gpu)       # (deferred by init_distributed_mode: runtime is up now)
     allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
-    xgmi_pending = None
+    xgmi_pending = streams = None
     if distributed and world > 1 and allreduce in ("xgmi", "auto"):
+        # the trainer's two streams first: the setup thread's self-test streams must not take the
+        # hardware queues they would otherwise get (few queues per process in one-GPU rehearsals)
+        from .engine.trainer import make_streams
+        streams = make_streams(device)
         # the xGMI communicator (IPC export / exchange / peer mapping / self-test) builds on a helper
         # thread while this one builds the model, wraps it and allocates the trainer's buffers
         from .ops import native
@@ -354,7 +358,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                            args.batch_size, args.test_batch_size, num_samples=len(train_stream),
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
                            allreduce=allreduce, two_buckets=two_buckets,
-                           fp32=getattr(args, "dtype", "bf16") == "fp32", xgmi_pending=xgmi_pending)
+                           fp32=getattr(args, "dtype", "bf16") == "fp32", xgmi_pending=xgmi_pending,
+                           streams=streams)
     if xgmi_pending is not None:
         setup.add_info("xgmi_setup_thread_s", xgmi_pending.seconds)
     setup.mark("trainer")

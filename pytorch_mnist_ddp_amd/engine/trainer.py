@@ -114,6 +114,11 @@ class StartupValidationError(RuntimeError):
         self.setup = setup
 
 
+def make_streams(dev) -> tuple:
+    """The trainer's compute and (high-priority) comm streams."""
+    return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev, priority=-1)
+
+
 class FusedTrainer:
     """``allreduce`` (DDP): "rccl", "xgmi" or "auto" (default).  Every candidate transport is built
     and its PRODUCTION schedule - the captured chunk graph training replays - is validated and timed
@@ -130,7 +135,8 @@ class FusedTrainer:
                  test_batch_size: int, num_samples: int, world_size: int = 1, rank: int = 0,
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
                  two_buckets: bool = True, allreduce: str | None = None, overlap: bool = True,
-                 xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False, xgmi_pending=None):
+                 xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False, xgmi_pending=None,
+                 streams=None):
         C = native.load()
         self.C, self.ms = C, mstate
         # host seconds per setup phase (engine, xgmi_comm, stream_probe, validate.<transport>,
@@ -147,8 +153,9 @@ class FusedTrainer:
         self.num_samples = int(num_samples)                 # per-rank samples per epoch
         self.steps_per_epoch = math.ceil(self.num_samples / self.B)
         self.rng_base = 0
-        self.compute = torch.cuda.Stream(device=dev)
-        self.comm_stream = torch.cuda.Stream(device=dev, priority=-1)
+        # (``streams``: created by a caller that starts other stream users first - the xGMI setup
+        # thread's self-test - so these two are the process's first and keep their own hardware queues)
+        self.compute, self.comm_stream = streams if streams is not None else make_streams(dev)
         # ---- device-resident data
         self.train_u8 = train.images.reshape(len(train), -1).contiguous().to(dev)
         self.train_labels = train.targets.to(torch.int32).to(dev)
@@ -255,10 +262,6 @@ class FusedTrainer:
                                          and (self.world > 1 or probe_world1))
         want_r = comm is not None and allreduce in ("rccl", "auto")
         x = None
-        # compute / comm streams on distinct hardware queues: the device-counter hand-offs of the
-        # XGMI schedule and of the RCCL schedule's fc update need it (one probe, every rank)
-        handoff = self._probe_streams() if (want_x or (want_r and two_buckets)) else False
-        self.engine.set_rccl_handoff(handoff)
         pending, self._xgmi_pending = self._xgmi_pending, None
         if pending is not None and not want_x:      # started by the caller, not a candidate after all
             with self.setup.phase("xgmi_comm"):
@@ -275,6 +278,13 @@ class FusedTrainer:
                     sub = {}
                     x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel(), timings=sub)
                 self.setup.add_info("xgmi_comm_steps_s", sub)
+        # compute / comm streams on distinct hardware queues: the device-counter hand-offs of the
+        # XGMI schedule and of the RCCL schedule's fc update need it (one probe, every rank; after
+        # the xGMI setup, whose self-test keeps three more streams busy - with few hardware queues per
+        # process, as in the one-GPU rehearsals, the two would share queues)
+        handoff = self._probe_streams() if (x is not None or (want_r and two_buckets)) else False
+        self.engine.set_rccl_handoff(handoff)
+        if want_x:
             if x is not None and not handoff:
                 if self.rank == 0:
                     print("[engine] compute/comm streams share a hardware queue: no xGMI schedule", flush=True)
