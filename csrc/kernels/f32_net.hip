@@ -17,9 +17,8 @@
 //     engines drop the same units of the same step; every reduction runs in a fixed order
 //     (split-K partial slabs summed by one kernel), so the step is bitwise repeatable.
 // Layouts (fp32): a1 [B][26][26][32] (NHWC, ReLU applied; its storage is reused for the conv1
-// pre-activation gradient), y2 [B][24][24][64] (conv2 pre-activation; its storage then holds the
-// compact gradient wrt the conv2 output, DyCompact), p [B][9216] torch flatten order, pm u8 [B][9216]
-// (bits 0-1 argmax, 2 keep, 3 pooled > 0).
+// pre-activation gradient), y2 / dy2 [B][24][24][64] (conv2 pre-activation / its gradient, shared
+// storage), p [B][9216] torch flatten order, pm u8 [B][9216] (bits 0-1 argmax, 2 keep, 3 pooled > 0).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
@@ -60,6 +59,11 @@ __device__ __forceinline__ const uint8_t* image_row(const F32Step& a, int step, 
 // elements: the scalar form spent more VALU issue on addressing than the MFMAs took (the conv GEMMs
 // ran at 30-38 % of the f32 matrix peak).  Vector axes are 4-aligned (M, N, K multiples of 4 on
 // them, split-K chunks multiples of 16); a policy whose vector crosses its bound zero-fills itself.
+template <class P, class = void>
+struct has_put4 { static constexpr bool value = false; };
+template <class P>
+struct has_put4<P, decltype(void(P::PUT4))> { static constexpr bool value = P::PUT4; };
+
 template <int BM, int BN, int BK, class P>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
   static_assert((BM / 32) * (BN / 32) == 4, "4 waves of 32 x 32");
@@ -139,13 +143,17 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      const int mb = m0 + wm * 32 + i * 16 + 4 * (lane >> 4);
+      const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+      if constexpr (has_put4<P>::value) {       // the lane's 4 consecutive rows at once (M % 4 == 0)
+        if (mb < p.M && n < p.N) p.put4(mb, n, acc[i][j], blockIdx.z);
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
-        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-        if (m < p.M && n < p.N) p.put(m, n, acc[i][j][r], blockIdx.z);
+        for (int r = 0; r < 4; ++r)
+          if (mb + r < p.M && n < p.N) p.put(mb + r, n, acc[i][j][r], blockIdx.z);
       }
+    }
 }
 
 // k-tile: 16 (4 MFMA k-steps per barrier pair) or 32 (MNIST_AMD_F32_KT=32, A/B knob)
@@ -211,35 +219,17 @@ struct PFc1W {
   __device__ void put(int m, int n, float v, int) const { g[(int64_t)m * NFLAT + n] = v; }
 };
 
-// The gradient wrt the conv2 output (the max-pool backward input) is kept COMPACT: per image and
-// pooled position the 64 pooled gradients (already dropout-scaled and ReLU-masked, fp32) and the 64
-// argmax routes (2x2 window code, one byte each), both position-major - dyp [B][144][64] fp32 and
-// rt [B][144][64] u8, in the (dead) y2 storage.  The dense dy2[b][y][x][c] = (rt == window code of
-// (y, x)) ? dyp : 0 is decoded inside the conv2 gradient GEMMs' operand loads (4 channels at once),
-// so the 75 %-zero dense tensor (29.5 MB at B = 200) is never written or read.
-struct DyCompact {
-  const float* dyp;
-  const uint8_t* rt;
-  __device__ DyCompact(const float* y2, int B) : dyp(y2), rt(reinterpret_cast<const uint8_t*>(y2 + (int64_t)B * NFLAT)) {}
-  // dy2[b][oy][ox][c..c+3]
-  __device__ __forceinline__ float4 load4(int b, int oy, int ox, int c) const {
-    const int64_t i = ((int64_t)b * NPOOL + (oy >> 1) * HP + (ox >> 1)) * C2 + c;
-    const float4 g = *reinterpret_cast<const float4*>(dyp + i);
-    const uint32_t r = *reinterpret_cast<const uint32_t*>(rt + i);
-    const uint32_t q = (uint32_t)(((oy & 1) << 1) | (ox & 1));
-    return make_float4((r & 0xffu) == q ? g.x : 0.0f, ((r >> 8) & 0xffu) == q ? g.y : 0.0f,
-                       ((r >> 16) & 0xffu) == q ? g.z : 0.0f, (r >> 24) == q ? g.w : 0.0f);
-  }
-};
-
 // fc1 input gradient dp[b][j] = sum_o dz1[b][o] w1[o][j], through dropout-1 and the max-pool +
-// ReLU masks in the epilogue, stored compact (DyCompact).  N runs position-major (n = pos * 64 + c,
-// B operand = the w1p copy): the 16 consecutive columns of an MFMA output row are 16 channels of
-// one position, so each store is a 64-B (gradient) / 16-B (route) run.  (The dense NHWC dy2 written
-// in torch order took 79.5 us of a 555 us step at B = 200; dense position-major 24 us.)
+// ReLU backward in the epilogue: the 2 x 2 window's four conv2-output gradients (one non-zero).
+// Computed TRANSPOSED - rows = fc1 inputs j in position-major order (j' = pos * 64 + c, A operand =
+// the w1p copy), columns = images - so each lane's four MFMA accumulators are 4 consecutive channels
+// of one pooled position of one image: the four dense NHWC dy2 stores are 16-B vectors (put4).
+// (In torch order the lanes were 2 pixels = 512 B apart: 29.5 MB of scattered 4-byte stores took
+// 79.5 us of a 555 us step at B = 200; position-major 4-byte stores 22-24 us.  A compact dy2 decoded
+// inside the conv2 GEMM loads instead cost those GEMMs more VALU than the stores it saved: 27 us.)
 struct PFc1X {
-  static constexpr bool A_KF = true, B_KF = false;
-  int M, N, K, kc;
+  static constexpr bool A_KF = false, B_KF = true, PUT4 = true;
+  int M, N, K, kc;      // M = 9216 (j'), N = B, K = 128
   const float* dz1;
   const float* w1p;
   const uint8_t* pm;
@@ -250,15 +240,25 @@ struct PFc1X {
     const StepState* s = st ? st : &g_zero_state;
     dscale = (s->flags & STEP_FLAG_NO_DROPOUT) ? 1.0f : (1.0f / KEEP1);
   }
-  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)m * NH + k); }
-  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w1p + (int64_t)k * NFLAT + n); }
-  __device__ void put(int m, int n, float v, int) const {
-    const int c = n & (C2 - 1), pos = n >> 6;
-    const uint32_t fl = pm[(int64_t)m * NFLAT + c * NPOOL + pos];
-    const float g = ((fl & 12u) == 12u) ? v * dscale : 0.0f;    // kept by dropout, ReLU alive
-    const int64_t i = ((int64_t)m * NPOOL + pos) * C2 + c;       // compact form (DyCompact)
-    dy2[i] = g;
-    reinterpret_cast<uint8_t*>(dy2 + (int64_t)M * NFLAT)[i] = (uint8_t)(fl & 3u);
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(w1p + (int64_t)k * NFLAT + m); }
+  __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)n * NH + k); }
+  __device__ void put4(int m, int n, const floatx4& v, int) const {
+    const int c = m & (C2 - 1), pos = m >> 6, py = pos / HP, px = pos - py * HP;
+    const uint8_t* f = pm + (int64_t)n * NFLAT + c * NPOOL + pos;
+    uint32_t fl[4];
+    float g[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fl[j] = f[j * NPOOL];
+      g[j] = ((fl[j] & 12u) == 12u) ? v[j] * dscale : 0.0f;       // kept by dropout, ReLU alive
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int y = 2 * py + (q >> 1), x = 2 * px + (q & 1);
+      *reinterpret_cast<float4*>(dy2 + (((int64_t)n * H2 + y) * H2 + x) * C2 + c) =
+          make_float4((int)(fl[0] & 3u) == q ? g[0] : 0.0f, (int)(fl[1] & 3u) == q ? g[1] : 0.0f,
+                      (int)(fl[2] & 3u) == q ? g[2] : 0.0f, (int)(fl[3] & 3u) == q ? g[3] : 0.0f);
+    }
   }
 };
 
@@ -267,15 +267,11 @@ struct PFc1X {
 struct PConv2W {
   static constexpr bool A_KF = false, B_KF = false;
   int M, N, K, kc;
-  const float* dy2;     // compact (DyCompact)
+  const float* dy2;
   const float* a1;
   float* part;
-  int B;
   __device__ void prepare() {}
-  __device__ float4 a4(int m, int k) const {
-    const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
-    return DyCompact(dy2, B).load4(b, oy, ox, m);
-  }
+  __device__ float4 a4(int m, int k) const { return *reinterpret_cast<const float4*>(dy2 + (int64_t)k * C2 + m); }
   __device__ float4 b4(int k, int n) const {
     if (n >= K2) return make_float4(1.0f, 0.0f, 0.0f, 0.0f);      // the bias column (n = 288) + padding
     const int b = k / NPIX2, pix = k - b * NPIX2, oy = pix / H2, ox = pix - oy * H2;
@@ -290,17 +286,17 @@ struct PConv2W {
 struct PConv2X {
   static constexpr bool A_KF = true, B_KF = false;
   int M, N, K, kc;
-  const float* dy2;     // compact (DyCompact)
+  const float* dy2;
   const float* w2bwd;   // [tap][co][ci]
   float* a1;
-  int B;
   __device__ void prepare() {}
   __device__ float4 a4(int m, int k) const {
     const int b = m / NPIX1, pix = m - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
     const int tap = k >> 6, co = k & 63, ky = tap / 3, kx = tap - 3 * ky;
     const int oy = iy - ky, ox = ix - kx;
-    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2) ? DyCompact(dy2, B).load4(b, oy, ox, co)
-                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    return (oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
+               ? *reinterpret_cast<const float4*>(dy2 + (((int64_t)b * H2 + oy) * H2 + ox) * C2 + co)
+               : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w2bwd + k * C1 + n); }
   __device__ void put(int m, int n, float v, int) const {
@@ -689,11 +685,11 @@ void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s) {
 // the rest: fc1 input gradient (reads the w1p copy, not the fc1 parameters the update rewrites),
 // conv2 weight / input gradients, conv1 weight gradient, slab reduce
 void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s) {
-  gemm<64, 64>(PFc1X{B, NFLAT, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
+  gemm<64, 64>(PFc1X{NFLAT, B, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
   const int64_t k2 = (int64_t)B * NPIX2;
   const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
-  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part, B}, s2, s);
-  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1, B}, 1, s);
+  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part}, s2, s);
+  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
   const int s1 = f32_conv1w_splits(B);
   hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
   hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, s2, s1);
