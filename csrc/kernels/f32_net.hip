@@ -22,8 +22,6 @@
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
-#include <stdlib.h>
-
 #include <algorithm>
 #include <stdexcept>
 
@@ -156,22 +154,18 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
     }
 }
 
-// k-tile: 16 (4 MFMA k-steps per barrier pair) or 32 (MNIST_AMD_F32_KT=32, A/B knob)
-inline int f32_ktile() {
-  static const int kt = [] {
-    const char* v = getenv("MNIST_AMD_F32_KT");
-    return v && atoi(v) == 32 ? 32 : 16;
-  }();
-  return kt;
-}
+// k-tile: P::KT when the policy sets one (the thin fc GEMMs: fewer, fuller k-iterations), else 16
+// (4 MFMA k-steps per barrier pair; 32 for every GEMM measured the same step time: 0.3367-0.3388 vs
+// 0.3360-0.3367 ms)
+template <class P, class = void>
+struct kt_of { static constexpr int value = 16; };
+template <class P>
+struct kt_of<P, decltype(void(P::KT))> { static constexpr int value = P::KT; };
 
 template <int BM, int BN, class P>
 void gemm(const P& p, int splits, hipStream_t s) {
   const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
-  if (f32_ktile() == 32)
-    hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, 32, P>), grid, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, 16, P>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, kt_of<P>::value, P>), grid, dim3(256), 0, s, p);
 }
 
 // ---- policies
@@ -196,6 +190,7 @@ struct PConv2Fwd {
 // fc1 forward, split-K partial sums: z1part[z][b][o] = sum_(i in split z) p[b][i] w1[o][i]
 struct PFc1 {
   static constexpr bool A_KF = true, B_KF = true;
+  static constexpr int KT = 32;
   int M, N, K, kc;
   const float* p;
   const float* w1;
@@ -209,6 +204,7 @@ struct PFc1 {
 // fc1 weight gradient: g[o][i] = sum_b dz1[b][o] p[b][i]
 struct PFc1W {
   static constexpr bool A_KF = false, B_KF = false;
+  static constexpr int KT = 32;
   int M, N, K, kc;
   const float* dz1;
   const float* p;
@@ -229,6 +225,7 @@ struct PFc1W {
 // inside the conv2 GEMM loads instead cost those GEMMs more VALU than the stores it saved: 27 us.)
 struct PFc1X {
   static constexpr bool A_KF = false, B_KF = true, PUT4 = true;
+  static constexpr int KT = 32;
   int M, N, K, kc;      // M = 9216 (j'), N = B, K = 128
   const float* dz1;
   const float* w1p;
@@ -325,25 +322,29 @@ __global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a, int train) {
       make_float4(src[c * NPOOL], src[(c + 1) * NPOOL], src[(c + 2) * NPOOL], src[(c + 3) * NPOOL]);
 }
 
-// conv1 + bias + ReLU: one thread = 4 channels of one output pixel (the bf16 engine's fma order);
-// 8 consecutive lanes cover a pixel's 32 channels, so each float4 store instruction writes 8 whole
-// pixels (1 KB contiguous; one thread per pixel wrote 64 lines in 16-B pieces per instruction)
+// conv1 + bias + ReLU: workgroup = 32 output pixels of one image, thread = 4 channels of one pixel
+// (the bf16 engine's fma order).  The image is normalised once into LDS (784 LUT loads per workgroup
+// instead of 9 per thread), and 8 consecutive lanes cover a pixel's 32 channels, so each float4 store
+// instruction writes 8 whole pixels (1 KB contiguous)
+constexpr int C1_PIX_PER_WG = 32, C1_WG_PER_IMG = (NPIX1 + C1_PIX_PER_WG - 1) / C1_PIX_PER_WG;   // 22
 __global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)B * NPIX1 * 8) return;
-  const int64_t q = t >> 3;
-  const int c4 = (int)(t & 7);
-  const int b = (int)(q / NPIX1), pix = (int)(q - (int64_t)b * NPIX1), y = pix / H1, x = pix - y * H1;
-  const uint8_t* src = image_row(a, state_of(a)->step, b) + y * IMG + x;
+  __shared__ float img[IMG * IMG];
+  const int b = blockIdx.x / C1_WG_PER_IMG, part = blockIdx.x - b * C1_WG_PER_IMG;
+  const uint8_t* src = image_row(a, state_of(a)->step, b);
+  for (int i = threadIdx.x; i < IMG * IMG; i += 256) img[i] = normalize_u8(src[i]);   // (LUT: the same bits)
+  __syncthreads();
+  const int pix = part * C1_PIX_PER_WG + (threadIdx.x >> 3), c4 = threadIdx.x & 7;
+  if (pix >= NPIX1) return;
+  const int y = pix / H1, x = pix - y * H1;
   float xv[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) xv[k] = normalize_u8(src[(k / 3) * IMG + k % 3]);   // (LUT: the same bits)
+  for (int k = 0; k < 9; ++k) xv[k] = img[(y + k / 3) * IMG + x + k % 3];
   const float* w = a.param + OFF_CONV1_W;
   const float* bias = a.param + OFF_CONV1_B;
   float o[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) o[j] = fmaxf(conv1_preact(xv, 3, w + (4 * c4 + j) * 9, bias[4 * c4 + j]), 0.0f);
-  reinterpret_cast<float4*>(a.a1 + q * C1)[c4] = make_float4(o[0], o[1], o[2], o[3]);
+  reinterpret_cast<float4*>(a.a1 + ((int64_t)b * NPIX1 + pix) * C1)[c4] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // ReLU + 2x2 max-pool (first max wins, as torch) + dropout(0.25): one thread = 16 consecutive
@@ -662,7 +663,7 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
   // (training: + the position-major fc1 weight copy for the backward)
   hipLaunchKernelGGL(f32_prep_kernel, dim3(blocks(C2 * K2) + (train ? blocks(NH * NFLAT / 4) : 0)), dim3(256), 0, s,
                      a, train ? 1 : 0);
-  hipLaunchKernelGGL(f32_conv1_kernel, dim3(blocks((int64_t)B * NPIX1 * 8)), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(f32_conv1_kernel, dim3(B * C1_WG_PER_IMG), dim3(256), 0, s, a, B);
   gemm<64, 64>(PConv2Fwd{B * NPIX2, C2, K2, K2, a.a1, a.w2fwd, a.param + OFF_CONV2_B, a.y2}, 1, s);
   if (train)
     hipLaunchKernelGGL(f32_pool_kernel<true>, dim3(blocks((int64_t)B * C2 * 9)), dim3(256), 0, s, a, B);
