@@ -18,7 +18,8 @@
 //     (split-K partial slabs summed by one kernel), so the step is bitwise repeatable.
 // Layouts (fp32): a1 [B][26][26][32] (NHWC, ReLU applied; its storage is reused for the conv1
 // pre-activation gradient), y2 / dy2 [B][24][24][64] (conv2 pre-activation / its gradient, shared
-// storage), p [B][9216] torch flatten order, pm u8 [B][9216] (bits 0-1 argmax, 2 keep, 3 pooled > 0).
+// storage), p [B][9216] torch flatten order, pm u8 [B][144][64] position-major (bits 0-1 argmax,
+// 2 keep, 3 pooled > 0).
 #include "../include/device_utils.h"
 #include "../include/kernels.h"
 
@@ -241,12 +242,12 @@ struct PFc1X {
   __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(dz1 + (int64_t)n * NH + k); }
   __device__ void put4(int m, int n, const floatx4& v, int) const {
     const int c = m & (C2 - 1), pos = m >> 6, py = pos / HP, px = pos - py * HP;
-    const uint8_t* f = pm + (int64_t)n * NFLAT + c * NPOOL + pos;
+    const uint32_t f4 = *reinterpret_cast<const uint32_t*>(pm + (int64_t)n * NFLAT + m);   // pm[n][pos][c..c+3]
     uint32_t fl[4];
     float g[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      fl[j] = f[j * NPOOL];
+      fl[j] = (f4 >> (8 * j)) & 0xffu;
       g[j] = ((fl[j] & 12u) == 12u) ? v[j] * dscale : 0.0f;       // kept by dropout, ReLU alive
     }
 #pragma unroll
@@ -383,7 +384,13 @@ __global__ __launch_bounds__(256) void f32_pool_kernel(F32Step a, int B) {
   float4* dst = reinterpret_cast<float4*>(a.p + (int64_t)b * NFLAT + flat0);
 #pragma unroll
   for (int q = 0; q < 4; ++q) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-  if (TRAIN) *reinterpret_cast<uint4*>(a.pm + (int64_t)b * NFLAT + flat0) = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+  // flags position-major (pm[b][pos][c]: each byte store instruction writes 64 consecutive channels),
+  // the layout the fc1 input-gradient epilogue reads 4 channels at a time
+  if (TRAIN) {
+    uint8_t* pmb = a.pm + (int64_t)b * NFLAT + (16 * j) * C2 + c;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pmb[q * C2] = (uint8_t)(fl[q >> 2] >> (8 * (q & 3)));
+  }
 }
 
 __device__ __forceinline__ void log_softmax10_f32(const float* x, float* lp) {
