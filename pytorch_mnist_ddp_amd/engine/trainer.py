@@ -116,6 +116,7 @@ class StartupValidationError(RuntimeError):
 
 def make_streams(dev) -> tuple:
     """The trainer's compute and (high-priority) comm streams."""
+    # (comm at normal priority, or compute raised instead: 600 steps within noise, profiles/r5/ab/stream_priority.txt)
     return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev, priority=-1)
 
 
