@@ -235,7 +235,7 @@ def ranks_share_a_device(device) -> bool:
 
 def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 3,
                      verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None,
-                     timings: dict | None = None):
+                     timings: dict | None = None, store=None):
     """Direct xGMI all-reduce communicator over ``numel`` floats (csrc/runtime/xgmi_comm.h).
 
     The communicator owns its input / output buffers (``x.grad_in`` / ``x.grad_out``: zero-copy fp32
@@ -246,7 +246,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     to map its peers or to verify (callers then keep the RCCL all-reduce).  ``co_ranks`` (default:
     measured with :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning
     workgroups are resident.  ``timings`` (optional dict) receives host seconds per sub-step
-    (co_ranks, alloc, exchange, connect, verify): the N > 1 startup budget."""
+    (co_ranks, alloc, exchange, connect, verify): the N > 1 startup budget.  ``store``: the client
+    for the record exchange (default: the default process group's)."""
     from torch.utils.dlpack import from_dlpack
 
     from ..ops import native
@@ -275,7 +276,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
         x.grad_out = from_dlpack(x.dlpack("out"))
         lap("alloc")
         if world_size > 1:
-            store = dist.distributed_c10d._get_default_store()
+            if store is None:
+                store = dist.distributed_c10d._get_default_store()
             store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
             keys = [f"{_XGMI_KEY}/{tag}/{q}" for q in range(world_size)]
             store.wait(keys, timedelta(minutes=5))
@@ -311,8 +313,9 @@ class PendingXgmiComm:
     ``seconds`` / ``timings`` are the helper's."""
 
     def __init__(self, world_size: int, rank: int, device, numel: int):
-        from .hostcomm import channel
-        self._hc = channel("xgmi_setup")
+        from .hostcomm import channel, own_store_client
+        self._store = own_store_client()                 # its own socket (None: share the default)
+        self._hc = channel("xgmi_setup", self._store)
         self._args = (world_size, rank, torch.device(device), int(numel))
         self._comm, self._err, self.seconds, self.timings = None, None, None, {}
         self._t = threading.Thread(target=self._run, name="xgmi-setup", daemon=True)
@@ -325,7 +328,7 @@ class PendingXgmiComm:
             world, rank, dev, numel = self._args
             torch.cuda.set_device(dev)
             with use_channel(self._hc):
-                self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings)
+                self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings, store=self._store)
         except BaseException as e:  # noqa: BLE001 - re-raised in result()
             import traceback
             self._err = e
