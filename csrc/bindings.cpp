@@ -419,20 +419,25 @@ PYBIND11_MODULE(_C, m) {
     // the runtime's own first-use costs the setup would otherwise pay on the main thread: the blit
     // kernels behind hipMemset and the staging path of pageable host copies (measured on the box:
     // 80 ms of first hipMemsets, 28 ms of first pageable H2D copies inside the reference timer)
+    clk::time_point tm = t2, th = t2, td = t2;
     {
       constexpr size_t kBytes = 1 << 20;
       void* d = nullptr;
       std::vector<char> h(kBytes, 0);
       if (hipMalloc(&d, kBytes) == hipSuccess) {
         (void)hipMemset(d, 0, kBytes);
+        (void)hipDeviceSynchronize();
+        tm = clk::now();
         (void)hipMemcpy(d, h.data(), kBytes, hipMemcpyHostToDevice);
+        th = clk::now();
         (void)hipMemcpy(h.data(), d, 4096, hipMemcpyDeviceToHost);
+        td = clk::now();
         (void)hipFree(d);
       }
     }
     const auto t3 = clk::now();
     auto sec = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
-    return std::make_tuple(sec(t0, t1), sec(t1, t2), sec(t2, t3));
+    return std::make_tuple(sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t2, tm), sec(tm, th), sec(th, td));
   }, py::call_guard<py::gil_scoped_release>(), py::arg("device"));
   // physical identity of a device (PCI domain:bus:device.function + UUID) straight from the HIP
   // runtime: callable from any thread, no amdsmi (torch.cuda.get_device_properties counts devices

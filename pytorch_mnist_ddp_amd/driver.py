@@ -241,9 +241,10 @@ def _prewarm_body(device, steps: dict | None = None) -> None:
     C = native.load()                        # the _C extension (dlopen; no device work)
     lap("native_load")
     # GIL released: the HIP runtime + context, then every kernel TU's code object
-    t_rt, t_co, t_cp = C.hip_prewarm(device.index if device.index is not None else 0)
+    t_rt, t_co, t_cp, t_ms, t_h2d, t_d2h = C.hip_prewarm(device.index if device.index is not None else 0)
     steps["hip_runtime_context"], steps["code_objects"] = round(t_rt, 4), round(t_co, 4)
     steps["memset_copy_paths"] = round(t_cp, 4)
+    steps["first_memset"], steps["first_h2d"], steps["first_d2h"] = round(t_ms, 4), round(t_h2d, 4), round(t_d2h, 4)
     lap("hip_prewarm_total")
     torch.cuda.init()
     lap("torch_cuda_init")
