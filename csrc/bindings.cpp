@@ -425,7 +425,7 @@ PYBIND11_MODULE(_C, m) {
       void* d = nullptr;
       std::vector<char> h(kBytes, 0);
       if (hipMalloc(&d, kBytes) == hipSuccess) {
-        (void)hipMemset(d, 0, kBytes);
+        launch_fill(d, kBytes, 0, nullptr);         // (our fill kernel: no blit-kernel load)
         (void)hipDeviceSynchronize();
         tm = clk::now();
         (void)hipMemcpy(d, h.data(), kBytes, hipMemcpyHostToDevice);
@@ -460,8 +460,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("memset_sync", [](uintptr_t ptr, int value, int64_t nbytes) {
     // setup-time buffer initialisation without a torch fill kernel (whose code object would load on
     // first launch inside the reference timer); synchronous
-    if (nbytes > 0 && hipMemset(reinterpret_cast<void*>(ptr), value, (size_t)nbytes) != hipSuccess)
-      throw std::runtime_error("memset_sync: hipMemset failed");
+    if (nbytes > 0) {
+      launch_fill(reinterpret_cast<void*>(ptr), nbytes, value, nullptr);
+      if (hipStreamSynchronize(nullptr) != hipSuccess) throw std::runtime_error("memset_sync: fill failed");
+    }
   }, py::call_guard<py::gil_scoped_release>());
   m.def("preload_code_objects", []() {
     preload_trunk();

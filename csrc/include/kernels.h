@@ -189,6 +189,8 @@ void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const 
                         int64_t n, uint8_t* dst_u8, int32_t* dst_labels, hipStream_t s);
 // device-counter stream hand-offs (engine DDP schedule 3)
 void launch_stream_signal(int* ctr, hipStream_t s);
+// byte fill of [p, p + bytes) on `s` (hipMemset's job without the runtime's blit kernels)
+void launch_fill(void* p, int64_t bytes, int value, hipStream_t s);
 void launch_stream_wait(const int* a, const int* b, int delta, int* err, hipStream_t s, double timeout_s = 60.0);
 // signal then wait in one launch (*sig += 1; wait *a >= *b + delta)
 void launch_stream_signal_wait(int* sig, const int* a, const int* b, int delta, int* err, hipStream_t s,

@@ -34,7 +34,8 @@ BucketReducer::BucketReducer(const std::vector<std::vector<int64_t>>& bucket_num
     k.outs.assign(k.numels.size(), nullptr);
     k.seen.assign(k.numels.size(), 0);
     hip_ok(hipMalloc(&k.buf, (size_t)(off > 0 ? off : 1) * sizeof(float)), "hipMalloc(bucket)");
-    hip_ok(hipMemset(k.buf, 0, (size_t)(off > 0 ? off : 1) * sizeof(float)), "hipMemset(bucket)");
+    launch_fill(k.buf, (int64_t)(off > 0 ? off : 1) * (int64_t)sizeof(float), 0, nullptr);
+    hip_ok(hipStreamSynchronize(nullptr), "fill(bucket)");
     hip_ok(hipEventCreateWithFlags(&k.ready, hipEventDisableTiming), "hipEventCreate");
     hip_ok(hipEventCreateWithFlags(&k.done, hipEventDisableTiming), "hipEventCreate");
   }
@@ -85,7 +86,7 @@ void BucketReducer::mark_ready(int b, int slot, const float* grad, float* grad_o
   k.seen[slot] = 1;
   float* view = k.buf + k.offs[slot];
   if (grad) launch_scale_copy(view, grad, k.numels[slot], 1.0f / (float)world_, stream);
-  else hip_ok(hipMemsetAsync(view, 0, k.numels[slot] * sizeof(float), stream), "hipMemsetAsync");
+  else launch_fill(view, (int64_t)k.numels[slot] * (int64_t)sizeof(float), 0, stream);
   hip_ok(hipGetLastError(), "scale_copy launch");
   k.outs[slot] = grad_out;
   if (--k.pending == 0) launch(b, stream);

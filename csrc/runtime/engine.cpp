@@ -55,7 +55,8 @@ void Engine::alloc_workspace() {
       compute_workspace_layout(max_batch_, max_test_batch_, conv_wgrad_groups(max_batch_), fc_bwd_splits(max_batch_));
   ws_bytes_ = L.total;
   HIP_OK(hipMalloc(&ws_, ws_bytes_));
-  HIP_OK(hipMemset(ws_, 0, ws_bytes_));   // padding rows of p etc. must be finite
+  launch_fill(ws_, ws_bytes_, 0, nullptr);   // padding rows of p etc. must be finite
+  HIP_OK(hipStreamSynchronize(nullptr));
   char* base = static_cast<char*>(ws_);
   a1_ = reinterpret_cast<uint16_t*>(base + L.a1);
   p_ = reinterpret_cast<uint16_t*>(base + L.p);
@@ -88,7 +89,8 @@ void Engine::alloc_workspace_f32() {
   const int64_t o_c2 = carve((int64_t)F32_MAX_SPLITS * C2 * (9 * C1 + 1) * 4);
   const int64_t o_c1 = carve((int64_t)F32_C1W_BLOCKS * C1 * 10 * 4);
   HIP_OK(hipMalloc(&ws32_, off));
-  HIP_OK(hipMemset(ws32_, 0, off));
+  launch_fill(ws32_, off, 0, nullptr);
+  HIP_OK(hipStreamSynchronize(nullptr));
   ws_bytes_ += off;
   char* b = static_cast<char*>(ws32_);
   F32Step& w = f32ws_;
@@ -157,7 +159,7 @@ void Engine::reset_counters() {
   // change or an aborted chunk they restart from zero, and so does the hand-off error flag [2]
   // (callers read it with check_errors before they get here)
   sync_streams();
-  HIP_OK(hipMemsetAsync(sync_ + 0, 0, 5 * sizeof(int), compute_));
+  launch_fill(sync_ + 0, 5 * sizeof(int), 0, compute_);
   HIP_OK(hipStreamSynchronize(compute_));
   reset_host_state();
 }
@@ -766,7 +768,7 @@ void Engine::broadcast_params(int root) {
 
 bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
   // scratch counters sync_[8..11]: [8] a, [9] b, [10] zero, [11] error
-  HIP_OK(hipMemsetAsync(sync_ + 8, 0, 4 * sizeof(int), x));
+  launch_fill(sync_ + 8, 4 * sizeof(int), 0, x);
   HIP_OK(hipStreamSynchronize(x));
   launch_stream_wait(sync_ + 8, sync_ + 10, 1, sync_ + 11, x, timeout_s);   // x waits ...
   launch_stream_signal(sync_ + 8, y);                                        // ... for y
@@ -784,7 +786,7 @@ bool Engine::probe_stream_handoff(double timeout_s) { return probe_stream_pair(c
 // fault injection (tests): the compute stream spins until fault_release (scratch counters
 // [12] released, [13] zero, [14] the hold's own timeout flag - never the engine's error flag [2])
 void Engine::fault_hold(double timeout_s) {
-  HIP_OK(hipMemsetAsync(sync_ + 12, 0, 4 * sizeof(int), compute_));
+  launch_fill(sync_ + 12, 4 * sizeof(int), 0, compute_);
   launch_stream_wait(sync_ + 12, sync_ + 13, 1, sync_ + 14, compute_, timeout_s);
   HIP_OK(hipGetLastError());
 }

@@ -89,9 +89,10 @@ XgmiComm::XgmiComm(int world, int rank, int device, int64_t numel, int channels,
   ok(hipMalloc(&ctr_, sizeof(int) * XGMI_MAX_WG * channels), "hipMalloc(ctr)");
   ok(hipMalloc(&err_, sizeof(int)), "hipMalloc(err)");
   ok(hipMalloc(&timeout_, sizeof(uint64_t)), "hipMalloc(timeout)");
-  ok(hipMemset(block_, 0, (size_t)L.sig_off), "hipMemset");
-  ok(hipMemset(ctr_, 0, sizeof(int) * XGMI_MAX_WG * channels), "hipMemset");
-  ok(hipMemset(err_, 0, sizeof(int)), "hipMemset");
+  launch_fill(block_, L.sig_off, 0, nullptr);
+  launch_fill(ctr_, (int64_t)sizeof(int) * XGMI_MAX_WG * channels, 0, nullptr);
+  launch_fill(err_, (int64_t)sizeof(int), 0, nullptr);
+  ok(hipGetLastError(), "fill");
   // signatures {magic, rank, pid, region id} that peers read back through their mapping after
   // connect() (a mapping that does not show them is refused)
   int32_t sig[4][4];
