@@ -13,6 +13,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-process / long-running CPU test")
 
 
+def pytest_collection_modifyitems(config, items):
+    # child-process-only GPU tests first, while the pytest process has not brought HIP up yet (the
+    # in-process tests' session fixture creates a context that then lives to the end)
+    items.sort(key=lambda it: 0 if "gpu_box" in getattr(it, "fixturenames", ()) else 1)
+
+
+@pytest.fixture(scope="session")
+def gpu_box():
+    """A GPU is usable, checked WITHOUT bringing HIP up in the pytest process: for tests whose GPU work
+    runs in child processes only (several ranks on one GPU - an idle context in the parent would hold
+    hardware queues of its own beside the ranks' spinning all-reduce kernels)."""
+    from pytorch_mnist_ddp_amd.driver import gpu_present
+    if not gpu_present():
+        pytest.skip("no GPU")
+    return True
+
+
 @pytest.fixture(scope="session")
 def cuda_device():
     import torch

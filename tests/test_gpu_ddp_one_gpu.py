@@ -27,7 +27,7 @@ def _env(**kw):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_ddp_matches_world1_large_batch(cuda_device, world):
+def test_ddp_matches_world1_large_batch(gpu_box, world):
     # W*B stays below FC1_BIG_MIN_B (512) so the world-1 run on the W*B batch uses the same forward
     # kernels as the shards: the forward is then row-wise bitwise identical and only the gradient
     # reductions differ in order (at W*B >= 512 fc1 switches to its 4-way split-K form, whose
@@ -43,7 +43,7 @@ def test_ddp_matches_world1_large_batch(cuda_device, world):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("W", [2, 8])
-def test_mnist_ddp_xgmi_without_rccl(cuda_device, tmp_path, W):
+def test_mnist_ddp_xgmi_without_rccl(gpu_box, tmp_path, W):
     n_train, B = 8000, 200 if W == 2 else 50       # 20 steps per rank per epoch either way
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
            "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
@@ -80,7 +80,7 @@ def test_mnist_ddp_xgmi_without_rccl(cuda_device, tmp_path, W):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("W,launcher", [(2, "torchrun"), (8, "self")])
-def test_bench_reports_correctness(cuda_device, tmp_path, W, launcher):
+def test_bench_reports_correctness(gpu_box, tmp_path, W, launcher):
     """``bench.py --gpus W`` under torchrun, and (W = 8) launching its W ranks itself with no launcher
     (the driver's plain command): ONE JSON line with n_gpus W, params in sync, the transport, its
     validation and the per-phase setup seconds."""
@@ -112,7 +112,7 @@ def test_bench_reports_correctness(cuda_device, tmp_path, W, launcher):
 
 
 @pytest.mark.timeout(200)
-def test_validation_fault_in_replayed_graph_is_named(cuda_device, tmp_path):
+def test_validation_fault_in_replayed_graph_is_named(gpu_box, tmp_path):
     """A rank held back while the startup validation REPLAYS the captured training graph: its peers'
     stage waits time out inside the graph, the collective verdict names the ranks, and with no RCCL
     communicator to fall back to (gloo + --allreduce xgmi) the run stops with that error instead of
@@ -132,7 +132,7 @@ def test_validation_fault_in_replayed_graph_is_named(cuda_device, tmp_path):
 
 
 @pytest.mark.timeout(200)
-def test_bench_startup_fault_reports_json(cuda_device, tmp_path):
+def test_bench_startup_fault_reports_json(gpu_box, tmp_path):
     """The same fault through ``bench.py --gpus 4`` (self-launched ranks): rank 0 still prints ONE
     JSON line - value null, the failing phase, the decoded error and every rank's failure record
     with its transport report and setup phases - and the exit code is non-zero."""
@@ -156,7 +156,7 @@ def test_bench_startup_fault_reports_json(cuda_device, tmp_path):
 
 
 @pytest.mark.timeout(200)
-def test_bench_nccl_process_group_stays_lazy_w4(cuda_device, tmp_path):
+def test_bench_nccl_process_group_stays_lazy_w4(gpu_box, tmp_path):
     """Production bootstrap on one GPU: the default ``nccl`` process group (lazy - no device_id) with
     the xGMI transport.  RCCL refuses two ranks on one GPU, so this passes only if nothing in the
     fused path issues a torch collective (ProcessGroupNCCL would build a communicator): shape check,
@@ -173,7 +173,7 @@ def test_bench_nccl_process_group_stays_lazy_w4(cuda_device, tmp_path):
 
 
 @pytest.mark.timeout(300)
-def test_mnist_ddp_stdout_contract_nccl_check_sync_w2(cuda_device, tmp_path):
+def test_mnist_ddp_stdout_contract_nccl_check_sync_w2(gpu_box, tmp_path):
     """``mnist_ddp.py`` at world 2 on the production ``nccl`` process group (lazy) with ``--check-sync``:
     rank 0's stdout holds only the reference's line kinds (init line, train lines, test
     lines, the timer - the transport line goes to stderr), and the per-epoch desync check runs over
@@ -198,7 +198,7 @@ def test_mnist_ddp_stdout_contract_nccl_check_sync_w2(cuda_device, tmp_path):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("W", [2, 8])
-def test_bench_fp32_xgmi_rehearsal(cuda_device, tmp_path, W):
+def test_bench_fp32_xgmi_rehearsal(gpu_box, tmp_path, W):
     """The fp32 step (the reference's precision) on the xGMI transport: ``bench.py --dtype fp32`` at
     W ranks on one GPU (gloo + --allreduce xgmi, no RCCL) trains with every rank's parameters bitwise
     equal, validated by replaying the captured fp32 chunk."""

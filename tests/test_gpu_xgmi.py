@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.timeout(260)
 @pytest.mark.parametrize("world,engine_steps,fault", [(2, 30, False), (3, 20, False), (4, 30, False), (8, 30, False),
                                                        (4, 0, True)])
-def test_xgmi_allreduce_multiprocess_one_gpu(cuda_device, world, engine_steps, fault):
+def test_xgmi_allreduce_multiprocess_one_gpu(gpu_box, world, engine_steps, fault):
     """With engine steps the FUSED schedule (the production default) runs with W ranks' spinning
     grids on one GPU: the residency planner must shrink them so all are resident.  W = 3 and 8
     execute those template instantiations of every xGMI kernel (8 = the headline config)."""
