@@ -366,6 +366,10 @@ PYBIND11_MODULE(_C, m) {
       .def("reset_counters", &Engine::reset_counters, py::call_guard<py::gil_scoped_release>())
       .def("probe_stream_handoff", &Engine::probe_stream_handoff, py::arg("timeout_s") = 2.0,
            py::call_guard<py::gil_scoped_release>())
+      .def("set_conv2_stream", [](Engine& e, uintptr_t stream, double timeout_s) {
+             return e.set_conv2_stream(S(stream), timeout_s);
+           }, py::arg("stream"), py::arg("timeout_s") = 2.0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("conv2_stream_on", &Engine::conv2_stream_on)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

@@ -25,26 +25,32 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_done2_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  for (SideLauncher& l : side_) HIP_OK(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
   alloc_workspace();
   if (f32_) alloc_workspace_f32();
 }
 
 Engine::~Engine() {
-  if (side_thread_.joinable()) {
-    {
-      std::lock_guard<std::mutex> lk(side_mu_);
-      side_stop_ = true;
+  for (SideLauncher& l : side_) {
+    if (l.thread.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(l.mu);
+        l.stop = true;
+      }
+      l.cv.notify_all();
+      l.thread.join();
     }
-    side_cv_.notify_all();
-    side_thread_.join();
+    if (l.join) hipEventDestroy(l.join);
   }
   for (auto g : side_graphs_)
     if (g) hipGraphExecDestroy(g);
+  for (auto g : c2_graphs_)
+    if (g) hipGraphExecDestroy(g);
   for (auto g : graphs_) hipGraphExecDestroy(g);
   for (auto g : graph_defs_) hipGraphDestroy(g);
-  for (hipEvent_t e : {ev_fc_, ev_done_, ev_fork_, ev_join_})
+  for (hipEvent_t e : {ev_fc_, ev_done_, ev_done2_, ev_fork_})
     if (e) hipEventDestroy(e);
   if (ws_) hipFree(ws_);
   if (ws32_) hipFree(ws32_);
@@ -229,9 +235,11 @@ void Engine::enqueue_step(int batch, bool last) {
   const int32_t* labels = pre ? buf_.epoch_labels : buf_.train_labels;
   TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
+  const bool c2s = use_conv2_stream();
   if (side && !side_forked_) {         // once per chunk: order the comm stream after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    if (c2s) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fc_, 0));
     side_forked_ = true;
   }
   // the previous step's fc update (comm stream) must be done before fc1_fwd reads w1: trunk_fwd
@@ -355,7 +363,8 @@ void Engine::enqueue_step(int batch, bool last) {
   // XGMI (fused kernels) runs the same chain: the fc all-reduce + update holds its completion, the
   // conv2 reduce + all-reduce + update signals [1] at its start (world-1 timeline: two hand-off launches
   // a step fewer, conv2's part no longer queued behind them)
-  const bool chain = !trace_ && (!xg || xgmi_fuse_update_);
+  // With a conv2 stream (OVERLAP) conv2's part leaves the comm stream: no chain, plain waits / signals
+  const bool chain = !trace_ && (!xg || xgmi_fuse_update_) && !c2s;
   phase_begin("allreduce_fc+update");
   if (S) {
     if (chain && comm_sig3_pending_)
@@ -418,8 +427,10 @@ void Engine::enqueue_step(int batch, bool last) {
     u2.state_inc = nullptr;
     u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
     cb.w2d = w2d_cur;
-    if (S) {
-      if (!chain) launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+    // conv stream: the comm stream after the fc update, or (c2s) the conv2 stream beside it
+    hipStream_t s2 = c2s ? conv2_stream_ : comm_stream_;
+    if (c2s ? enq_c2_ : S) {
+      if (!chain) launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, s2);
       if (chain) u2.signal_start = sync_ + 1;     // the fc update (previous launch) is done
       if (xg) {
         XgmiConvPart p2;
@@ -427,12 +438,12 @@ void Engine::enqueue_step(int batch, bool last) {
         p2.hi = RED_W2_PARTS;
         xgmi_->conv_reduce_fused(XGMI_CH_CONV2, cb, B, comm_stream_, u2, p2);
       } else {
-        launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, comm_stream_);
+        launch_adadelta_reduce_parts(u2, cb, B, 0, RED_W2_PARTS, s2);
       }
       if (chain && !last)
         comm_sig3_pending_ = true;                // signalled by the next step's first comm launch
       else
-        launch_stream_signal(sync_ + 3, comm_stream_);
+        launch_stream_signal(sync_ + 3, s2);
     }
     ConvBwdArgs cbd = cb;
     cbd.signal_ctr = sync_ + 4;
@@ -468,6 +479,10 @@ void Engine::enqueue_step(int batch, bool last) {
     if (M && !skip_join_) {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
+      if (c2s) {
+        HIP_OK(hipEventRecord(ev_done2_, conv2_stream_));
+        HIP_OK(hipStreamWaitEvent(compute_, ev_done2_, 0));
+      }
     }
     side_pending_ = false;
     side_forked_ = false;
@@ -585,12 +600,13 @@ int Engine::capture_train(int n, int batch, int stride) {
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   side_graphs_.push_back(nullptr);
+  c2_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
 }
 
 void Engine::reset_host_state() {
   comm_sig3_pending_ = false;
-  enq_main_ = enq_side_ = true;
+  enq_main_ = enq_side_ = enq_c2_ = true;
   skip_join_ = false;
   side_pending_ = false;
   side_forked_ = false;
@@ -608,64 +624,92 @@ void Engine::reset_host_state() {
 // (comm stream -> compute) become two events at replay.
 int Engine::capture_train_split(int n, int batch) {
   const bool sp = side_pending_, w2 = w2d_in_alt_;
-  hipGraph_t gs = nullptr, gm = nullptr;
-  auto pass = [&](hipStream_t s, bool m, bool side, hipGraph_t* out) {
+  const bool c2s = use_conv2_stream();        // a third pass: the conv2 stream's chain
+  hipGraph_t gs = nullptr, gm = nullptr, g2 = nullptr;
+  auto pass = [&](hipStream_t s, bool m, bool side, bool c2, hipGraph_t* out) {
     side_pending_ = sp;
     w2d_in_alt_ = w2;
     comm_sig3_pending_ = false;
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;
     enq_side_ = side;
+    enq_c2_ = c2;
     skip_join_ = true;
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
     HIP_OK(hipStreamEndCapture(s, out));
   };
   try {
-    pass(comm_stream_, false, true, &gs);
-    pass(compute_, true, false, &gm);
-    enq_main_ = enq_side_ = true;
+    pass(comm_stream_, false, true, false, &gs);
+    if (c2s) pass(conv2_stream_, false, false, true, &g2);
+    pass(compute_, true, false, false, &gm);
+    enq_main_ = enq_side_ = enq_c2_ = true;
     skip_join_ = false;
   } catch (...) {
     reset_host_state();
     hipStreamCaptureStatus st;
-    for (hipStream_t s : {comm_stream_, compute_}) {
+    for (hipStream_t s : {comm_stream_, conv2_stream_, compute_}) {
       hipGraph_t junk = nullptr;
-      if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive) hipStreamEndCapture(s, &junk);
+      if (s && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
+        hipStreamEndCapture(s, &junk);
       if (junk) hipGraphDestroy(junk);
     }
-    for (hipGraph_t g : {gs, gm})
+    for (hipGraph_t g : {gs, gm, g2})
       if (g) hipGraphDestroy(g);
     throw;
   }
-  hipGraphExec_t xs = nullptr, xm = nullptr;
+  hipGraphExec_t xs = nullptr, xm = nullptr, x2 = nullptr;
   HIP_OK(hipGraphInstantiate(&xs, gs, nullptr, nullptr, 0));
   HIP_OK(hipGraphInstantiate(&xm, gm, nullptr, nullptr, 0));
+  if (g2) HIP_OK(hipGraphInstantiate(&x2, g2, nullptr, nullptr, 0));
   graph_defs_.push_back(gs);
   graph_defs_.push_back(gm);
+  if (g2) graph_defs_.push_back(g2);
   graphs_.push_back(xm);
   side_graphs_.push_back(xs);
+  c2_graphs_.push_back(x2);
   return (int)graphs_.size() - 1;
 }
 
 // --- side-graph launcher thread: hipGraphLaunch(side, comm stream) + the join event, concurrently
 // with the compute graph's launch on the calling thread (measured 20-step window, single GPU: 75.8
 // vs 78.9 us/step launching both from the calling thread)
-void Engine::side_worker() {
-  std::unique_lock<std::mutex> lk(side_mu_);
+void Engine::side_worker(int k) {
+  SideLauncher& l = side_[k];
+  std::unique_lock<std::mutex> lk(l.mu);
   for (;;) {
-    side_cv_.wait(lk, [this] { return side_stop_ || side_job_ != nullptr; });
-    if (side_stop_) return;
-    hipGraphExec_t job = side_job_;
+    l.cv.wait(lk, [&l] { return l.stop || l.job != nullptr; });
+    if (l.stop) return;
+    hipGraphExec_t job = l.job;
+    hipStream_t s = l.stream;
     lk.unlock();
-    hipError_t e = hipGraphLaunch(job, comm_stream_);
-    if (e == hipSuccess) e = hipEventRecord(ev_join_, comm_stream_);
+    hipError_t e = hipGraphLaunch(job, s);
+    if (e == hipSuccess) e = hipEventRecord(l.join, s);
     lk.lock();
-    side_err_ = e;
-    side_job_ = nullptr;
-    side_done_ = true;
-    side_cv_.notify_all();
+    l.err = e;
+    l.job = nullptr;
+    l.done = true;
+    l.cv.notify_all();
   }
+}
+
+void Engine::side_start(int k, hipGraphExec_t g, hipStream_t s) {
+  SideLauncher& l = side_[k];
+  {
+    std::lock_guard<std::mutex> lk(l.mu);
+    if (!l.thread.joinable()) l.thread = std::thread(&Engine::side_worker, this, k);
+    l.job = g;
+    l.stream = s;
+    l.done = false;
+  }
+  l.cv.notify_all();
+}
+
+hipError_t Engine::side_wait(int k) {
+  SideLauncher& l = side_[k];
+  std::unique_lock<std::mutex> lk(l.mu);
+  l.cv.wait(lk, [&l] { return l.done; });
+  return l.err;
 }
 
 void Engine::gather_rows(int64_t start, int64_t n) {
@@ -682,25 +726,21 @@ void Engine::replay(int id) {
     HIP_OK(hipGraphLaunch(graphs_[id], compute_));
     return;
   }
-  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chain ordered after earlier compute work
+  hipGraphExec_t c2 = c2_graphs_[id];
+  if (c2 && !conv2_stream_) throw std::runtime_error("replay: graph captured with the conv2 stream, now unset");
+  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chains ordered after earlier compute work
   HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
-  {
-    std::lock_guard<std::mutex> lk(side_mu_);
-    if (!side_thread_.joinable()) side_thread_ = std::thread(&Engine::side_worker, this);
-    side_job_ = side;
-    side_done_ = false;
-  }
-  side_cv_.notify_all();
+  if (c2) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fork_, 0));
+  side_start(0, side, comm_stream_);
+  if (c2) side_start(1, c2, conv2_stream_);
   const hipError_t em = hipGraphLaunch(graphs_[id], compute_);
-  hipError_t es;
-  {
-    std::unique_lock<std::mutex> lk(side_mu_);
-    side_cv_.wait(lk, [this] { return side_done_; });
-    es = side_err_;
-  }
+  const hipError_t es = side_wait(0);
+  const hipError_t e2 = c2 ? side_wait(1) : hipSuccess;
   HIP_OK(em);
   HIP_OK(es);
-  HIP_OK(hipStreamWaitEvent(compute_, ev_join_, 0));   // chunk end: compute joins the side chain
+  HIP_OK(e2);
+  HIP_OK(hipStreamWaitEvent(compute_, side_[0].join, 0));   // chunk end: compute joins the side chains
+  if (c2) HIP_OK(hipStreamWaitEvent(compute_, side_[1].join, 0));
 }
 
 void Engine::enqueue_eval(int n_total, int batch) {
@@ -750,6 +790,7 @@ int Engine::capture_eval(int n_total, int batch) {
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   side_graphs_.push_back(nullptr);
+  c2_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
 }
 
@@ -782,6 +823,15 @@ bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
 }
 
 bool Engine::probe_stream_handoff(double timeout_s) { return probe_stream_pair(compute_, comm_stream_, timeout_s); }
+
+bool Engine::set_conv2_stream(hipStream_t s, double timeout_s) {
+  sync_streams();
+  // graphs captured for the other stream layout stay valid only in their own (replay refuses a
+  // conv2-stream graph once the stream is unset; graphs captured without it run the 2-stream chain)
+  const bool ok = s && probe_stream_pair(compute_, s, timeout_s) && probe_stream_pair(comm_stream_, s, timeout_s);
+  conv2_stream_ = ok ? s : nullptr;
+  return ok;
+}
 
 // fault injection (tests): the compute stream spins until fault_release (scratch counters
 // [12] released, [13] zero, [14] the hold's own timeout flag - never the engine's error flag [2])
@@ -821,6 +871,7 @@ void Engine::check_errors() const {
 void Engine::sync_streams() {
   HIP_OK(hipStreamSynchronize(compute_));
   HIP_OK(hipStreamSynchronize(comm_stream_));
+  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
 }
 
 void Engine::synchronize() {

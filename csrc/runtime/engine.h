@@ -106,6 +106,12 @@ class Engine {
   // until fault_release, launched on another stream, lets it go
   void fault_hold(double timeout_s);
   void fault_release(hipStream_t s);
+  // OVERLAP (single GPU): conv2's slab reduce + update on a third stream, released by dgrad's start
+  // and running beside the fc update instead of queued behind it.  Probes `s` against both streams
+  // (three distinct hardware queues needed) and keeps it only if both hand-offs complete; nullptr =
+  // off (conv2's part back on the comm stream, after the fc update).  Call while idle.
+  bool set_conv2_stream(hipStream_t s, double timeout_s);
+  bool conv2_stream_on() const { return conv2_stream_ != nullptr; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -145,10 +151,11 @@ class Engine {
   void enqueue_step_f32(int batch, bool last);
   F32Step f32_args() const;
   bool side_schedule() const { return sched_ == OVERLAP || (sched_ == XGMI && !f32_); }
+  bool use_conv2_stream() const { return conv2_stream_ && sched_ == OVERLAP && !f32_ && !trace_; }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
   void reset_host_state();
-  void side_worker();
+  void side_worker(int k);
   void enqueue_eval(int n_total, int batch);
   void alloc_workspace();
   void alloc_workspace_f32();
@@ -172,23 +179,35 @@ class Engine {
   int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
                                     // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch,
                                     // [12..15] fault-injection hold
-  bool enq_main_ = true, enq_side_ = true;   // split capture: which stream's pass enqueue_step feeds
+  hipStream_t conv2_stream_ = nullptr;       // set_conv2_stream
+  // split capture: which stream's pass enqueue_step feeds (main = compute, side = comm, c2 = conv2)
+  bool enq_main_ = true, enq_side_ = true, enq_c2_ = true;
   bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
   std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
-  std::thread side_thread_;                   // launches side graphs concurrently with the compute graph
-  std::mutex side_mu_;
-  std::condition_variable side_cv_;
-  hipGraphExec_t side_job_ = nullptr;
-  bool side_done_ = false, side_stop_ = false;
-  hipError_t side_err_ = hipSuccess;
+  std::vector<hipGraphExec_t> c2_graphs_;     // per graph id: its conv2-stream graph or null
+  hipEvent_t ev_fork_ = nullptr;
+  // side-graph launchers: [0] the comm stream's graph, [1] the conv2 stream's, each on its own host
+  // thread, concurrently with the compute graph's launch on the calling thread
+  struct SideLauncher {
+    std::thread thread;
+    std::mutex mu;
+    std::condition_variable cv;
+    hipGraphExec_t job = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t join = nullptr;                // recorded on `stream` after the graph (chunk-end join)
+    bool done = false, stop = false;
+    hipError_t err = hipSuccess;
+  };
+  SideLauncher side_[2];
+  void side_start(int k, hipGraphExec_t g, hipStream_t s);
+  hipError_t side_wait(int k);
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
   void phase_begin(const char* name);
   void phase_end();
   float* c1red_ = nullptr;          // conv1 partial group sums (large batches)
   uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv2 update on the comm stream)
   bool w2d_in_alt_ = false;         // enqueue-time: the current w2d lives in w2d_alt_
-  hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr;
+  hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr, ev_done2_ = nullptr;
   // workspace
   int64_t ws_bytes_ = 0;
   void* ws_ = nullptr;

@@ -250,6 +250,20 @@ class FusedTrainer:
         # conv2's part moved too); SERIAL when the streams share a hardware queue
         self.overlap = bool(overlap) and self._probe_streams()
         self.engine.set_schedule(C.SCHED_OVERLAP if self.overlap else C.SCHED_SERIAL)
+        # opt-in (MNIST_AMD_CONV2_STREAM=1): conv2's slab reduce + update on a third stream, beside the
+        # fc update from dgrad's start on, if it gets its own hardware queue.  Measured slower (600
+        # steps 64.5-64.8 -> 66.0-67.9 us/step for fc-update grids 144-577: dgrad 14.4 -> 17.5 us with
+        # two co-runners; profiles/r5/ab/conv2_stream.txt), so off by default
+        self.conv2_stream = None
+        # (a hand-off completes in microseconds: a short probe, skipped outright with fewer than 4
+        # hardware queues per process, where the third stream would share one)
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        if (self.overlap and not self.fp32 and queues >= 4
+                and os.environ.get("MNIST_AMD_CONV2_STREAM", "0") == "1"):
+            with self.setup.phase("stream_probe"):
+                s = torch.cuda.Stream(device=self.device)
+                if self.engine.set_conv2_stream(int(s.cuda_stream), 1.0):
+                    self.conv2_stream = s
 
     def _use_graph_set(self, name: str) -> None:
         self._graphs = self._graph_sets.setdefault(name, {})
