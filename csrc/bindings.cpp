@@ -119,6 +119,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.attr("PARAM_TOTAL") = PARAM_TOTAL;
   m.attr("FC1_KSPLIT") = FC1_KSPLIT;
+  m.attr("DYC_REC") = DYC_REC;
   py::dict offs;
   offs["fc1.weight"] = OFF_FC1_W; offs["fc1.bias"] = OFF_FC1_B;
   offs["fc2.weight"] = OFF_FC2_W; offs["fc2.bias"] = OFF_FC2_B;

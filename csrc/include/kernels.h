@@ -68,10 +68,13 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s);
 
 // ---------------- backward ----------------
 // Compact gradient wrt the conv2 output (the max-pool backward input): one record per (image,
-// pooled position) = 64 bf16 pooled gradients (already dropout-scaled, ReLU-masked) followed by
-// 64 argmax codes (2x2 window position, 0..3).  Dense dy[y][x][c] = (code == 2(y&1)+(x&1)) ? g : 0.
-constexpr int DYC_REC = 192, DYC_ROUTE = 128;
-constexpr int64_t DYC_BYTES_PER_IMAGE = (int64_t)NPOOL * DYC_REC;   // 27648
+// pooled position) = 64 bf16 pooled gradients (already dropout-scaled, ReLU-masked) followed by the
+// 64 argmax codes (2x2 window position, 0..3) as bit planes: per 8-channel chunk c8 two bytes at
+// DYC_ROUTE + 2 c8, bit i of the first = bit 0 of channel 8 c8 + i's code, of the second = bit 1
+// (16 B of codes instead of 64: 144-B records, 25 % fewer record bytes written by fc_bwd and read by
+// the conv backward).  Dense dy[y][x][c] = (code == 2(y&1)+(x&1)) ? g : 0.
+constexpr int DYC_REC = 144, DYC_ROUTE = 128;
+constexpr int64_t DYC_BYTES_PER_IMAGE = (int64_t)NPOOL * DYC_REC;   // 20736
 
 struct FcBwdArgs {
   const uint16_t* dz1;        // bf16 [Bp][128]

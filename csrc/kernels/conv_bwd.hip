@@ -89,62 +89,32 @@ __device__ __forceinline__ int swz_dy(int pix) { return (pix ^ (pix >> 1)) & 7; 
 
 // Expand one 16-B chunk of the compact un-pooled gradient (8 channels of one pooled position) to
 // the dense chunk of window pixel q (0..3): channel j keeps its value iff its argmax code == q.
-__device__ __forceinline__ uint4 dyc_expand(uint4 g, uint2 route, int q) {
-  // per route word (4 channels): 0xFF in the bytes whose code == q (SWAR zero-byte test), then
-  // v_perm_b32 doubles each byte into the 16-bit lane of its bf16
-  const uint32_t rep = (uint32_t)q * 0x01010101u;
-  uint32_t keep[2];
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const uint32_t x = (w ? route.y : route.x) ^ rep;                        // 0 byte <=> match
-    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 <=> no match
-    keep[w] = ~((nz >> 7) * 0xFFu);                                            // 0xFF <=> match
-  }
+// The chunk's codes arrive as two bit planes r16 (bit j = code bit 0 of channel j, bit 8 + j = code
+// bit 1; kernels.h DYC_ROUTE).  v_perm_b32's sign selectors (8 / 9 = 0xFF iff bit 15 / 31 of src1
+// is set) expand a match flag straight into a 16-bit lane mask, so for output word k (channels 2k,
+// 2k + 1) the flags only need to sit at bits 15 / 31: rr = r16 | (r16 >> 1) << 16 puts channel
+// 2k + 1's bit 0 at 16 + 2k next to channel 2k's at 2k, and its bit 1 at 24 + 2k next to channel
+// 2k's at 8 + 2k; rr << (15 - 2k) and rr << (7 - 2k) bring them to 15 / 31 (tests/test_dyc_expand_cpu.py).
+__device__ __forceinline__ uint32_t dyc_rr(uint32_t r16) { return r16 | ((r16 >> 1) << 16); }
+__device__ __forceinline__ uint4 dyc_expand_flags(uint4 g, uint32_t bx, uint32_t by) {
+  // bx / by: rr or ~rr (code bit 0 / 1 == the pixel's); a match needs both at bits 15 / 31
   uint4 o;
-  o.x = g.x & __builtin_amdgcn_perm(0u, keep[0], 0x01010000u);
-  o.y = g.y & __builtin_amdgcn_perm(0u, keep[0], 0x03030202u);
-  o.z = g.z & __builtin_amdgcn_perm(0u, keep[1], 0x01010000u);
-  o.w = g.w & __builtin_amdgcn_perm(0u, keep[1], 0x03030202u);
+  o.x = g.x & __builtin_amdgcn_perm(0u, (bx << 15) & (by << 7), 0x09090808u);
+  o.y = g.y & __builtin_amdgcn_perm(0u, (bx << 13) & (by << 5), 0x09090808u);
+  o.z = g.z & __builtin_amdgcn_perm(0u, (bx << 11) & (by << 3), 0x09090808u);
+  o.w = g.w & __builtin_amdgcn_perm(0u, (bx << 9) & (by << 1), 0x09090808u);
   return o;
 }
-// dyc_expand with the window code pre-multiplied (rep = q * 0x01010101; q = 4 selects nothing)
-__device__ __forceinline__ uint4 dyc_expand_rep(uint4 g, uint2 route, uint32_t rep) {
-  uint32_t keep[2];
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const uint32_t x = (w ? route.y : route.x) ^ rep;                        // 0 byte <=> match
-    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 <=> no match
-    keep[w] = ~((nz >> 7) * 0xFFu);                                            // 0xFF <=> match
-  }
-  uint4 o;
-  o.x = g.x & __builtin_amdgcn_perm(0u, keep[0], 0x01010000u);
-  o.y = g.y & __builtin_amdgcn_perm(0u, keep[0], 0x03030202u);
-  o.z = g.z & __builtin_amdgcn_perm(0u, keep[1], 0x01010000u);
-  o.w = g.w & __builtin_amdgcn_perm(0u, keep[1], 0x03030202u);
-  return o;
+// one pixel q (0..3), or nothing (q = 4: the lean wgrad zeroes rows past a chunk this way)
+__device__ __forceinline__ uint4 dyc_expand(uint4 g, uint32_t r16, int q) {
+  const uint32_t rr = dyc_rr(r16);
+  const uint32_t none = q < 4 ? ~0u : 0u;
+  return dyc_expand_flags(g, ((q & 1) ? rr : ~rr) & none, (q & 2) ? rr : ~rr);
 }
-// dyc_expand for all four window pixels of one chunk, sharing the route decoding: v_perm_b32's
-// sign selectors (8..11 = 0xFF if bit 15 / 31 / 47 / 63 of {src0, src1} is set) expand a match flag
-// straight into a 16-bit lane mask, so per route word the four flags only need to sit at bits 15 / 31
-// of two words: channels 0 / 2 of the word from (route << 15, route << 14) (the code's bit 0 / bit 1),
-// channels 1 / 3 from (route << 7, route << 6).  Per pixel 2 x (2 bit-ops + 2 perms + 2 ands)
-// instead of ~24 VALU; the same bits as dyc_expand (routes are 0..3).
-struct DycRoute {
-  uint32_t e0x, e1x, o0x, o1x, e0y, e1y, o0y, o1y;
-};
-__device__ __forceinline__ DycRoute dyc_route(uint2 r) {
-  return DycRoute{r.x << 15, r.x << 14, r.x << 7, r.x << 6, r.y << 15, r.y << 14, r.y << 7, r.y << 6};
-}
+// all four window pixels of one chunk share rr (conv2_dgrad's staging by pooled record)
 template <int Q>
-__device__ __forceinline__ uint32_t dyc_flag(uint32_t b0, uint32_t b1) {
-  return ((Q & 1) ? b0 : ~b0) & ((Q & 2) ? b1 : ~b1);
-}
-template <int Q>
-__device__ __forceinline__ uint4 dyc_expand_q(uint4 g, const DycRoute& R) {
-  const uint32_t mex = dyc_flag<Q>(R.e0x, R.e1x), mox = dyc_flag<Q>(R.o0x, R.o1x);
-  const uint32_t mey = dyc_flag<Q>(R.e0y, R.e1y), moy = dyc_flag<Q>(R.o0y, R.o1y);
-  return uint4{g.x & __builtin_amdgcn_perm(mex, mox, 0x08080A0Au), g.y & __builtin_amdgcn_perm(mex, mox, 0x09090B0Bu),
-               g.z & __builtin_amdgcn_perm(mey, moy, 0x08080A0Au), g.w & __builtin_amdgcn_perm(mey, moy, 0x09090B0Bu)};
+__device__ __forceinline__ uint4 dyc_expand_q(uint4 g, uint32_t rr) {
+  return dyc_expand_flags(g, (Q & 1) ? rr : ~rr, (Q & 2) ? rr : ~rr);
 }
 __device__ __forceinline__ const uint8_t* dyc_record(const uint8_t* dyc, int b, int y, int x) {
   return dyc + (int64_t)b * DYC_BYTES_PER_IMAGE + ((y >> 1) * HP + (x >> 1)) * DYC_REC;
@@ -175,7 +145,7 @@ enum DgX { DGX_PRE = 0, DGX_IDX = 1, DGX_XIN = 2 };
 constexpr int DG_JOBS = 5 * HP * 8;                // 480
 struct DgLoad {
   uint4 v[2];
-  uint2 rt[2];
+  uint32_t rt[2];                                 // the chunk's code planes (r16)
   uint32_t okm;                                   // bit j: job j's pooled row is inside the image
   float xv;                                       // fp32 module input, or the raw pixel byte
 };
@@ -195,7 +165,7 @@ __device__ __forceinline__ void dgrad_fetch(const ConvBwdArgs& a, int strip, int
     L.okm |= (ok ? 1u : 0u) << k;
     const uint8_t* rec = a.dyc + (int64_t)b * DYC_BYTES_PER_IMAGE + ((ok ? py : 0) * HP + pc) * DYC_REC;
     L.v[k] = *reinterpret_cast<const uint4*>(rec + c8 * 16);
-    L.rt[k] = *reinterpret_cast<const uint2*>(rec + DYC_ROUTE + c8 * 8);
+    L.rt[k] = *reinterpret_cast<const uint16_t*>(rec + DYC_ROUTE + c8 * 2);
   }
   const int e = tid < DG_TROWS * IMG ? tid : 0;   // DG_TROWS * IMG = 252 <= 256
   const bool okx = tid < DG_TROWS * IMG && r0 + e / IMG < IMG;
@@ -235,14 +205,14 @@ __device__ __forceinline__ void dgrad_dy_store(unsigned char* smem, int strip, i
       const int c8 = jb & 7, pc = (jb >> 3) % HP, pr = (jb >> 3) / HP;
       const int ly0 = 2 * (py0 + pr) - (r0 - 2);  // tile row of the window's top pixel row (-1..9)
       const bool ok = (L.okm >> k) & 1u;
-      const DycRoute R = dyc_route(L.rt[k]);
+      const uint32_t rr = dyc_rr(L.rt[k]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int ly = ly0 + (q >> 1);
         if (ly >= 0 && ly < DG_TROWS) {
           const int row = ly * DG_PITCH + 2 * pc + (q & 1) + 2;
-          uint4 e = q == 0 ? dyc_expand_q<0>(L.v[k], R) : q == 1 ? dyc_expand_q<1>(L.v[k], R)
-                  : q == 2 ? dyc_expand_q<2>(L.v[k], R) : dyc_expand_q<3>(L.v[k], R);
+          uint4 e = q == 0 ? dyc_expand_q<0>(L.v[k], rr) : q == 1 ? dyc_expand_q<1>(L.v[k], rr)
+                  : q == 2 ? dyc_expand_q<2>(L.v[k], rr) : dyc_expand_q<3>(L.v[k], rr);
           const uint32_t okm = ok ? ~0u : 0u;           // per component (a select of the uint4 went
           e.x &= okm; e.y &= okm; e.z &= okm; e.w &= okm;   // through scratch memory)
           dys[row * 8 + (c8 ^ swz8(row))] = e;
@@ -547,7 +517,7 @@ template <int NTH>
 struct WlChunkT {
   static constexpr int VD = WDY_BYTES / 16 / NTH, VA = (WA1_BYTES / 16 + NTH - 1) / NTH;
   uint4 vd[VD], va[VA];
-  uint2 rt[VD];
+  uint32_t rt[VD];                                 // code planes (r16) of each dy chunk
 };
 // chunk-invariant staging plan of thread tid (dense dy chunk c = tid + NTH i: pixel c >> 3, channels
 // 8(c & 7)..; every chunk of the workgroup starts on a row of the parity of r0 (chunks are 8 rows),
@@ -580,7 +550,7 @@ __device__ __forceinline__ void wl_fetch(const ConvBwdArgs& a, const WlPlanT<NTH
     const int y = nx ? t - H2 : t;
     const int off = (nx ? (int)DYC_BYTES_PER_IMAGE : 0) + (y >> 1) * (HP * DYC_REC) + (P.rec[i] & 0xFFF);
     k.vd[i] = *reinterpret_cast<const uint4*>(recb + off);
-    k.rt[i] = *reinterpret_cast<const uint2*>(recb + off + DYC_ROUTE - c8 * 8);
+    k.rt[i] = *reinterpret_cast<const uint16_t*>(recb + off + DYC_ROUTE - c8 * 14);   // + 128 + 2 c8 - 16 c8
   }
   const int A0 = a1_row_of(c0), A1 = a1_row_of(c1 - 1) + 3;
   const int na1 = (A1 - A0) * H1 * 4;
@@ -595,9 +565,8 @@ __device__ __forceinline__ void wl_store(const WlPlanT<NTH>& P, unsigned char* b
   uint4* a1s = reinterpret_cast<uint4*>(buf + WDY_BYTES);
 #pragma unroll
   for (int i = 0; i < WlChunkT<NTH>::VD; ++i) {
-    const uint32_t code = (P.rec[i] >> 16) < c1 - c0 ? ((uint32_t)P.rec[i] >> 12) & 3u : 4u;   // 4: no route matches -> 0
-    const uint32_t rp = code * 0x01010101u;
-    dys[P.dst0 + NTH * i] = dyc_expand_rep(k.vd[i], k.rt[i], rp);
+    const int code = (P.rec[i] >> 16) < c1 - c0 ? (P.rec[i] >> 12) & 3 : 4;   // 4: no route matches -> 0
+    dys[P.dst0 + NTH * i] = dyc_expand(k.vd[i], k.rt[i], code);
   }
 #pragma unroll
   for (int i = 0; i < WlChunkT<NTH>::VA; ++i) {

@@ -623,15 +623,23 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
         const float v = ((mk & 12) == 12) ? acc[nt][r] * dscale : 0.0f;   // kept by dropout, ReLU alive
         unsigned char* rec = recs + (bl * 4 + wave) * DYC_REC;
         reinterpret_cast<uint16_t*>(rec)[c] = f2bf(v);
-        rec[DYC_ROUTE + c] = (uint8_t)(mk & 3);
+        // argmax code bit planes: ballot bit 16 kg + m = channel 16 nt + m of row 4 kg + r, so the
+        // 16-bit slice kg of each ballot is this row's planes of chunks 2 nt (low byte), 2 nt + 1
+        const uint64_t p0 = __ballot(mk & 1), p1 = __ballot(mk & 2);
+        if (m == 0) {
+          const uint32_t w0 = (uint32_t)(p0 >> (16 * kg)), w1 = (uint32_t)(p1 >> (16 * kg));
+          // bytes [plane 0, plane 1] of chunk 2 nt, then of chunk 2 nt + 1
+          reinterpret_cast<uint32_t*>(rec + DYC_ROUTE)[nt] = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+        }
       }
     lds_barrier();
-    // 16 runs of 4 contiguous records (768 B) -> 48 x 16 B per image row, 3 per thread
+    // 16 runs of 4 contiguous records (576 B) -> 36 x 16 B per image row
     constexpr int RUN16 = 4 * DYC_REC / 16;
+    static_assert(RUN16 * 16 <= 3 * 256, "three 16-B chunks per thread");
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int cidx = tid + 256 * k, bl = cidx / RUN16, off = cidx - bl * RUN16;
-      if (b0 + bl < B)        // write-through: the conv backward kernels read the records
+      if (cidx < RUN16 * 16 && b0 + bl < B)   // write-through: the conv backward kernels read the records
         store16(B <= WT_MAX_B, a.dyc, ((int64_t)(b0 + bl) * NPOOL + s0) * DYC_REC + off * 16,
                    reinterpret_cast<const uint4*>(recs)[cidx]);
     }

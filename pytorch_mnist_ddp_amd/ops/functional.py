@@ -14,6 +14,7 @@ import torch
 from . import native
 
 NFLAT, NH, NCLS = 9216, 128, 10
+DYC_REC = 144                       # compact dy record bytes (csrc/include/kernels.h DYC_REC)
 
 
 def _C():
@@ -39,7 +40,7 @@ class StepBuffers:
     dz1: torch.Tensor         # bf16 [Bp64, 128]
     h_bf: torch.Tensor        # bf16 [Bp64, 128]
     dl_bf: torch.Tensor       # bf16 [Bp64, 16]
-    dyc: torch.Tensor         # uint8 [B, 144*192] compact grad wrt conv2 output (pooled grads + argmax)
+    dyc: torch.Tensor         # uint8 [B, 144*144] compact grad wrt conv2 output (pooled grads + argmax planes)
     fcpart: torch.Tensor      # f32 fc-gradient split partials (B > 1024), else a 1-element placeholder
     c1part: torch.Tensor      # f32 [4B, 320]
     w2part: torch.Tensor      # f32 [G, 18496]
@@ -63,7 +64,7 @@ class StepBuffers:
             dz1=torch.zeros(Bp, NH, **bf),
             h_bf=torch.zeros(Bp, NH, **bf),
             dl_bf=torch.zeros(Bp, 16, **bf),
-            dyc=torch.zeros(B, 144 * 192, dtype=torch.uint8, device=device),
+            dyc=torch.zeros(B, 144 * DYC_REC, dtype=torch.uint8, device=device),
             fcpart=torch.zeros(max(1, (C.fc_bwd_splits(B) > 1) * C.fc_bwd_splits(B) * C.FCB_PART_STRIDE),
                                dtype=torch.float32, device=device),
             c1part=torch.zeros(4 * B, 320, dtype=torch.float32, **z),
@@ -150,13 +151,21 @@ def eval_forward(ms, data_u8, labels, idx, buf: StepBuffers) -> None:
     head_eval(ms, labels, idx, buf)
 
 
+def route_codes(planes: torch.Tensor) -> torch.Tensor:
+    """[..., 16] uint8 code bit planes of a record (byte 2 c8 + p: bit j = bit p of channel 8 c8 + j's
+    argmax code) -> [..., 64] int64 codes 0..3."""
+    pl = planes.long().view(*planes.shape[:-1], 8, 2)              # [..., chunk, plane]
+    bits = (pl.unsqueeze(-1) >> torch.arange(8, device=planes.device)) & 1   # [..., chunk, plane, j]
+    return (bits[..., 0, :] | (bits[..., 1, :] << 1)).reshape(*planes.shape[:-1], 64)
+
+
 def dense_dy(buf: StepBuffers) -> torch.Tensor:
     """Expand the compact un-pooled gradient records to the dense NHWC bf16 [B,24,24,64] map
     (what the conv backward kernels stage in LDS); for tests and tools."""
     B = buf.B
-    rec = buf.dyc.view(B, 12, 12, 192)
+    rec = buf.dyc.view(B, 12, 12, DYC_REC)
     g = rec[..., :128].contiguous().view(torch.bfloat16).view(B, 12, 12, 64)
-    code = rec[..., 128:].long()                                    # [B,12,12,64] window position
+    code = route_codes(rec[..., 128:])                              # [B,12,12,64] window position
     dense = torch.zeros(B, 12, 2, 12, 2, 64, dtype=torch.bfloat16, device=g.device)
     for q in range(4):
         sel = (code == q)

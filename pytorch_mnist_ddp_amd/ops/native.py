@@ -23,6 +23,9 @@ def load(build_if_missing: bool = True):
     if os.environ.get("MNIST_AMD_TIMELINE") == "1":
         _C = _load_timeline_variant(build_if_missing)
         return _C
+    if os.environ.get("MNIST_AMD_EXT_PATH"):      # A/B runs: another build of the same sources
+        _C = _load_from(os.environ["MNIST_AMD_EXT_PATH"])
+        return _C
     try:
         _C = importlib.import_module("pytorch_mnist_ddp_amd._C")
         return _C
@@ -49,6 +52,15 @@ def _load_timeline_variant(build_if_missing: bool):
             raise RuntimeError(f"timeline build {path} missing (python -m pytorch_mnist_ddp_amd._build --timeline)")
         from .. import _build
         _build.build(timeline=True)
+    return _load_from(path)
+
+
+def _load_from(path: str):
+    """The extension file ``path`` imported under the module name ``_C`` (its PyInit symbol)."""
+    import importlib.util
+    import sys
+    if not os.path.exists(path):
+        raise RuntimeError(f"native extension {path} missing")
     spec = importlib.util.spec_from_file_location("pytorch_mnist_ddp_amd._C", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)

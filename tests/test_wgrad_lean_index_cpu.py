@@ -11,7 +11,7 @@ c >= 24 bnd - 32 ks with bnd = 24 - c0 % 24 (a scalar per k-step).  The staging 
 record offset, the 2x2-window code ((r0 + row) & 1, x & 1) and the chunk row into one register.
 """
 
-H1, H2, HP, DYC_REC = 26, 24, 12, 192
+H1, H2, HP, DYC_REC = 26, 24, 12, 144
 
 
 def a1_row_of(r):

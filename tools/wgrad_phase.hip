@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> rec((size_t)B * DYC_BYTES_PER_IMAGE);
   for (size_t i = 0; i < rec.size(); ++i) {
     const size_t o = i % DYC_REC;
-    rec[i] = o < DYC_ROUTE ? (uint8_t)((o & 1) ? 0x3B : (rand() & 0xFF)) : (uint8_t)(rand() & 3);
+    rec[i] = o < DYC_ROUTE ? (uint8_t)((o & 1) ? 0x3B : (rand() & 0xFF)) : (uint8_t)(rand() & 0xFF);   // code bit planes: any byte
   }
   uint8_t* dyc; CK(hipMalloc(&dyc, rec.size())); CK(hipMemcpy(dyc, rec.data(), rec.size(), hipMemcpyHostToDevice));
   uint16_t* a1 = dev_rand<uint16_t>((size_t)B * H1 * H1 * C1, 0x3BFF);
