@@ -207,7 +207,13 @@ def parse_args(argv=None):
     ap.add_argument("--no-script-run", dest="script_run", action="store_false",
                     help="skip the mnist_ddp.py child job (total_cost_time_s)")
     ap.add_argument("--no-warm-replay", dest="warm_replay", action="store_false",
-                    help="do not replay the timed region's graphs once (state restored) before the warmup")
+                    help="do not replay the timed region's graphs (state restored) before the warmup")
+    ap.add_argument("--warm-replay-steps", type=int, default=int(os.environ.get("MNIST_AMD_WARM_STEPS", "500")),
+                    help="replay the timed region's graphs for at least this many steps before the warmup "
+                         "(model / optimizer / step state restored bit for bit; 0 = one round).  The GPU's "
+                         "clocks ramp over ~10 ms of load: a 20-step window opened on a device that ran "
+                         "only the warmup reads 67.8-68.3 us/step of device time, after 500 warm steps "
+                         "65.7-65.9 (600 steps: 64.7); profiles/r5/ab/warm_replay_steps.txt")
     return ap.parse_args(argv)
 
 
@@ -383,6 +389,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
     phases.add("graph_capture", tr.setup.s.get("graph_capture", 0.0) - cap0)
+    warm_steps = 0
     if args.warm_replay and args.steps > 0:
         # every graph the timed region replays has run once before t0 (model, optimizer and step
         # state restored bit for bit): the first timed replay pays no first-launch cost, and exactly
@@ -391,7 +398,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
         with phases.phase("warm_replay"):
             first = sum(set(tr._chunks(args.steps))) if tr.use_graphs else 0   # rows the replays read
             tr.engine.gather_rows(0, min(total, max(first, args.warmup)) * B)
-            tr.warm_graphs(args.steps)
+            warm_steps = tr.warm_graphs(args.steps, args.warm_replay_steps)
     diag.phase = "warmup"
     tr.engine.gather_rows(0, args.warmup * B)
     tr.run_steps(args.warmup)
@@ -542,7 +549,7 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                        "global_batch": B * world, "batch_per_gpu": B, "seq_len": None,
                        "parallelism": f"dp{world}", "optimizer": "Adadelta(lr=1.0)",
                        "graph_steps": args.graph_steps, "buckets": 1 if args.single_bucket else 2,
-                       "warm_replay": bool(args.warm_replay), **comm_info},
+                       "warm_replay": bool(args.warm_replay), "warm_replay_steps": warm_steps, **comm_info},
             "params_in_sync": in_sync,
             "desync_epoch": desync_epoch,
             "total_cost_time_s": script.get("total_cost_time_s") if script else None,

@@ -750,20 +750,32 @@ class FusedTrainer:
             for k in set(self._chunks(n)):
                 self._graph(k, self.B)
 
-    def warm_graphs(self, n: int) -> None:
-        """Replay once every graph ``run_steps(n)`` will use, then restore the model, optimizer and
-        step state bit for bit: a later timed ``run_steps(n)`` then starts on executables that have
-        already run (code objects resident, packets uploaded) without counting extra steps.  Runs
-        on every rank (the replays include the DDP collectives).  The rows the replays read must be
-        gathered (``engine.gather_rows``) beforehand."""
+    def warm_graphs(self, n: int, min_steps: int = 0) -> int:
+        """Replay every graph ``run_steps(n)`` will use - once, or as many rounds as it takes to run
+        ``min_steps`` steps (a step count, not a time, so every rank replays the same collectives) -
+        then restore the model, optimizer and step state bit for bit: a later timed ``run_steps(n)``
+        then starts on executables that have already run (code objects resident, packets uploaded)
+        on a device that has been busy for a while (its clocks ramp over ~10 ms of load: a 20-step
+        window measured from idle reads 67-68 us/step where 600 steps read 64.7), without counting
+        extra steps.  Runs on every rank (the replays include the DDP collectives).  The rows the
+        replays read must be gathered (``engine.gather_rows``) beforehand.  Returns the steps run."""
         if not self.use_graphs or n <= 0:
-            return
+            return 0
         ms = self.ms
         torch.cuda.synchronize(self.device)
         snap = {k: getattr(ms, k).clone() for k in ("param", "square_avg", "acc_delta", "state")}
         torch.cuda.synchronize(self.device)
-        for k in sorted(set(self._chunks(n))):
-            self.engine.replay(self._graph(k, self.B))
+        sizes = sorted(set(self._chunks(n)))
+        rounds = max(1, -(-int(min_steps) // sum(sizes)))
+        for r in range(rounds):
+            for k in sizes:
+                self.engine.replay(self._graph(k, self.B))
+            if r + 1 < rounds:
+                # every round replays the same steps: the device step counter (which indexes the
+                # gathered rows and the loss log) goes back to the snapshot, ordered after the round
+                # on the compute stream (the chunk-end join has the comm stream's work behind it)
+                with torch.cuda.stream(self.compute), torch.no_grad():
+                    ms.state.copy_(snap["state"])
         self.synchronize()
         with torch.no_grad():
             for k, v in snap.items():
@@ -771,6 +783,7 @@ class FusedTrainer:
         torch.cuda.synchronize(self.device)
         self.engine.refresh_shadows()
         torch.cuda.synchronize(self.device)
+        return rounds * sum(sizes)
 
     def run_steps(self, n: int) -> None:
         """Enqueue ``n`` full-batch steps continuing from the device step counter (no host sync)."""
