@@ -228,7 +228,9 @@ struct F32Step {
   float* w2bwd;               // [9][64][32] conv2 weight, input-gradient B operand
   float* w1p;                 // [128][144][64] fc1 weight with its input index position-major
                               // (pooled position, channel): the fc1 input-gradient B operand
-  float* a1;                  // [B][26][26][32] ReLU(conv1); then the conv1 pre-activation gradient
+  float* a1;                  // [B][26][26][32] ReLU(conv1)
+  float* dx1;                 // [B][26][26][32] the conv1 pre-activation gradient (its own buffer, so
+                              // the conv2 weight gradient - which reads a1 - can run beside it)
   float* y2;                  // [B][24][24][64] conv2 pre-activation; then its gradient
   float* p;                   // [B][9216] pooled + dropout, torch flatten order
   uint8_t* pm;                // [B][9216] argmax (bits 0-1), dropout keep (2), pooled > 0 (3)
@@ -254,6 +256,13 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s);
 void launch_f32_backward(const F32Step& a, int B, hipStream_t s);
 void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s);     // = the first half of it
 void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s);   // = the second half
+// ... which is, in order: fc1 input gradient (dy2), conv2 weight gradient (reads dy2 + a1), conv2
+// input gradient + conv1 weight gradient (dy2 -> dx1), split-K reduce (both partial sets).  The
+// OVERLAP schedule runs the weight gradient on the comm stream beside the input-gradient part.
+void launch_f32_fc1x(const F32Step& a, int B, hipStream_t s);
+void launch_f32_conv2w(const F32Step& a, int B, hipStream_t s);
+void launch_f32_conv2x_conv1w(const F32Step& a, int B, hipStream_t s);
+void launch_f32_conv_reduce(const F32Step& a, int B, hipStream_t s);
 
 // direct xGMI all-reduce (reduce-scatter + all-gather over IPC-mapped peer buckets; xgmi_allreduce.hip)
 constexpr int XGMI_MAX_RANKS = 8;          // one node

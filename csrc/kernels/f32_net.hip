@@ -286,7 +286,8 @@ struct PConv2X {
   int M, N, K, kc;
   const float* dy2;
   const float* w2bwd;   // [tap][co][ci]
-  float* a1;
+  const float* a1;      // the ReLU mask operand
+  float* dx1;
   __device__ void prepare() {}
   __device__ float4 a4(int m, int k) const {
     const int b = m / NPIX1, pix = m - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
@@ -298,8 +299,8 @@ struct PConv2X {
   }
   __device__ float4 b4(int k, int n) const { return *reinterpret_cast<const float4*>(w2bwd + k * C1 + n); }
   __device__ void put(int m, int n, float v, int) const {
-    float* q = a1 + (int64_t)m * C1 + n;
-    *q = (*q > 0.0f) ? v : 0.0f;
+    const int64_t e = (int64_t)m * C1 + n;
+    dx1[e] = (a1[e] > 0.0f) ? v : 0.0f;
   }
 };
 
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G
         const bool ok = m < p1;
         const int pix = (ok ? m : p0) - b * NPIX1, iy = pix / H1, ix = pix - iy * H1;
         off[u] = iy * IMG + ix;
-        d[u] = ok ? a.a1[(int64_t)(ok ? m : p0) * C1 + c] : 0.0f;
+        d[u] = ok ? a.dx1[(int64_t)(ok ? m : p0) * C1 + c] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -692,15 +693,29 @@ void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s) {
 
 // the rest: fc1 input gradient (reads the w1p copy, not the fc1 parameters the update rewrites),
 // conv2 weight / input gradients, conv1 weight gradient, slab reduce
-void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s) {
+void launch_f32_fc1x(const F32Step& a, int B, hipStream_t s) {
   gemm<64, 64>(PFc1X{NFLAT, B, NH, NH, a.dz1, a.w1p, a.pm, a.y2, a.state, 1.0f}, 1, s);
-  const int64_t k2 = (int64_t)B * NPIX2;
-  const int kc2 = kchunk(k2, F32_MAX_SPLITS), s2 = nsplit(k2, kc2);
-  gemm<64, 64>(PConv2W{C2, K2 + 1, (int)k2, kc2, a.y2, a.a1, a.c2part}, s2, s);
-  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1}, 1, s);
+}
+namespace {
+int conv2w_kc(int B) { return kchunk((int64_t)B * NPIX2, F32_MAX_SPLITS); }
+}  // namespace
+void launch_f32_conv2w(const F32Step& a, int B, hipStream_t s) {
+  gemm<64, 64>(PConv2W{C2, K2 + 1, B * NPIX2, conv2w_kc(B), a.y2, a.a1, a.c2part}, f32_conv2w_splits(B), s);
+}
+void launch_f32_conv2x_conv1w(const F32Step& a, int B, hipStream_t s) {
+  gemm<128, 32>(PConv2X{B * NPIX1, C1, 9 * C2, 9 * C2, a.y2, a.w2bwd, a.a1, a.dx1}, 1, s);
   const int s1 = f32_conv1w_splits(B);
   hipLaunchKernelGGL(f32_conv1w_kernel, dim3(s1), dim3(256), 0, s, a, B, s1);
-  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, s2, s1);
+}
+void launch_f32_conv_reduce(const F32Step& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(f32_conv_reduce_kernel, dim3(RED2_BLOCKS + RED1_BLOCKS), dim3(256), 0, s, a, f32_conv2w_splits(B),
+                     f32_conv1w_splits(B));
+}
+void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s) {
+  launch_f32_fc1x(a, B, s);
+  launch_f32_conv2w(a, B, s);
+  launch_f32_conv2x_conv1w(a, B, s);
+  launch_f32_conv_reduce(a, B, s);
 }
 
 void launch_f32_backward(const F32Step& a, int B, hipStream_t s) {

@@ -94,6 +94,7 @@ void Engine::alloc_workspace_f32() {
   const int64_t o_loss = carve(M * 4);
   const int64_t o_c2 = carve((int64_t)F32_MAX_SPLITS * C2 * (9 * C1 + 1) * 4);
   const int64_t o_c1 = carve((int64_t)F32_C1W_BLOCKS * C1 * 10 * 4);
+  const int64_t o_dx1 = carve(M * H1 * H1 * C1 * 4);
   HIP_OK(hipMalloc(&ws32_, off));
   launch_fill(ws32_, off, 0, nullptr);
   HIP_OK(hipStreamSynchronize(nullptr));
@@ -104,6 +105,7 @@ void Engine::alloc_workspace_f32() {
   w.w2bwd = reinterpret_cast<float*>(b + o_w2b);
   w.w1p = reinterpret_cast<float*>(b + o_w1p);
   w.a1 = reinterpret_cast<float*>(b + o_a1);
+  w.dx1 = reinterpret_cast<float*>(b + o_dx1);
   w.y2 = reinterpret_cast<float*>(b + o_y2);
   w.p = reinterpret_cast<float*>(b + o_p);
   w.pm = reinterpret_cast<uint8_t*>(b + o_pm);
@@ -493,8 +495,9 @@ void Engine::enqueue_step(int batch, bool last) {
 // compute stream), the whole Adadelta update (which advances the device step counter).
 // OVERLAP (single GPU): the fc update (98 % of the parameters) runs on the comm stream beside the
 // conv backward once the fc gradients are final; the next step's first kernel waits for it.
-//   C: (wait [1] >= [0]) forward, fc grads, +[0], conv grads, conv update (+step)
-//   M: wait [0] >= [1]+1, fc update, +[1]
+//   C: (wait [1] >= [0]) forward, fc grads, +[0], fc1 input grad, +[4], conv2 input grad + conv1
+//      weight grad, wait [3] >= [4], conv reduce, conv update (+step)
+//   M: wait [0] >= [1]+1, fc update, +[1], wait [4] >= [3]+1, conv2 weight grad, +[3]
 void Engine::enqueue_step_f32(int batch, bool last) {
   if (sched_ == OVERLAP) {
     const bool M = enq_main_, S = enq_side_;
@@ -513,12 +516,19 @@ void Engine::enqueue_step_f32(int batch, bool last) {
     a.inv_batch = ddp_head_inv_batch(batch, world_);
     AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                     buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+    // ... and the conv2 weight gradient (reads dy2 + a1) on the comm stream beside the conv2 input
+    // gradient + conv1 weight gradient: [4] counts fc1 input gradients (dy2) done, [3] conv2 weight
+    // gradients done (the bf16 schedules' dgrad / conv2 counters, unused by the fp32 step)
     if (M) {
       if (side_pending_) launch_stream_wait(sync_ + 1, sync_ + 0, 0, sync_ + 2, compute_);
       launch_f32_forward(a, batch, true, compute_);
       launch_f32_backward_fc(a, batch, compute_);
       launch_stream_signal(sync_ + 0, compute_);
-      launch_f32_backward_conv(a, batch, compute_);
+      launch_f32_fc1x(a, batch, compute_);
+      launch_stream_signal(sync_ + 4, compute_);
+      launch_f32_conv2x_conv1w(a, batch, compute_);
+      launch_stream_wait(sync_ + 3, sync_ + 4, 0, sync_ + 2, compute_);
+      launch_f32_conv_reduce(a, batch, compute_);
       AdadeltaArgs ac = ad;
       ac.state_inc = buf_.state;
       launch_adadelta(ac, ADA_CONV, compute_);
@@ -527,6 +537,9 @@ void Engine::enqueue_step_f32(int batch, bool last) {
       launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
       launch_stream_signal(sync_ + 1, comm_stream_);
+      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+      launch_f32_conv2w(a, batch, comm_stream_);
+      launch_stream_signal(sync_ + 3, comm_stream_);
     }
     side_pending_ = true;
     if (last) {
