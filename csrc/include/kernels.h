@@ -254,7 +254,9 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s);
 // fc2 / fc1-bias grads + loss log, fc1 weight grad, fc1 input grad (+ unpool), conv2 weight grad,
 // conv2 input grad (+ conv1 ReLU), conv1 weight grad, split-K reduce: every gradient of the step
 void launch_f32_backward(const F32Step& a, int B, hipStream_t s);
-void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s);     // = the first half of it
+void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s);     // = the first half of it:
+void launch_f32_fc_small(const F32Step& a, int B, hipStream_t s);   // fc2 weight / bias, fc1 bias, loss log
+void launch_f32_fc1w(const F32Step& a, int B, hipStream_t s);       // fc1 weight (reads dz1 + p)
 void launch_f32_backward_conv(const F32Step& a, int B, hipStream_t s);   // = the second half
 // ... which is, in order: fc1 input gradient (dy2), conv2 weight gradient (reads dy2 + a1), conv2
 // input gradient + conv1 weight gradient (dy2 -> dx1), split-K reduce (both partial sets).  The

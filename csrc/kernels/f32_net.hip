@@ -686,9 +686,15 @@ void launch_f32_forward(const F32Step& a, int B, bool train, hipStream_t s) {
 }
 
 // fc gradients (fc2 weight / bias, fc1 bias, fc1 weight): after these the fc update may start
-void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s) {
+void launch_f32_fc_small(const F32Step& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(f32_fc_small_kernel, dim3(NH), dim3(256), 0, s, a, B);
+}
+void launch_f32_fc1w(const F32Step& a, int B, hipStream_t s) {
   gemm<64, 64>(PFc1W{NH, NFLAT, B, (B + BK - 1) / BK * BK, a.dz1, a.p, a.grad + OFF_FC1_W}, 1, s);
+}
+void launch_f32_backward_fc(const F32Step& a, int B, hipStream_t s) {
+  launch_f32_fc_small(a, B, s);
+  launch_f32_fc1w(a, B, s);
 }
 
 // the rest: fc1 input gradient (reads the w1p copy, not the fc1 parameters the update rewrites),

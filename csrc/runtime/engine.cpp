@@ -495,9 +495,9 @@ void Engine::enqueue_step(int batch, bool last) {
 // compute stream), the whole Adadelta update (which advances the device step counter).
 // OVERLAP (single GPU): the fc update (98 % of the parameters) runs on the comm stream beside the
 // conv backward once the fc gradients are final; the next step's first kernel waits for it.
-//   C: (wait [1] >= [0]) forward, fc grads, +[0], fc1 input grad, +[4], conv2 input grad + conv1
-//      weight grad, wait [3] >= [4], conv reduce, conv update (+step)
-//   M: wait [0] >= [1]+1, fc update, +[1], wait [4] >= [3]+1, conv2 weight grad, +[3]
+//   C: (wait [1] >= [0]) forward, fc2 / fc1-bias grads, +[0], fc1 input grad, +[4], conv2 input grad
+//      + conv1 weight grad, wait [3] >= [4], conv reduce, conv update (+step)
+//   M: wait [0] >= [1]+1, fc1 weight grad, fc update, +[1], wait [4] >= [3]+1, conv2 weight grad, +[3]
 void Engine::enqueue_step_f32(int batch, bool last) {
   if (sched_ == OVERLAP) {
     const bool M = enq_main_, S = enq_side_;
@@ -522,7 +522,7 @@ void Engine::enqueue_step_f32(int batch, bool last) {
     if (M) {
       if (side_pending_) launch_stream_wait(sync_ + 1, sync_ + 0, 0, sync_ + 2, compute_);
       launch_f32_forward(a, batch, true, compute_);
-      launch_f32_backward_fc(a, batch, compute_);
+      launch_f32_fc_small(a, batch, compute_);
       launch_stream_signal(sync_ + 0, compute_);
       launch_f32_fc1x(a, batch, compute_);
       launch_stream_signal(sync_ + 4, compute_);
@@ -535,6 +535,7 @@ void Engine::enqueue_step_f32(int batch, bool last) {
     }
     if (S) {
       launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+      launch_f32_fc1w(a, batch, comm_stream_);
       launch_adadelta(ad, ADA_FC, comm_stream_);
       launch_stream_signal(sync_ + 1, comm_stream_);
       launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
