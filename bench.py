@@ -408,14 +408,13 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     torch.cuda.synchronize()
     diag.phase = "timed"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(tr.compute)                                   # device-side view of the same window
+    ev0.record(tr.compute)                                   # device-side view of the same window (the
+    t0 = time.perf_counter()                                 # streams are idle: it completes at once)
     tr.engine.gather_rows(args.warmup * B, args.steps * B)   # the device DataLoader work is timed too
     tr.run_steps(args.steps)
     ev1.record(tr.compute)                                   # (after the chunk's join: all streams)
     t_enq = time.perf_counter()                              # host: every timed chunk enqueued
-    tr.engine.sync_streams()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()                                 # every stream of the device
     if use_pg:
         barrier()
     t1 = time.perf_counter()
