@@ -634,6 +634,10 @@ class FusedTrainer:
         n = idx.numel()
         if n > self.train_idx.numel():
             raise ValueError("epoch index vector larger than the device buffer")
+        # the device gather and the step kernels read dataset rows by these indices unchecked: an
+        # out-of-range index is a GPU memory fault, so it is refused here (one host pass, ~20 us)
+        if n and (int(idx.min()) < 0 or int(idx.max()) >= self.train_u8.shape[0]):
+            raise ValueError(f"epoch index out of range [0, {self.train_u8.shape[0]})")
         k = self._idx_k
         self._idx_k ^= 1
         if self._idx_ev[k] is not None:

@@ -35,6 +35,28 @@ def test_graph_replay_bitwise_equals_eager(cuda_device):
     assert ms_g.get_step() == 10
 
 
+def test_multi_round_warm_replay_restores_state_bitwise(cuda_device):
+    """bench.py's warm replays (FusedTrainer.warm_graphs with a step budget): the timed chunk graphs
+    replayed for several rounds, the step counter restored after every round (it indexes the
+    gathered rows and the loss log: a run past them faulted the GPU once) and the whole state after
+    the last; the steps that follow are bitwise those of a trainer that never replayed."""
+    n, steps = 6, 4
+    idx = torch.randperm(n * 200, generator=torch.Generator().manual_seed(11))   # the dataset's rows
+    runs = []
+    for warm in (0, 5 * steps):
+        _, ms, t = _trainer(cuda_device, graph_steps=steps, n_train=n * 200)
+        t.start_stream(idx, gather=True)
+        t.precapture(steps)
+        if warm:
+            assert t.warm_graphs(steps, warm) == warm
+        t.run_steps(n)
+        t.synchronize()
+        runs.append((ms.param.clone(), t.loss_log[:n].clone(), ms.get_step()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert runs[0][2] == runs[1][2] == n
+
+
 def test_training_converges_on_synthetic(cuda_device):
     net, ms, t = _trainer(cuda_device, graph_steps=10, n_train=6000)
     stream = RandomIndexStream(6000)
