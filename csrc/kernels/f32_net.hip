@@ -263,6 +263,7 @@ struct PFc1X {
 // conv2 weight + bias gradient, split-K over the B*576 output pixels:
 // part[z][co][n] = sum_m dy2[m][co] im2col(a1)[m][n] (n < 288), sum_m dy2[m][co] (n = 288)
 struct PConv2W {
+  static constexpr int KT = 32;   // 600 steps 281.3 -> 274.4-274.9 us (the input-gradient / forward GEMMs: no gain / slower)
   static constexpr bool A_KF = false, B_KF = false;
   int M, N, K, kc;
   const float* dy2;
