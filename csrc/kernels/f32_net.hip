@@ -63,11 +63,14 @@ struct has_put4 { static constexpr bool value = false; };
 template <class P>
 struct has_put4<P, decltype(void(P::PUT4))> { static constexpr bool value = P::PUT4; };
 
-template <int BM, int BN, int BK, class P>
+// 4 waves in a WGM x (4 / WGM) grid, each owning a (BM / WGM) x (BN * WGM / 4) tile of TM x TN
+// 16 x 16 MFMA blocks: wider per-wave tiles read fewer LDS operands per MFMA
+template <int BM, int BN, int BK, int WGM, class P>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
-  static_assert((BM / 32) * (BN / 32) == 4, "4 waves of 32 x 32");
+  constexpr int WN = 4 / WGM, TM = BM / WGM / 16, TN = BN / WN / 16;
+  static_assert(WGM * WN == 4 && TM >= 1 && TN >= 1 && TM * WGM * 16 == BM && TN * WN * 16 == BN, "wave tiling");
   constexpr int NA = BM * BK / 4, NB = BN * BK / 4;            // float4s per operand tile
-  constexpr int EA = (NA + 255) / 256, EB = (NB + 255) / 256, WN = BN / 32;
+  constexpr int EA = (NA + 255) / 256, EB = (NB + 255) / 256;
   __shared__ __attribute__((aligned(16))) float As[BK][BM + 4];
   __shared__ __attribute__((aligned(16))) float Bs[BK][BN + 4];
   p.prepare();
@@ -76,11 +79,11 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int k_lo = blockIdx.z * p.kc;
   const int k_hi = min(p.K, k_lo + p.kc);
-  floatx4 acc[2][2];
+  floatx4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // register prefetch: the next k-tile's gathers are issued before this tile's MFMAs, so their
   // latency hides under the matrix work instead of sitting between the two barriers
@@ -127,24 +130,24 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
     if (k0 + BK < k_hi) { F32_GEMM_LOAD(k0 + BK) }   // in flight under the MFMAs below
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      float av[2], bv[2];
+      float av[TM], bv[TN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = As[kk + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < TM; ++i) av[i] = As[kk + (lane >> 4)][wm * (16 * TM) + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = Bs[kk + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[kk + (lane >> 4)][wn * (16 * TN) + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
   }
   // C/D map of the 16 x 16 MFMA: column = lane & 15, row = 4 * (lane >> 4) + register
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int mb = m0 + wm * 32 + i * 16 + 4 * (lane >> 4);
-      const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+    for (int j = 0; j < TN; ++j) {
+      const int mb = m0 + wm * (16 * TM) + i * 16 + 4 * (lane >> 4);
+      const int n = n0 + wn * (16 * TN) + j * 16 + (lane & 15);
       if constexpr (has_put4<P>::value) {       // the lane's 4 consecutive rows at once (M % 4 == 0)
         if (mb < p.M && n < p.N) p.put4(mb, n, acc[i][j], blockIdx.z);
       } else {
@@ -163,10 +166,10 @@ struct kt_of { static constexpr int value = 16; };
 template <class P>
 struct kt_of<P, decltype(void(P::KT))> { static constexpr int value = P::KT; };
 
-template <int BM, int BN, class P>
+template <int BM, int BN, class P, int WGM = BM / 32>
 void gemm(const P& p, int splits, hipStream_t s) {
   const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, kt_of<P>::value, P>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((f32_gemm_kernel<BM, BN, kt_of<P>::value, WGM, P>), grid, dim3(256), 0, s, p);
 }
 
 // ---- policies
