@@ -147,6 +147,8 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s);      // dgrad(
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 dgrad + conv1 wgrad partials
 void launch_conv_wgrad(const ConvBwdArgs& a, int B, hipStream_t s);    // conv2 wgrad + bias partials
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s);
+// reduce blocks [lo, hi) only (RED_W2_PARTS conv2 blocks, then the conv1 ones: see RED_ALL_PARTS)
+void launch_conv_grad_reduce_parts(const ConvBwdArgs& a, int B, int lo, int hi, hipStream_t s);
 
 // ---------------- optimizer ----------------
 struct AdadeltaArgs {

@@ -829,11 +829,11 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
 
 // --------------------------------------------------------------------------------------------
 // Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
-__global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B) {
+__global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B, int bid0) {
   TL_SCOPE(TL_CONV_REDUCE);
   __shared__ float4 red[256];
   float* grad = a.grad;
-  reduce_conv_grads(a, B, blockIdx.x, red, [grad](int64_t e, float v) { grad[e] = v; });
+  reduce_conv_grads(a, B, blockIdx.x + bid0, red, [grad](int64_t e, float v) { grad[e] = v; });
 }
 
 static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
@@ -909,7 +909,11 @@ void launch_conv_bwd(const ConvBwdArgs& a, int B, hipStream_t s) {
 }
 
 void launch_conv_grad_reduce(const ConvBwdArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_WGS), dim3(256), 0, s, a, B);
+  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(RED_WGS), dim3(256), 0, s, a, B, 0);
+}
+void launch_conv_grad_reduce_parts(const ConvBwdArgs& a, int B, int lo, int hi, hipStream_t s) {
+  if (lo < 0 || hi > RED_WGS || lo >= hi) throw std::runtime_error("conv_grad_reduce: bad part range");
+  hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3(hi - lo), dim3(256), 0, s, a, B, lo);
 }
 
 TL_DEFINE_HOST(conv_bwd)

@@ -2,6 +2,7 @@
 #include "host_logic.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -307,10 +308,10 @@ void Engine::enqueue_step(int batch, bool last) {
     // the fc bucket (98.4 % of the bytes) forks onto the comm stream as soon as fc_bwd is done and
     // overlaps the conv backward; the conv bucket follows on compute after the join, so the one
     // communicator sees fc, conv in the same order on every rank and never two collectives at once.
-    // The join waits for the fc ALL-REDUCE only: the fc update runs after it on the comm stream
-    // (144 workgroups, beside dgrad and the conv tail) and is ordered before the next step's fc1_fwd
-    // by trunk_fwd's completion hold on device counters ([0] wgrad starts, [1] fc updates done), as in
-    // OVERLAP - at world > 1 the update is no longer on the path to the conv all-reduce.
+    // The join waits for the fc all-reduce (and conv2's slab reduce, below) only: the fc update runs
+    // after them on the comm stream (144 workgroups, beside the conv tail) and is ordered before the
+    // next step's fc1_fwd by trunk_fwd's completion hold on device counters ([0] wgrad starts, [1] fc
+    // updates done), as in OVERLAP - at world > 1 the update is not on the path to the conv all-reduce.
     // (capture order matters: the graph executor keeps a fork's first-captured child on the
     // launching queue, so conv2 wgrad is enqueued before the comm branch)
     HIP_OK(hipEventRecord(ev_fc_, compute_));
@@ -323,6 +324,18 @@ void Engine::enqueue_step(int batch, bool last) {
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
+    // hand-offs (distinct queues): conv2's slab reduce (289 of the conv bucket's 309 reduce
+    // workgroups) follows the fc all-reduce on the comm stream, released by dgrad's start (wgrad,
+    // which writes the slabs, is done) and running under dgrad; the join waits for it, so the step
+    // tail keeps only conv1's 20 reduce workgroups before the conv all-reduce.  The fc update comes
+    // after it (world 1, 600 steps: 82.5-82.6 -> 75.3 us/step; the update before it, so that the
+    // join also waits for the update: 86.7; profiles/r5/ddp_world1/rccl_conv2_reduce_side.txt)
+    const bool c2r = rccl_handoff_ && !trace_;
+    if (c2r) {
+      launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
+      launch_conv_grad_reduce_parts(cb, B, 0, RED_W2_PARTS, comm_stream_);
+      launch_stream_signal(sync_ + 3, comm_stream_);
+    }
     if (rccl_handoff_) {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       launch_adadelta(ad, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
@@ -334,10 +347,15 @@ void Engine::enqueue_step(int batch, bool last) {
     }
     phase_end();
     phase_begin("bwd_conv_dgrad");
-    launch_conv_dgrad(cb, B, compute_);
+    ConvBwdArgs cbd = cb;
+    if (c2r) cbd.signal_ctr = sync_ + 4;        // dgrad's start releases conv2's reduce on the comm stream
+    launch_conv_dgrad(cbd, B, compute_);
     phase_end();
     phase_begin("allreduce_conv+update");
-    launch_conv_grad_reduce(cb, B, compute_);
+    if (c2r)
+      launch_conv_grad_reduce_parts(cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+    else
+      launch_conv_grad_reduce(cb, B, compute_);
     HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
     comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
     launch_adadelta(adc, ADA_CONV, compute_);
