@@ -510,14 +510,18 @@ void Engine::enqueue_step(int batch, bool last) {
 }
 
 // fp32 step: forward, every gradient, (RCCL: one all-reduce of the whole flat gradient on the
-// compute stream), the whole Adadelta update (which advances the device step counter).
+// compute stream), the whole Adadelta update (which advances the device step counter) - SERIAL / RCCL.
 // OVERLAP (single GPU): the fc update (98 % of the parameters) runs on the comm stream beside the
 // conv backward once the fc gradients are final; the next step's first kernel waits for it.
 //   C: (wait [1] >= [0]) forward, fc2 / fc1-bias grads, +[0], fc1 input grad, +[4], conv2 input grad
 //      + conv1 weight grad, wait [3] >= [4], conv reduce, conv update (+step)
 //   M: wait [0] >= [1]+1, fc1 weight grad, fc update, +[1], wait [4] >= [3]+1, conv2 weight grad, +[3]
+// XGMI (world > 1) runs the same two chains with each update replaced by its bucket's all-reduce with
+// the Adadelta step fused: the fc bucket (two-shot) on the comm stream beside the conv backward, the
+// conv bucket (one-shot) at the step tail (different channels, so the two never share flags)
 void Engine::enqueue_step_f32(int batch, bool last) {
-  if (sched_ == OVERLAP) {
+  if (sched_ == OVERLAP || sched_ == XGMI) {
+    const bool xg = sched_ == XGMI;
     const bool M = enq_main_, S = enq_side_;
     if (!side_forked_) {
       HIP_OK(hipEventRecord(ev_fc_, compute_));
@@ -549,12 +553,23 @@ void Engine::enqueue_step_f32(int batch, bool last) {
       launch_f32_conv_reduce(a, batch, compute_);
       AdadeltaArgs ac = ad;
       ac.state_inc = buf_.state;
-      launch_adadelta(ac, ADA_CONV, compute_);
+      if (xg) {
+        ac.grad = xgmi_->out();
+        xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_, &ac);
+      } else {
+        launch_adadelta(ac, ADA_CONV, compute_);
+      }
     }
     if (S) {
       launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
       launch_f32_fc1w(a, batch, comm_stream_);
-      launch_adadelta(ad, ADA_FC, comm_stream_);
+      if (xg) {
+        AdadeltaArgs af = ad;
+        af.grad = xgmi_->out();
+        xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_, &af);
+      } else {
+        launch_adadelta(ad, ADA_FC, comm_stream_);
+      }
       launch_stream_signal(sync_ + 1, comm_stream_);
       launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, comm_stream_);
       launch_f32_conv2w(a, batch, comm_stream_);
@@ -588,15 +603,8 @@ void Engine::enqueue_step_f32(int batch, bool last) {
   phase_begin("allreduce+update");
   AdadeltaArgs ad{buf_.param, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, buf_.state};
-  if (sched_ == XGMI) {
-    // the whole flat gradient in one two-shot xGMI all-reduce (the producers wrote x->in()) with the
-    // Adadelta step fused into its gather phase (same per-element math as the separate update)
-    ad.grad = xgmi_->out();
-    xgmi_->allreduce(XGMI_CH_FC, 0, PARAM_TOTAL, compute_, &ad);
-  } else {
-    if (sched_ == RCCL) comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
-    launch_adadelta(ad, ADA_ALL, compute_);
-  }
+  if (sched_ == RCCL) comm_->allreduce_sum(buf_.grad, PARAM_TOTAL, 0, compute_);
+  launch_adadelta(ad, ADA_ALL, compute_);
   phase_end();
 }
 

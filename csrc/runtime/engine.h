@@ -150,7 +150,7 @@ class Engine {
   void enqueue_step(int batch, bool last);
   void enqueue_step_f32(int batch, bool last);
   F32Step f32_args() const;
-  bool side_schedule() const { return sched_ == OVERLAP || (sched_ == XGMI && !f32_); }
+  bool side_schedule() const { return sched_ == OVERLAP || sched_ == XGMI; }
   bool use_conv2_stream() const { return conv2_stream_ && sched_ == OVERLAP && !f32_ && !trace_; }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);

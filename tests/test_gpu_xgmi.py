@@ -40,6 +40,30 @@ def _world1_trainer(dev, comm, **kw):
     return ms, t
 
 
+def test_fp32_xgmi_schedule_world1_matches_single_gpu(cuda_device):
+    """The fp32 step's XGMI schedule - the fc bucket's two-shot all-reduce with the Adadelta step
+    fused on the comm stream beside the conv backward, the conv bucket's one-shot at the step tail,
+    split side / compute graphs - at world 1 trains bitwise like the single-GPU fp32 OVERLAP step."""
+    import torch
+    import torch.distributed as dist
+    from conftest import init_world1_pg
+    init_world1_pg("gloo")
+    try:
+        idx = torch.randperm(2000, generator=torch.Generator().manual_seed(6))
+        res = {}
+        for name, kw in (("xgmi", dict(allreduce="xgmi", fp32=True)), ("single", dict(fp32=True))):
+            ms, t = _world1_trainer(cuda_device, None, **kw)
+            assert (t.allreduce == "xgmi") if name == "xgmi" else t.overlap
+            for ep in (1, 2):
+                t.train_epoch(ep, idx)
+            t.synchronize()
+            res[name] = (ms.param.clone(), t.loss_log.clone())
+        assert torch.equal(res["xgmi"][0], res["single"][0])
+        assert torch.equal(res["xgmi"][1], res["single"][1])
+    finally:
+        dist.destroy_process_group()
+
+
 def test_transport_choice_by_schedule_replay_world1(cuda_device):
     """--allreduce auto picks the transport by replaying each candidate's PRODUCTION schedule: at
     world 1 with an RCCL communicator and the xGMI candidate forced in (probe_world1), both captured
