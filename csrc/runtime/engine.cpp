@@ -520,7 +520,11 @@ void Engine::enqueue_step(int batch, bool last) {
 // the Adadelta step fused: the fc bucket (two-shot) on the comm stream beside the conv backward, the
 // conv bucket (one-shot) at the step tail (different channels, so the two never share flags)
 void Engine::enqueue_step_f32(int batch, bool last) {
-  if (sched_ == OVERLAP || sched_ == XGMI) {
+  // RCCL with hand-offs: the same chains in one graph, the fc bucket's all-reduce ahead of the fc
+  // update on the comm stream, the conv bucket's after compute's wait for [3] (which follows the fc
+  // all-reduce on the comm stream: the communicator never has two collectives in flight, fc first)
+  const bool rc = sched_ == RCCL && rccl_handoff_ && two_buckets_ && !trace_;
+  if (sched_ == OVERLAP || sched_ == XGMI || rc) {
     const bool xg = sched_ == XGMI;
     const bool M = enq_main_, S = enq_side_;
     if (!side_forked_) {
@@ -557,6 +561,7 @@ void Engine::enqueue_step_f32(int batch, bool last) {
         ac.grad = xgmi_->out();
         xgmi_->allreduce(XGMI_CH_CONV, OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, compute_, &ac);
       } else {
+        if (rc) comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
         launch_adadelta(ac, ADA_CONV, compute_);
       }
     }
@@ -568,6 +573,7 @@ void Engine::enqueue_step_f32(int batch, bool last) {
         af.grad = xgmi_->out();
         xgmi_->allreduce(XGMI_CH_FC, OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, comm_stream_, &af);
       } else {
+        if (rc) comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
         launch_adadelta(ad, ADA_FC, comm_stream_);
       }
       launch_stream_signal(sync_ + 1, comm_stream_);

@@ -102,17 +102,19 @@ def test_transport_choice_by_schedule_replay_world1(cuda_device):
         dist.destroy_process_group()
 
 
-def test_rccl_schedule_world1_matches_single_gpu(tmp_path):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_rccl_schedule_world1_matches_single_gpu(tmp_path, dtype):
     """The RCCL DDP schedule (fc bucket forked onto the comm stream, conv bucket after the join, one
     communicator, one graph per chunk in step order) at world 1 (--force-comm) trains bitwise like the
-    plain single-GPU step, and the bench JSON names one communicator and the startup validation."""
+    plain single-GPU step, and the bench JSON names one communicator and the startup validation
+    (fp32: the fp32 step's chains, the fc bucket's all-reduce on the comm stream)."""
     import json
     outs = {}
     runs = (("rccl", ["--force-comm"]), ("plain", []))
     for name, extra in runs:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--standalone",
                "--local-addr", "127.0.0.1", os.path.join(ROOT, "bench.py"), "--allreduce", "rccl",
-               "--no-full-run", "--steps", "60", "--warmup", "10", *extra]
+               "--no-full-run", "--steps", "60", "--warmup", "10", "--dtype", dtype, *extra]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=tmp_path,
                            env=dict(os.environ, PYTHONPATH=ROOT))
         assert r.returncode == 0, (name, r.stderr[-3000:])
