@@ -193,6 +193,8 @@ PYBIND11_MODULE(_C, m) {
                 P<const StepState>(state), P<float>(grad), P<uint8_t>(dyc), P<float>(loss_log), grad_scale,
                 inv_batch, P<float>(part)};
     if (role < 0) launch_fc_bwd(a, B, Bp, S(stream));
+    else if (role == 3) launch_fc_bwd_dw1(a, B, Bp, S(stream));                  // role A alone, lean kernel
+    else if (role == 4) launch_fc_bwd(a, B, Bp, S(stream), false, false);       // roles C + B (B > 1024)
     else launch_fc_bwd_role(a, B, Bp, role, S(stream));
     check_launch();
   }, py::arg("dz1"), py::arg("p"), py::arg("pmask"), py::arg("w1t"), py::arg("h_bf"), py::arg("dl_bf"),
@@ -360,6 +362,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_xgmi_fuse_update", &Engine::set_xgmi_fuse_update)
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_rccl_handoff", &Engine::set_rccl_handoff)
+      .def_property("fc_dw1_side", &Engine::fc_dw1_side, &Engine::set_fc_dw1_side)
       .def("fault_hold", &Engine::fault_hold)
       .def("fault_release", [](Engine& e, uintptr_t stream) { e.fault_release(S(stream)); })
       .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())

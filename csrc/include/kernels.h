@@ -107,7 +107,9 @@ constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_P
                   FCB_PART_STRIDE = (FCB_PART_LOSS + 1 + 63) / 64 * 64;
 // reduce = false (B > 1024): the split partials are left for launch_fc_grad_reduce, which the
 // engine runs on the comm stream ahead of the fc all-reduce / update (off the compute chain)
-void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce = true);
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce = true, bool with_a = true);
+// role A (fc1 weight gradient split partials) alone, for B > 1024 with reduce = false / with_a = false
+void launch_fc_bwd_dw1(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s);   // no-op for B <= 1024
 void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t s);   // profiling aid
 

@@ -452,7 +452,10 @@ __device__ __forceinline__ int swz_row128(int row, int col) {   // 64 bf16 per r
 constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
 
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
-// loaded into VGPRs while the current one (double-buffered LDS) feeds the MFMAs; one barrier per slab.
+// loaded into VGPRs while the current one feeds the MFMAs.  DB: double-buffered LDS (24 KB), one
+// barrier per slab; !DB: one 12-KB buffer and a second barrier (fc_bwd_dw1_kernel, which must fit
+// beside two conv2_dgrad workgroups' 140 KB of LDS).  The same MFMA order either way.
+template <bool DB = true>
 __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, int sp, int S,
                                               unsigned char* smem) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -485,8 +488,9 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
   };
   fetch(kb0);
   for (int kb = kb0; kb < kb1; ++kb) {
-    uint16_t* dzs = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288);          // [32][128]
-    uint16_t* ps = reinterpret_cast<uint16_t*>(smem + (kb & 1) * 12288 + 8192);    // [32][64]
+    const int buf = DB ? (kb & 1) : 0;
+    uint16_t* dzs = reinterpret_cast<uint16_t*>(smem + buf * 12288);          // [32][128]
+    uint16_t* ps = reinterpret_cast<uint16_t*>(smem + buf * 12288 + 8192);    // [32][64]
     {
       const int r0 = tid >> 4, r1 = 16 + (tid >> 4), c = (tid & 15) * 8;
       *reinterpret_cast<uint4*>(dzs + r0 * 128 + swz_row256(r0, c)) = rz0;
@@ -513,6 +517,7 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
         }
       }
     }
+    if (!DB) __syncthreads();                          // the next slab rewrites the one buffer
   }
   // S == 1: final (scaled) gradient (write-through at small batches: read by the fc update only);
   // S > 1: unscaled partial in the same layout (fc_grad_reduce)
@@ -733,15 +738,17 @@ __host__ __device__ inline int fc_bwd_role_b_wgs(int B) {
 }
 
 // workgroups [C | A | B]; bid0 offsets a partial grid (launch_fc_bwd_role)
+// skip_a: roles C and B only (role A runs as fc_bwd_dw1_kernel on the comm stream)
 template <bool BIG>
-__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0) {
+__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0, int skip_a) {
   TL_SCOPE(TL_FC_BWD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const int bid = blockIdx.x + bid0;
   const int S = fc_bwd_splits(B);
   const int nA = S * ROLE_A_WGS;
+  int bid = blockIdx.x + bid0;
+  if (skip_a && bid >= S) bid += nA;
   // role C (long-running, one per split) first so it is dispatched before the short role-B tiles
   if (bid < S) {
     fc_bwd_role_c(a, B, Bp, bid, S, smem);
@@ -751,6 +758,18 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
   } else {
     fc_bwd_role_b<BIG>(a, B, Bp, bid - S - nA, fcb_mr(B), smem);
   }
+}
+
+// Role A alone (large batches, side schedules): the fc1 weight gradient's split partials on the comm
+// stream, beside conv2_wgrad / conv2_dgrad instead of on the compute chain.  It streams p once from
+// HBM (151 MB at B = 8192) at ~11 % MFMA use, the complement of the conv kernels' LDS / MFMA-bound
+// loops; 12 KB of LDS and <= 80 VGPRs (6 waves per SIMD) so that it fits beside both of them
+// (dgrad: 2 x 70 KB LDS, 2 x 216 VGPRs per SIMD; wgrad: 89 KB, 2 x 208).  Bitwise the same partials.
+__global__ __launch_bounds__(256, 6) void fc_bwd_dw1_kernel(FcBwdArgs a, int B, int Bp) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[12288];
+  const int S = fc_bwd_splits(B);
+  const int r = blockIdx.x;
+  fc_bwd_role_a<false>(a, B, Bp, r % ROLE_A_WGS, r / ROLE_A_WGS, S, smem);
 }
 
 // S > 1: fixed-order sum of the split partials (fc1.w, fc1.b, fc2.w, fc2.b share the grad layout
@@ -789,13 +808,22 @@ void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
 }
 
-void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce) {
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce, bool with_a) {
   const int S = fc_bwd_splits(B);
   if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
-  const int grid = S + S * ROLE_A_WGS + fc_bwd_role_b_wgs(B);
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0);
+  if (!with_a && (S <= 1 || reduce))
+    throw std::runtime_error("fc_bwd: role A leaves the launch only for split partials reduced later");
+  const int grid = S + (with_a ? S * ROLE_A_WGS : 0) + fc_bwd_role_b_wgs(B);
+  const int skip = with_a ? 0 : 1;
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, skip);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, skip);
   if (reduce) launch_fc_grad_reduce(a, B, s);
+}
+
+void launch_fc_bwd_dw1(const FcBwdArgs& a, int B, int Bp, hipStream_t s) {
+  const int S = fc_bwd_splits(B);
+  if (S <= 1 || !a.part) throw std::runtime_error("fc_bwd_dw1: split partials only (batch > 1024)");
+  hipLaunchKernelGGL(fc_bwd_dw1_kernel, dim3(S * ROLE_A_WGS), dim3(256), 0, s, a, B, Bp);
 }
 
 // profiling aid: one role of fc_bwd on its own (0 = C, 1 = A, 2 = B)
@@ -804,8 +832,8 @@ void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t
   const int nb = fc_bwd_role_b_wgs(B);
   const int grid = role == 0 ? S : role == 1 ? S * ROLE_A_WGS : nb;
   const int bid0 = role == 0 ? 0 : role == 1 ? S : S + S * ROLE_A_WGS;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
 }
 
 TL_DEFINE_HOST(fc_head)

@@ -268,8 +268,14 @@ void Engine::enqueue_step(int batch, bool last) {
   // B > 1024: the fc split partials are summed on the comm stream, ahead of the fc update /
   // all-reduce that consumes them, instead of on the compute chain (SERIAL / one-bucket RCCL: here)
   const bool fc_reduce_side = fc_bwd_splits(B) > 1 && (side || (sched_ == RCCL && two_buckets_));
+  // ... and the fc1 weight gradient itself (fc_bwd role A: 145 workgroups per 1024-row split streaming
+  // p from HBM) leaves the compute chain for the comm stream, ahead of that reduce, where it runs
+  // beside conv2_wgrad / conv2_dgrad.  The next step cannot overwrite p / dz1 before it is done: the
+  // comm stream's later launches (fc update, conv2 update) gate the next trunk_fwd / fc1_fwd.  Not
+  // with the opt-in conv2 stream, whose conv2 update no longer queues behind it.
+  const bool dw1_side = fc_reduce_side && fc_dw1_side_ && !c2s;
   phase_begin("bwd_fc");
-  if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side);
+  if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side, !dw1_side);
   phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
@@ -322,6 +328,7 @@ void Engine::enqueue_step(int batch, bool last) {
     phase_end();
     phase_begin("allreduce_fc+update");
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
+    if (dw1_side) launch_fc_bwd_dw1(fb, B, Bp, comm_stream_);
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     comm_->allreduce_sum(buf_.grad + OFF_FC1_W, OFF_CONV1_W - OFF_FC1_W, 0, comm_stream_);
     // hand-offs (distinct queues): conv2's slab reduce (289 of the conv bucket's 309 reduce
@@ -392,6 +399,7 @@ void Engine::enqueue_step(int batch, bool last) {
     else
       launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
     comm_sig3_pending_ = false;
+    if (dw1_side) launch_fc_bwd_dw1(fb, B, Bp, comm_stream_);
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     if (!xg) {
       AdadeltaArgs af = ad;

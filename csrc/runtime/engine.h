@@ -91,6 +91,9 @@ class Engine {
   // the compute / comm streams on distinct hardware queues: probe_stream_handoff); off = the update
   // before the join (graph edges only)
   void set_rccl_handoff(bool on) { rccl_handoff_ = on; }
+  // B > 1024 side schedules: fc_bwd's role A (fc1 weight gradient) on the comm stream (default on)
+  void set_fc_dw1_side(bool on) { fc_dw1_side_ = on; }
+  bool fc_dw1_side() const { return fc_dw1_side_; }
   // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
   // hand-off counters and their error flag, so a schedule never inherits another's counts (e.g. an
   // aborted validation).  Detaching the xgmi communicator of the XGMI schedule unsets the schedule.
@@ -167,6 +170,7 @@ class Engine {
   float rho_, eps_, wd_;
   bool two_buckets_ = true;
   bool rccl_handoff_ = false;
+  bool fc_dw1_side_ = true;
   int idx_stride_ = 0;
   int sched_ = SERIAL;
   std::shared_ptr<RcclComm> comm_;

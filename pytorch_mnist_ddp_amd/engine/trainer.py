@@ -203,6 +203,9 @@ class FusedTrainer:
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay, fp32=self.fp32)
         self.engine.set_bucket_split(two_buckets)
+        # B > 1024, side schedules: fc_bwd's fc1 weight gradient on the comm stream beside the conv
+        # backward (MNIST_AMD_FC_DW1_SIDE=0: in the compute-stream fc_bwd launch, for A/B)
+        self.engine.fc_dw1_side = os.environ.get("MNIST_AMD_FC_DW1_SIDE", "1") != "0"
         self._graphs: dict[tuple[int, int], int] = {}        # captured chunks of the selected schedule
         self._graph_sets: dict[str, dict] = {}               # per transport (validation captures)
         self._eval_graph: int | None = None

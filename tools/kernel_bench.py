@@ -51,6 +51,7 @@ def main():
                                 round_up(B, 32), s, role=role, part=p(buf.fcpart))
     rows = [("fc_bwd (all roles)", fcb(-1)), ("fc_bwd role C (dW2, loss)", fcb(0)),
             ("fc_bwd role A (dW1, 145 WGs)", fcb(1)), ("fc_bwd role B (dy)", fcb(2)),
+            *([("fc_bwd_dw1 (role A, lean kernel)", fcb(3)), ("fc_bwd roles C+B", fcb(4))] if B > 1024 else []),
             ("fc1_fwd", lambda: Fk.fc1_fwd(ms, buf)),
             ("conv_bwd (dgrad+wgrad+reduce)", lambda: Fk.conv_bwd(ms, u8, idx, buf))]
     for name, fn in rows:
