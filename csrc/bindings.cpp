@@ -194,7 +194,9 @@ PYBIND11_MODULE(_C, m) {
                 inv_batch, P<float>(part)};
     if (role < 0) launch_fc_bwd(a, B, Bp, S(stream));
     else if (role == 3) launch_fc_bwd_dw1(a, B, Bp, S(stream));                  // role A alone, lean kernel
-    else if (role == 4) launch_fc_bwd(a, B, Bp, S(stream), false, false);       // roles C + B (B > 1024)
+    else if (role == 4) launch_fc_bwd(a, B, Bp, S(stream), false, FCB_ROLE_C | FCB_ROLE_B);   // B > 1024
+    else if (role == 5) launch_fc_bwd(a, B, Bp, S(stream), false, FCB_ROLE_C | FCB_ROLE_A);   // weight grads
+    else if (role == 6) launch_fc_bwd(a, B, Bp, S(stream), false, FCB_ROLE_B);
     else launch_fc_bwd_role(a, B, Bp, role, S(stream));
     check_launch();
   }, py::arg("dz1"), py::arg("p"), py::arg("pmask"), py::arg("w1t"), py::arg("h_bf"), py::arg("dl_bf"),

@@ -107,7 +107,10 @@ constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_P
                   FCB_PART_STRIDE = (FCB_PART_LOSS + 1 + 63) / 64 * 64;
 // reduce = false (B > 1024): the split partials are left for launch_fc_grad_reduce, which the
 // engine runs on the comm stream ahead of the fc all-reduce / update (off the compute chain)
-void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce = true, bool with_a = true);
+// fc_bwd workgroup roles (fc_head.hip): C = fc2 weight / bias gradient + loss, A = fc1 weight / bias
+// gradient, B = gradient into the conv trunk (compact dy records)
+constexpr int FCB_ROLE_C = 1, FCB_ROLE_A = 2, FCB_ROLE_B = 4, FCB_ROLES_ALL = 7;
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce = true, int roles = FCB_ROLES_ALL);
 // role A (fc1 weight gradient split partials) alone, for B > 1024 with reduce = false / with_a = false
 void launch_fc_bwd_dw1(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s);   // no-op for B <= 1024

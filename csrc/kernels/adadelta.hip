@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   Ada ad{a.rho, a.eps, a.weight_decay, UPDATE ? *a.lr : 0.0f};
   int bid = blockIdx.x;
-  if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (a.state_inc && !a.hold_a && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   if (a.signal_start && bid == 0 && threadIdx.x == 0)      // the previous launch on the stream is done
     __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   bool done = false;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * 72];
   __shared__ float4 red[256];
   int bid = blockIdx.x;
-  if (a.state_inc && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
+  if (a.state_inc && !a.hold_a && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   if (a.signal_start && bid == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   if (!conv_only) {
@@ -164,8 +164,13 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
   conv_reduce_update(a, c, B, bid + bid0, red);
   // single-GPU side-conv2 schedule: the step's last kernel completes only once the comm stream has
   // published this step's conv2 update, so the next trunk_fwd (stream order) reads the new weights
-  if (a.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+  // With a hold the step index advances after it: the comm stream's readers of this step's index
+  // (fc_bwd's role C writing loss_log[step] in the side-weight-gradient schedule) are ordered before
+  // the conv2 update that releases it.
+  if (a.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hold_err);
+    if (a.state_inc) a.state_inc->step += 1;
+  }
 }
 
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {

@@ -738,9 +738,10 @@ __host__ __device__ inline int fc_bwd_role_b_wgs(int B) {
 }
 
 // workgroups [C | A | B]; bid0 offsets a partial grid (launch_fc_bwd_role)
-// skip_a: roles C and B only (role A runs as fc_bwd_dw1_kernel on the comm stream)
+// roles: mask of FCB_ROLE_C / _A / _B; the grid covers the enabled roles' ranges in [C | A | B] order
+// (the side schedules split the launch: weight gradients on the comm stream, role B on compute)
 template <bool BIG>
-__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0, int skip_a) {
+__global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, int B, int Bp, int bid0, int roles) {
   TL_SCOPE(TL_FC_BWD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
@@ -748,7 +749,8 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
   const int S = fc_bwd_splits(B);
   const int nA = S * ROLE_A_WGS;
   int bid = blockIdx.x + bid0;
-  if (skip_a && bid >= S) bid += nA;
+  if (!(roles & FCB_ROLE_C)) bid += S;
+  if (!(roles & FCB_ROLE_A) && bid >= S) bid += nA;
   // role C (long-running, one per split) first so it is dispatched before the short role-B tiles
   if (bid < S) {
     fc_bwd_role_c(a, B, Bp, bid, S, smem);
@@ -808,15 +810,16 @@ void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(fc_grad_reduce_kernel, dim3((unsigned)((N4 + 255) / 256)), dim3(256), 0, s, a, B, S);
 }
 
-void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce, bool with_a) {
+void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce, int roles) {
   const int S = fc_bwd_splits(B);
   if (S > 1 && !a.part) throw std::runtime_error("fc_bwd: batch > 1024 needs the split-partial workspace");
-  if (!with_a && (S <= 1 || reduce))
-    throw std::runtime_error("fc_bwd: role A leaves the launch only for split partials reduced later");
-  const int grid = S + (with_a ? S * ROLE_A_WGS : 0) + fc_bwd_role_b_wgs(B);
-  const int skip = with_a ? 0 : 1;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, skip);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, skip);
+  if (roles <= 0 || roles > FCB_ROLES_ALL) throw std::runtime_error("fc_bwd: bad role mask");
+  if (roles != FCB_ROLES_ALL && S > 1 && reduce)
+    throw std::runtime_error("fc_bwd: a partial launch leaves the split partials for a later reduce");
+  const int grid = ((roles & FCB_ROLE_C) ? S : 0) + ((roles & FCB_ROLE_A) ? S * ROLE_A_WGS : 0) +
+                   ((roles & FCB_ROLE_B) ? fc_bwd_role_b_wgs(B) : 0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, roles);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, 0, roles);
   if (reduce) launch_fc_grad_reduce(a, B, s);
 }
 
@@ -832,8 +835,8 @@ void launch_fc_bwd_role(const FcBwdArgs& a, int B, int Bp, int role, hipStream_t
   const int nb = fc_bwd_role_b_wgs(B);
   const int grid = role == 0 ? S : role == 1 ? S * ROLE_A_WGS : nb;
   const int bid0 = role == 0 ? 0 : role == 1 ? S : S + S * ROLE_A_WGS;
-  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
-  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, 0);
+  if (fcb_mr(B) > 1) hipLaunchKernelGGL(fc_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, FCB_ROLES_ALL);
+  else hipLaunchKernelGGL(fc_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, a, B, Bp, bid0, FCB_ROLES_ALL);
 }
 
 TL_DEFINE_HOST(fc_head)

@@ -591,7 +591,8 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
     }
   }
   if (!xgmi_stage(a, 0, b, e, XGMI_K_CONV_FUSED)) return;
-  if (b == 0 && tid == 0 && a.ada.state_inc) a.ada.state_inc->step += 1;   // end-of-step marker
+  // end-of-step marker (with a wait: after it, so the comm stream's readers of the step index are done)
+  if (b == 0 && tid == 0 && a.ada.state_inc && !part.wait_a) a.ada.state_inc->step += 1;
   __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) src[p] = rsrc(a.stage[p] + slot, p == r ? 0 : bytes);   // own: registers
@@ -635,6 +636,7 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
         break;
       }
     }
+    if (a.ada.state_inc) a.ada.state_inc->step += 1;
   }
 }
 

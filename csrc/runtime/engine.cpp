@@ -80,6 +80,7 @@ void Engine::alloc_workspace() {
   sync_ = reinterpret_cast<int*>(base + L.sync);
   w2d_alt_ = reinterpret_cast<uint16_t*>(base + L.w2d_alt);
   c1red_ = reinterpret_cast<float*>(base + L.c1red);
+  w1t_alt_ = reinterpret_cast<uint16_t*>(base + L.w1t_alt);
 }
 
 void Engine::alloc_workspace_f32() {
@@ -168,7 +169,7 @@ void Engine::reset_counters() {
   // change or an aborted chunk they restart from zero, and so does the hand-off error flag [2]
   // (callers read it with check_errors before they get here)
   sync_streams();
-  launch_fill(sync_ + 0, 5 * sizeof(int), 0, compute_);
+  launch_fill(sync_ + 0, 6 * sizeof(int), 0, compute_);
   HIP_OK(hipStreamSynchronize(compute_));
   reset_host_state();
 }
@@ -274,13 +275,29 @@ void Engine::enqueue_step(int batch, bool last) {
   // comm stream's later launches (fc update, conv2 update) gate the next trunk_fwd / fc1_fwd.  Not
   // with the opt-in conv2 stream, whose conv2 update no longer queues behind it.
   const bool dw1_side = fc_reduce_side && fc_dw1_side_ && !c2s;
+  // OVERLAP / XGMI chain, B <= 1024: both fc weight gradients (roles C + A, 146 workgroups) leave the
+  // compute launch for the comm stream, released by fc_bwd's start (counter [5]: head_train done)
+  // instead of by wgrad's start, so the fc update (or fc all-reduce + update) that follows them
+  // starts ~wgrad's length earlier and the comm chain - conv2's reduce + update at its end gates the
+  // next trunk_fwd - finishes earlier.  The compute chain keeps role B (dy records) only.
+  const bool fcw_side = side && !c2s && !trace_ && (!xg || xgmi_fuse_update_) && fc_bwd_splits(B) == 1 &&
+                        fc_dw1_side_;
+  // [5] counts fc_bwd starts in every schedule that counts wgrad starts in [0] (lockstep with [1])
+  if (side || (sched_ == RCCL && two_buckets_)) fb.signal_ctr = sync_ + 5;
+  const int roles = fcw_side ? FCB_ROLE_B : dw1_side ? (FCB_ROLE_C | FCB_ROLE_B) : FCB_ROLES_ALL;
+  // ... so that fc update runs beside role B, which reads w1t: role B reads this step's copy while the
+  // update writes the other (ping-pong like w2d below; every element is rewritten each step)
+  uint16_t* const w1t_cur = w1t_in_alt_ ? w1t_alt_ : buf_.w1t;
+  uint16_t* const w1t_next = fcw_side ? (w1t_in_alt_ ? buf_.w1t : w1t_alt_) : w1t_cur;
+  fb.w1t = w1t_cur;
   phase_begin("bwd_fc");
-  if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side, !dw1_side);
+  if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side, roles);
   phase_end();
 
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
-                  buf_.w2f, buf_.w2d, buf_.w1, buf_.w1t, nullptr};
+                  buf_.w2f, buf_.w2d, buf_.w1, w1t_next, nullptr};
   ad.wt = B <= WT_MAX_B;                          // write-through stores at small batches (store16)
+  if (fcw_side) w1t_in_alt_ = !w1t_in_alt_;
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
@@ -394,11 +411,17 @@ void Engine::enqueue_step(int batch, bool last) {
   const bool chain = !trace_ && (!xg || xgmi_fuse_update_) && !c2s;
   phase_begin("allreduce_fc+update");
   if (S) {
+    int* const rel = fcw_side ? sync_ + 5 : sync_ + 0;   // fc_bwd's start / wgrad's start
     if (chain && comm_sig3_pending_)
-      launch_stream_signal_wait(sync_ + 3, sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+      launch_stream_signal_wait(sync_ + 3, rel, sync_ + 1, 1, sync_ + 2, comm_stream_);
     else
-      launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
+      launch_stream_wait(rel, sync_ + 1, 1, sync_ + 2, comm_stream_);
     comm_sig3_pending_ = false;
+    if (fcw_side) {
+      FcBwdArgs fw = fb;
+      fw.signal_ctr = nullptr;
+      launch_fc_bwd(fw, B, Bp, comm_stream_, true, FCB_ROLE_C | FCB_ROLE_A);
+    }
     if (dw1_side) launch_fc_bwd_dw1(fb, B, Bp, comm_stream_);
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     if (!xg) {
@@ -496,6 +519,12 @@ void Engine::enqueue_step(int batch, bool last) {
     }
     phase_end();
     w2d_in_alt_ = !w2d_in_alt_;
+    if (last && w1t_in_alt_) {                  // after the conv1 part: the fc update is published
+      if (M)
+        HIP_OK(hipMemcpyAsync(buf_.w1t, w1t_alt_, (size_t)NFLAT * NH * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                              compute_));
+      w1t_in_alt_ = false;
+    }
     if (last && w2d_in_alt_) {
       if (M)
         HIP_OK(hipMemcpyAsync(buf_.w2d, w2d_alt_, (size_t)9 * C1 * C2 * sizeof(uint16_t), hipMemcpyDeviceToDevice,
@@ -665,6 +694,7 @@ void Engine::reset_host_state() {
   side_pending_ = false;
   side_forked_ = false;
   w2d_in_alt_ = false;
+  w1t_in_alt_ = false;
 }
 
 // OVERLAP / XGMI chunks as TWO graphs: the side chain (comm stream: per step counter waits, the fc
@@ -677,12 +707,13 @@ void Engine::reset_host_state() {
 // read 93-97 us/step against 73.5 steady state.  The fork (chunk start -> comm stream) and the join
 // (comm stream -> compute) become two events at replay.
 int Engine::capture_train_split(int n, int batch) {
-  const bool sp = side_pending_, w2 = w2d_in_alt_;
+  const bool sp = side_pending_, w2 = w2d_in_alt_, w1 = w1t_in_alt_;
   const bool c2s = use_conv2_stream();        // a third pass: the conv2 stream's chain
   hipGraph_t gs = nullptr, gm = nullptr, g2 = nullptr;
   auto pass = [&](hipStream_t s, bool m, bool side, bool c2, hipGraph_t* out) {
     side_pending_ = sp;
     w2d_in_alt_ = w2;
+    w1t_in_alt_ = w1;
     comm_sig3_pending_ = false;
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;

@@ -91,7 +91,9 @@ class Engine {
   // the compute / comm streams on distinct hardware queues: probe_stream_handoff); off = the update
   // before the join (graph edges only)
   void set_rccl_handoff(bool on) { rccl_handoff_ = on; }
-  // B > 1024 side schedules: fc_bwd's role A (fc1 weight gradient) on the comm stream (default on)
+  // side schedules: fc_bwd's weight-gradient roles on the comm stream (default on): role A alone for
+  // B > 1024 (lean kernel ahead of the split reduce), roles C + A for B <= 1024 in the chained OVERLAP /
+  // XGMI schedules (released by fc_bwd's start)
   void set_fc_dw1_side(bool on) { fc_dw1_side_ = on; }
   bool fc_dw1_side() const { return fc_dw1_side_; }
   // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
@@ -181,7 +183,8 @@ class Engine {
   bool side_forked_ = false;        // comm stream already ordered after this chunk's start
   bool comm_sig3_pending_ = false;  // OVERLAP chain: the last conv2 update's [3] signal is owed
   int* sync_ = nullptr;             // [0] wgrad starts (fc grads final), [1] fc updates done, [2] error,
-                                    // [3] conv2 updates done, [4] dgrad starts, [8..11] probe scratch,
+                                    // [3] conv2 updates done, [4] dgrad starts, [5] fc_bwd starts,
+                                    // [8..11] probe scratch,
                                     // [12..15] fault-injection hold
   hipStream_t conv2_stream_ = nullptr;       // set_conv2_stream
   // split capture: which stream's pass enqueue_step feeds (main = compute, side = comm, c2 = conv2)
@@ -211,6 +214,9 @@ class Engine {
   float* c1red_ = nullptr;          // conv1 partial group sums (large batches)
   uint16_t* w2d_alt_ = nullptr;     // second dgrad-layout conv2 shadow (conv2 update on the comm stream)
   bool w2d_in_alt_ = false;         // enqueue-time: the current w2d lives in w2d_alt_
+  uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (side fc weight gradients: the fc
+                                    // update of step k runs beside fc_bwd role B, which reads w1t)
+  bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
   hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr, ev_done2_ = nullptr;
   // workspace
   int64_t ws_bytes_ = 0;

@@ -31,7 +31,8 @@ constexpr float kDdpEpilogueScale = 1.0f;
 
 // ---------------------------------------------------------------------------- engine workspace
 struct WorkspaceLayout {
-  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w2d_alt, c1red;
+  int64_t a1, p, pmask, z1part, loss_rows, dz1, h_bf, dl_bf, dyc, c1part, w2part, fcpart, sync, w2d_alt, c1red,
+      w1t_alt;
   int64_t total;   // bytes
 };
 
@@ -65,6 +66,7 @@ inline WorkspaceLayout compute_workspace_layout(int max_batch, int max_test_batc
   L.sync = carve(256);                                                                // hand-off counters
   L.w2d_alt = carve((int64_t)9 * C1 * C2 * 2);                                         // alternate w2d
   L.c1red = carve((int64_t)C1_PRE_SLABS * 320 * 4);                                    // conv1 group sums
+  L.w1t_alt = carve((int64_t)NFLAT * NH * 2);                                          // alternate w1t
   L.total = off;
   return L;
 }
