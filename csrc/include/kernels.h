@@ -111,6 +111,9 @@ constexpr int64_t FCB_PART_W1 = 0, FCB_PART_B1 = 128 * 9216, FCB_PART_W2 = FCB_P
 // gradient, B = gradient into the conv trunk (compact dy records)
 constexpr int FCB_ROLE_C = 1, FCB_ROLE_A = 2, FCB_ROLE_B = 4, FCB_ROLES_ALL = 7;
 void launch_fc_bwd(const FcBwdArgs& a, int B, int Bp, hipStream_t s, bool reduce = true, int roles = FCB_ROLES_ALL);
+struct AdadeltaArgs;
+// roles C + A with the fc Adadelta step fused (one split; single-GPU OVERLAP chain)
+void launch_fc_wgrad_update(const FcBwdArgs& a, const AdadeltaArgs& u, int B, int Bp, hipStream_t s);
 // role A (fc1 weight gradient split partials) alone, for B > 1024 with reduce = false / with_a = false
 void launch_fc_bwd_dw1(const FcBwdArgs& a, int B, int Bp, hipStream_t s);
 void launch_fc_grad_reduce(const FcBwdArgs& a, int B, hipStream_t s);   // no-op for B <= 1024

@@ -451,13 +451,85 @@ __device__ __forceinline__ int swz_row128(int row, int col) {   // 64 bf16 per r
 }
 constexpr int ROLE_B_SBLOCKS = NPOOL / 4;    // 36 blocks of 4 pooled positions (one third of a row)
 
+// Adadelta step of one element whose gradient g is final (fc1 bias, fc2): grad buffer, param, state
+__device__ __forceinline__ void ada_elem(const AdadeltaArgs& u, const Ada& ad, int64_t e, float g) {
+  float p = u.param[e], sq = u.square_avg[e], ac = u.acc_delta[e];
+  const_cast<float*>(u.grad)[e] = g;               // (the engine grad buffer, = FcBwdArgs::grad)
+  ad.step(p, g, sq, ac);
+  u.param[e] = p;
+  u.square_avg[e] = sq;
+  u.acc_delta[e] = ac;
+}
+
+// fused update epilogue of a role-A tile (grad_scale 1: the engine's head carries 1/B); acc[mt][nt]:
+// lane (l & 15, g) of wave w holds columns i0 + 16 nt + 4 g + r of row o = 32 w + 16 mt + (l & 15)
+__device__ __forceinline__ void fc_role_a_update(const AdadeltaArgs& u, const floatx4 (&acc)[2][4], bool ones, int i0,
+                                                 unsigned char* smem) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
+  const Ada ad{u.rho, u.eps, u.weight_decay, *u.lr};
+  if (ones) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((lane & 15) == 0) ada_elem(u, ad, OFF_FC1_B + 32 * wave + 16 * mt + 4 * g + r, acc[mt][0][r]);
+    return;
+  }
+  constexpr int TR = 72, TT = 136;                     // padded LDS rows: w1 tile [128 o][64 i], w1t [64 i][128 o]
+  uint16_t* tr = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* tt = reinterpret_cast<uint16_t*>(smem + 128 * TR * 2);
+  __syncthreads();                                     // every wave's last MFMA operand reads are done
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int ol = 32 * wave + 16 * mt + (lane & 15);
+    float4 pp[4], sq[4], ac[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {                   // all loads of the half-tile first
+      const int64_t e = OFF_FC1_W + (int64_t)ol * NFLAT + i0 + 16 * nt + 4 * g;
+      pp[nt] = *reinterpret_cast<const float4*>(u.param + e);
+      sq[nt] = *reinterpret_cast<const float4*>(u.square_avg + e);
+      ac[nt] = *reinterpret_cast<const float4*>(u.acc_delta + e);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int il = 16 * nt + 4 * g;
+      const int64_t e = OFF_FC1_W + (int64_t)ol * NFLAT + i0 + il;
+      const floatx4 gv = acc[mt][nt];
+      store16(u.wt, u.grad, e * 4, gv);
+      ad.step(pp[nt].x, gv[0], sq[nt].x, ac[nt].x);
+      ad.step(pp[nt].y, gv[1], sq[nt].y, ac[nt].y);
+      ad.step(pp[nt].z, gv[2], sq[nt].z, ac[nt].z);
+      ad.step(pp[nt].w, gv[3], sq[nt].w, ac[nt].w);
+      store16(u.wt, u.param, e * 4, make_floatx4(pp[nt]));
+      store16(u.wt, u.square_avg, e * 4, make_floatx4(sq[nt]));
+      store16(u.wt, u.acc_delta, e * 4, make_floatx4(ac[nt]));
+      const float v[4] = {pp[nt].x, pp[nt].y, pp[nt].z, pp[nt].w};
+      *reinterpret_cast<uint2*>(tr + ol * TR + il) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tt[(il + r) * TT + ol] = f2bf(v[r]);
+    }
+  }
+  lds_barrier();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {                        // w1: 128 rows x 128 B, w1t: 64 rows x 256 B
+    const int c = tid + 256 * k;
+    const int o = c >> 3, ic = (c & 7) * 8;
+    store16(u.wt, u.w1, ((int64_t)o * NFLAT + i0 + ic) * 2, *reinterpret_cast<const uint4*>(tr + o * TR + ic));
+    const int il = c >> 4, oc = (c & 15) * 8;
+    store16(u.wt, u.w1t, ((int64_t)(i0 + il) * NH + oc) * 2, *reinterpret_cast<const uint4*>(tt + il * TT + oc));
+  }
+}
+
 // A: dW_fc1 tile [128 o][64 i] over K = batch.  Register-prefetch pipeline: the next 32-row k-slab is
 // loaded into VGPRs while the current one feeds the MFMAs.  DB: double-buffered LDS (24 KB), one
 // barrier per slab; !DB: one 12-KB buffer and a second barrier (fc_bwd_dw1_kernel, which must fit
 // beside two conv2_dgrad workgroups' 140 KB of LDS).  The same MFMA order either way.
-template <bool DB = true>
+// UPD (single GPU, S == 1, fc_wgrad_update_kernel): the epilogue also applies the Adadelta step to the
+// tile (gradient -> grad buffer, param / square_avg / acc_delta, bf16 shadows w1 and w1t staged through
+// LDS for 16-B stores) - per element the same math as adadelta_kernel's fc1_tile, so the same bits.
+template <bool DB = true, bool UPD = false>
 __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp, int ib, int sp, int S,
-                                              unsigned char* smem) {
+                                              unsigned char* smem, const AdadeltaArgs* up = nullptr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const bool ones = (ib == NFLAT / 64);
@@ -523,6 +595,10 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
   // S > 1: unscaled partial in the same layout (fc_grad_reduce)
   float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
   const float sc = (S == 1) ? a.grad_scale : 1.0f;
+  if constexpr (UPD) {
+    fc_role_a_update(*up, acc, ones, i0, smem);
+    return;
+  }
   if (ones) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -652,8 +728,9 @@ __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp,
   }
 }
 
+template <bool UPD = false>
 __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp, int sp, int S,
-                                              unsigned char* smem) {
+                                              unsigned char* smem, const AdadeltaArgs* up = nullptr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem + wave * 9216);          // [32][128]
@@ -714,7 +791,11 @@ __device__ __forceinline__ void fc_bwd_role_c(const FcBwdArgs& a, int B, int Bp,
     float* dst = (S == 1) ? a.grad : a.part + (int64_t)sp * FCB_PART_STRIDE;
     const float sc = (S == 1) ? a.grad_scale : 1.0f;
     const int64_t k = (c >= NCLS) ? -1 : (nt < 8) ? OFF_FC2_W + c * NH + 16 * nt + col : (col == 0) ? OFF_FC2_B + c : -1;
-    if (k >= 0) dst[k] = s * sc;
+    if constexpr (UPD) {
+      if (k >= 0) ada_elem(*up, Ada{up->rho, up->eps, up->weight_decay, *up->lr}, k, s * sc);
+    } else {
+      if (k >= 0) dst[k] = s * sc;
+    }
   }
   if (wave == 0) {
     const int b_lo = sp * FC_BWD_SPLIT_ROWS, b_hi = min(B, b_lo + FC_BWD_SPLIT_ROWS);
@@ -772,6 +853,27 @@ __global__ __launch_bounds__(256, 6) void fc_bwd_dw1_kernel(FcBwdArgs a, int B, 
   const int S = fc_bwd_splits(B);
   const int r = blockIdx.x;
   fc_bwd_role_a<false>(a, B, Bp, r % ROLE_A_WGS, r / ROLE_A_WGS, S, smem);
+}
+
+// Single-GPU OVERLAP chain, B <= 1024 (one split): the fc weight gradients (roles C + A, 146
+// workgroups) with the fc Adadelta step fused into their epilogues, on the comm stream beside fc_bwd's
+// role B and the conv backward - one launch instead of the gradient launch + adadelta_kernel(ADA_FC),
+// no gradient round trip, each tile updated as soon as its gradient is final.  The completion hold
+// (u.hold_*) is adadelta_kernel's: the conv2 update that follows on the stream starts after dgrad's start.
+__global__ __launch_bounds__(256, 2) void fc_wgrad_update_kernel(FcBwdArgs a, AdadeltaArgs u, int B, int Bp) {
+  TL_SCOPE(TL_ADA_FC);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
+  if (blockIdx.x == 0) fc_bwd_role_c<true>(a, B, Bp, 0, 1, smem, &u);
+  else fc_bwd_role_a<true, true>(a, B, Bp, blockIdx.x - 1, 0, 1, smem, &u);
+  if (u.hold_a && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    spin_until_geq(u.hold_a, __hip_atomic_load(u.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + u.hold_delta,
+                   u.hold_err);
+}
+
+void launch_fc_wgrad_update(const FcBwdArgs& a, const AdadeltaArgs& u, int B, int Bp, hipStream_t s) {
+  if (fc_bwd_splits(B) != 1 || a.grad_scale != 1.0f || u.grad != a.grad || u.state_inc || u.signal_start)
+    throw std::runtime_error("fc_wgrad_update: one split, unit grad scale, the engine's grad buffer");
+  hipLaunchKernelGGL(fc_wgrad_update_kernel, dim3(1 + ROLE_A_WGS), dim3(256), 0, s, a, u, B, Bp);
 }
 
 // S > 1: fixed-order sum of the split partials (fc1.w, fc1.b, fc2.w, fc2.b share the grad layout

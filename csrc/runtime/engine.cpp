@@ -417,11 +417,9 @@ void Engine::enqueue_step(int batch, bool last) {
     else
       launch_stream_wait(rel, sync_ + 1, 1, sync_ + 2, comm_stream_);
     comm_sig3_pending_ = false;
-    if (fcw_side) {
-      FcBwdArgs fw = fb;
-      fw.signal_ctr = nullptr;
-      launch_fc_bwd(fw, B, Bp, comm_stream_, true, FCB_ROLE_C | FCB_ROLE_A);
-    }
+    FcBwdArgs fw = fb;
+    fw.signal_ctr = nullptr;
+    if (fcw_side && xg) launch_fc_bwd(fw, B, Bp, comm_stream_, true, FCB_ROLE_C | FCB_ROLE_A);
     if (dw1_side) launch_fc_bwd_dw1(fb, B, Bp, comm_stream_);
     if (fc_reduce_side) launch_fc_grad_reduce(fb, B, comm_stream_);
     if (!xg) {
@@ -435,7 +433,11 @@ void Engine::enqueue_step(int batch, bool last) {
       // 144 workgroups instead of 577: the update has ~15 us of slack before the next step's trunk
       // ends, and fewer co-resident waves leave wgrad / dgrad more of the CUs (600 steps, two boxes:
       // 65.9 -> 65.2, 65.0-65.7 -> 64.4-64.9 us/step; 96 / 64 workgroups: 67.6 / 74-75)
-      launch_adadelta(af, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
+      // Side weight gradients: the update is fused into their 146 workgroups (one launch).
+      if (fcw_side)
+        launch_fc_wgrad_update(fw, af, B, Bp, comm_stream_);
+      else
+        launch_adadelta(af, ADA_FC, comm_stream_, ADA_FC_LEAN_GRID);
     } else if (xgmi_fuse_update_) {             // fc bucket all-reduce with the fc Adadelta step fused
       AdadeltaArgs af = ad;
       if (chain) {                              // completes once this step's dgrad has started

@@ -15,3 +15,6 @@ for v in 0 1; do
   MNIST_AMD_FC_DW1_SIDE=$v timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-full-run > $O/s20_$v.log 2>&1 || exit 1
 done
 for f in $O/s*.log; do echo "$(basename $f) $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+if [ "$3" = timeline ]; then
+  timeout -k 10 200 python tools/timeline_tl.py --batch 200 --steps 300 --graph-steps 50 --out $O/timeline_on.md > $O/tl_on.log 2>&1 || exit 1
+fi
