@@ -321,7 +321,11 @@ void launch_xgmi_allreduce_oneshot(const XgmiArgs& a, hipStream_t s) {
 // result is bitwise that of the all-reduce + separate update it replaces.  Registers and LDS are kept
 // at the single-GPU update's scale (one unit per pass at W <= 2, 4.6 KB of LDS) so the kernel fits
 // beside the persistent conv2_dgrad's workgroups (2 x 216 VGPRs per SIMD, 150 KB of LDS per CU) -
-// at 103 VGPRs it did not, and dgrad ran 2 us longer beside it (world-1 in-kernel timeline).
+// at 103 VGPRs it did not, and dgrad ran 2 us longer beside it (world-1 in-kernel timeline).  Every
+// world size is held to <= 80 VGPRs (6 waves per SIMD: beside dgrad's 2 x 216 and wgrad's 2 x 208):
+// one phase-2 unit in flight per lane and phase-1 peer loads in groups of 4 (W = 4..8 reached
+// 106-113 VGPRs with two phase-2 units in flight, so at N >= 4 the fc branch could not co-run with
+// the conv backward at all).
 namespace {
 constexpr int FCU_TILES = 2 * (NFLAT / 32);                      // 576
 constexpr int FCU_UNITS = FCU_TILES + 1;                         // + tail
@@ -392,9 +396,9 @@ __device__ __forceinline__ void fcu_update(const XgmiArgs& a, const Ada& ad, int
 }  // namespace
 
 template <int W>
-__global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
+__global__ __launch_bounds__(256, 6) void xgmi_fc_fused_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_FC);
-  constexpr int PG = W >= 4 ? 2 : 1;                             // phase-2 units in flight per lane
+  constexpr int PG = 1;                                          // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * FCU_TS];
   const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
@@ -436,15 +440,19 @@ __global__ __launch_bounds__(256) void xgmi_fc_fused_kernel(XgmiArgs a) {
 #pragma unroll
           for (int p = 1; p < W; ++p) g[h] += v[h][p];
         }
-      } else {                                                   // one half's W loads at a time
+      } else {                                                   // one half's loads at a time, in
+#pragma unroll                                                   // groups of <= 4 peers (the rank-order
+        for (int h = 0; h < 2; ++h) {                            // sum is unchanged; <= 80 VGPRs at W = 8)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f4 v[W];
+          for (int p0 = 0; p0 < W; p0 += 4) {
+            f4 v[4];
 #pragma unroll
-          for (int p = 0; p < W; ++p) v[p] = ld_sys(in[p], q[h] < 0 ? a.nvec : q[h]);
-          g[h] = v[0];
+            for (int k = 0; k < 4; ++k)
+              if (p0 + k < W) v[k] = ld_sys(in[p0 + k], q[h] < 0 ? a.nvec : q[h]);
 #pragma unroll
-          for (int p = 1; p < W; ++p) g[h] += v[p];
+            for (int k = 0; k < 4; ++k)
+              if (p0 + k < W) g[h] = (p0 + k == 0) ? v[0] : g[h] + v[k];
+          }
         }
       }
 #pragma unroll
