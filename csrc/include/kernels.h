@@ -141,6 +141,7 @@ struct ConvBwdArgs {
   // 20 reduce workgroups walking 4B slabs is a dependent-load chain, 81 us at B = 8192)
   float* c1red;
   int c1_rows;                // conv1 partial rows the dgrad launch writes: conv_dgrad_c1_rows(B)
+  int dgrad_full_grid;        // 1: persistent dgrad on 2 x CUs workgroups; 0: the equal-count grid
 };
 // 4B: 4 strips of 7 rows per image, items of the persistent dgrad (2 workgroups per CU)
 int conv_dgrad_c1_rows(int B);

@@ -458,7 +458,7 @@ int conv_dgrad_c1_rows(int B) { return 4 * B; }
 // epilogue, 0.980 vs 1.062 ms/step).  set_dgrad_grid(n > 0) overrides it (tests: ragged item rounds).
 static int g_dgrad_grid_override = 0;
 void set_dgrad_grid(int n) { g_dgrad_grid_override = n > 0 ? n : 0; }
-static int dgrad_persist_grid(int B) {
+static int dgrad_persist_grid(int B, bool full) {
   int g = g_dgrad_grid_override;
   if (g <= 0) {
     static int cus = 0;
@@ -467,7 +467,15 @@ static int dgrad_persist_grid(int B) {
       if (hipGetDevice(&dev) != hipSuccess) dev = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
-    g = 2 * cus;
+    // equal item counts: as many rounds as 2 x CUs workgroups need, spread over the fewest workgroups
+    // that keep that round count (B = 200: 800 items on 400 workgroups instead of 512 with 288 doing
+    // two; the CUs left free run the comm stream's conv2 reduce + update, whose waves do not fit beside
+    // two dgrad workgroups: 600 steps 63.3 -> 62.6 us/step; 448 / 360 / 320 / 272: 62.9 / 64.2 /
+    // 65.1 / 65.4, profiles/r5/ab/dgrad_grid.txt).  B = 8192: 64 rounds of 512 either way.
+    // The DDP schedules keep 2 x CUs (ConvBwdArgs::dgrad_full_grid: world-1 XGMI 68.6-68.8 us/step
+    // with it, 69.5-71.5 with the equal-count grid - its conv2 part is the 124-VGPR xGMI kernel).
+    const int n = 4 * B, g2 = 2 * cus, rounds = (n + g2 - 1) / g2;
+    g = full ? g2 : (n + rounds - 1) / rounds;
   }
   return g < 4 * B ? g : 4 * B;
 }
@@ -878,7 +886,7 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s) {
 
 void launch_conv_dgrad(const ConvBwdArgs& a, int B, hipStream_t s) {
   if (a.c1_rows != 4 * B) throw std::runtime_error("conv_dgrad: c1_rows must be conv_dgrad_c1_rows(B)");
-  const dim3 g(dgrad_persist_grid(B));
+  const dim3 g(dgrad_persist_grid(B, a.dgrad_full_grid != 0));
   if (a.xin)
     hipLaunchKernelGGL((conv2_dgrad_persist_kernel<DGX_XIN>), g, dim3(256), 0, s, a, B);
   else if (a.idx)

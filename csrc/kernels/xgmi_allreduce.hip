@@ -396,7 +396,7 @@ __device__ __forceinline__ void fcu_update(const XgmiArgs& a, const Ada& ad, int
 }  // namespace
 
 template <int W>
-__global__ __launch_bounds__(256, 6) void xgmi_fc_fused_kernel(XgmiArgs a) {
+__global__ __launch_bounds__(256, W >= 4 ? 6 : 1) void xgmi_fc_fused_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_FC);
   constexpr int PG = 1;                                          // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;

@@ -303,6 +303,7 @@ void Engine::enqueue_step(int batch, bool last) {
                  conv_wgrad_groups(B), nullptr};
   cb.c1_rows = conv_dgrad_c1_rows(B);
   if (cb.c1_rows > C1_PRE_MIN_SLABS) cb.c1red = c1red_;   // large batch: conv1 partials pre-reduced
+  cb.dgrad_full_grid = sched_ == OVERLAP || sched_ == SERIAL ? 0 : 1;
   AdadeltaArgs adc = ad;
   adc.state_inc = buf_.state;   // last kernel of the step advances the device step counter
 

@@ -206,6 +206,8 @@ class FusedTrainer:
         # B > 1024, side schedules: fc_bwd's fc1 weight gradient on the comm stream beside the conv
         # backward (MNIST_AMD_FC_DW1_SIDE=0: in the compute-stream fc_bwd launch, for A/B)
         self.engine.fc_dw1_side = os.environ.get("MNIST_AMD_FC_DW1_SIDE", "1") != "0"
+        if os.environ.get("MNIST_AMD_DGRAD_GRID"):     # A/B only: persistent dgrad grid (0 = 2 x CUs)
+            C.set_dgrad_grid(int(os.environ["MNIST_AMD_DGRAD_GRID"]))
         self._graphs: dict[tuple[int, int], int] = {}        # captured chunks of the selected schedule
         self._graph_sets: dict[str, dict] = {}               # per transport (validation captures)
         self._eval_graph: int | None = None
