@@ -46,7 +46,7 @@ static void test_workspace() {
           {L.w2part, (int64_t)wgrad_groups(B) * (18432 + 64) * 4},
           {L.fcpart, fc_bwd_splits(B) > 1 ? (int64_t)fc_bwd_splits(B) * FCB_PART_STRIDE * 4 : 4},
           {L.sync, 64},                           {L.w2d_alt, 9LL * C1 * C2 * 2},
-          {L.c1red, (int64_t)C1_PRE_SLABS * 320 * 4}};
+          {L.c1red, (int64_t)C1_PRE_SLABS * 320 * 4}, {L.w1t_alt, (int64_t)NFLAT * NH * 2}};
       std::sort(bufs.begin(), bufs.end());
       int64_t end = 0;
       for (auto& b : bufs) {
