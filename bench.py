@@ -198,9 +198,13 @@ def parse_args(argv=None):
                     help="attach the RCCL communicator even at world_size 1 (exercises the DDP schedule)")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
                     help="bf16: the bf16-MFMA step (default); fp32: the fp32 step (f32_net.hip; RCCL or xGMI at N > 1)")
-    ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
-                    help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernels, or "
-                         "auto (validate and time both production schedules at startup, keep the faster)")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi", "fastest"],
+                    default=os.environ.get("MNIST_AMD_ALLREDUCE", "auto"),
+                    help="DDP gradient all-reduce: RCCL, the direct xGMI reduce-scatter/all-gather kernels, auto "
+                         "(xGMI when its production schedule validates on one node; RCCL only as the fallback, "
+                         "never waited for otherwise) or fastest (validate and time both, keep the faster)")
+    ap.add_argument("--hook", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine variant for A/B runs (FusedTrainer.HOOKS: fc_dw1_side=0|1, dgrad_grid=N)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (gloo + --allreduce xgmi: no RCCL, e.g. MNIST_AMD_ONE_GPU=1 rehearsals)")
     ap.add_argument("--cpu", action="store_true", help="reference CPU config (mnist.py --no-cuda, batch 64)")
@@ -272,6 +276,7 @@ class Diag:
         self.phase = "start"
         self.phases = PhaseTimes()
         self.tr = None
+        self.pending = None           # the PendingRcclComm, if any
 
     def record(self, exc: BaseException) -> dict:
         if getattr(exc, "setup", None) is not None:       # the trainer's phases up to the failure
@@ -336,11 +341,16 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
             # lazy (no device_id): ProcessGroupNCCL never builds a communicator - the engine's all-reduce
             # runs on its own RCCL communicator or the xGMI kernels, verdicts over the TCPStore
             dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank)
-        if args.allreduce != "xgmi":       # the RCCL communicator initialises while data / model build
+        if args.allreduce != "xgmi":
+            # the RCCL communicator (as the driver): rccl / fastest start its non-blocking init now, while
+            # data and model build; auto on one node defers it - the trainer starts it only if xGMI fails
+            eager = args.allreduce != "auto" or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != world
             with phases.phase("rccl_comm_start"):
-                pending = start_rccl_comm(world, rank, local)
+                pending = start_rccl_comm(world, rank, local, start=eager)
+    diag.pending = pending
     xgmi_pending = streams = None
-    if world > 1 and args.allreduce != "rccl":   # so does the xGMI communicator (helper thread)
+    probe_world1 = world == 1 and use_pg and args.allreduce in ("auto", "fastest")
+    if (world > 1 or probe_world1) and args.allreduce != "rccl":   # the xGMI communicator (helper thread)
         from pytorch_mnist_ddp_amd.engine.trainer import make_streams
         from pytorch_mnist_ddp_amd.ops import native
         from pytorch_mnist_ddp_amd.parallel.distributed import PendingXgmiComm
@@ -360,18 +370,15 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
         steps_per_epoch = math.ceil(len(sampler) / B)
         num_samples = max(total * B, steps_per_epoch * B)
         ms = ModelState(net, dev, lr=1.0)
-    comm = None
-    if pending is not None:
-        diag.phase = "rccl_comm"
-        with phases.phase("rccl_comm_wait"):
-            comm = pending.result()
-        phases.add_info("rccl_comm_init_thread_s", pending.seconds)
     diag.phase = "trainer"
     t_tr = time.perf_counter()
+    hooks = dict(h.split("=", 1) for h in args.hook)
     tr = FusedTrainer(ms, train, test, B, 1000, num_samples=num_samples, world_size=world, rank=rank,
-                      comm=comm, seed=args.seed, graph_steps=args.graph_steps,
+                      seed=args.seed, graph_steps=args.graph_steps,
                       two_buckets=not args.single_bucket, allreduce=args.allreduce,
-                      fp32=args.dtype == "fp32", xgmi_pending=xgmi_pending, streams=streams)
+                      fp32=args.dtype == "fp32", xgmi_pending=xgmi_pending, streams=streams,
+                      rccl_pending=pending, probe_world1=probe_world1, hooks=hooks)
+    comm = tr.comm
     diag.tr = tr
     phases.add("trainer", time.perf_counter() - t_tr)
 
@@ -432,6 +439,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                  "rccl_world": comm.world_size if comm is not None else None,
                  "rccl_comms": 1 if comm is not None else 0,
                  "rccl_aborted": bool(comm.aborted) if comm is not None else None,
+                 "rccl_init": pending.status if pending is not None else None,
+                 "hooks": hooks or None,
                  "allreduce_schedule_us": tr.allreduce_timings or None,
                  "transport_report": tr.transport_report or None,
                  "xgmi_validation": tr.xgmi_validation,
@@ -440,6 +449,14 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                                 if tr.xgmi is not None else None),
                  "schedule": ["serial", "overlap", "rccl", "xgmi"][tr.engine.schedule]}
     phases.update(tr.setup, prefix="trainer.")
+    # bimodal-slowdown guard (docs/DEBUGGING.md): the timed window against the same schedule's startup
+    # validation replay (max over ranks, dropout off); > 1.25x flags a slow mode loudly
+    sched_us = tr.allreduce_timings.get(tr.allreduce) if tr.allreduce else None
+    slowdown = round(1e6 * elapsed / args.steps / sched_us, 3) if sched_us else None
+    if slowdown is not None and slowdown > 1.25 and rank == 0:
+        print(f"bench.py: SLOW MODE - {1e6 * elapsed / args.steps:.1f} us/step is {slowdown}x the {tr.allreduce} "
+              f"schedule's validation replay ({sched_us} us/step)", file=sys.stderr, flush=True)
+    comm_info.update(schedule_slowdown=slowdown, slow_mode=bool(slowdown is not None and slowdown > 1.25))
 
     # ---- the README workload end to end: 20 epochs train + rank-0 eval, fresh model, on the SAME
     # trainer (engine, graphs, communicators, transport choice and validation reused, state reset)
@@ -618,6 +635,8 @@ def main(argv=None) -> int:
             sys.stderr.flush()
             os._exit(3)
         rc = 1
+    if getattr(diag, "pending", None) is not None:
+        diag.pending.close(30.0)      # a cancelled / unused RCCL init's helper thread
     if use_pg and dist.is_initialized():
         try:
             if rc == 0:

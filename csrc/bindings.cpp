@@ -233,7 +233,7 @@ PYBIND11_MODULE(_C, m) {
 
   // ---------------- communicator ----------------
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
-      .def(py::init([](py::bytes uid, int world, int rank, int device, double init_timeout_s) {
+      .def(py::init([](py::bytes uid, int world, int rank, int device, double init_timeout_s, bool wait) {
              std::string s = uid;
              std::shared_ptr<RcclComm> c;
              {
@@ -241,12 +241,12 @@ PYBIND11_MODULE(_C, m) {
                // (distributed.PendingRcclComm overlaps it with data / model / trainer setup)
                py::gil_scoped_release nogil;
                c = std::make_shared<RcclComm>(std::vector<uint8_t>(s.begin(), s.end()), world, rank, device,
-                                              init_timeout_s);
+                                              init_timeout_s, wait);
              }
              return c;
            }),
            py::arg("unique_id"), py::arg("world_size"), py::arg("rank"), py::arg("device"),
-           py::arg("init_timeout_s") = 600.0)
+           py::arg("init_timeout_s") = 600.0, py::arg("wait") = true)
       .def("abort", [](RcclComm& c) {
         py::gil_scoped_release nogil;
         c.abort();
@@ -254,6 +254,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("nonblocking", &RcclComm::nonblocking)
       .def("async_error", &RcclComm::async_error)
+      .def("init_status", &RcclComm::init_status, py::call_guard<py::gil_scoped_release>())
+      .def_static("error_string", &RcclComm::error_string)
       .def_static("available", &RcclComm::available)
       .def_static("version", &RcclComm::version)
       .def_static("unique_id", []() {
@@ -365,6 +367,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_bucket_split", &Engine::set_bucket_split)
       .def("set_rccl_handoff", &Engine::set_rccl_handoff)
       .def_property("fc_dw1_side", &Engine::fc_dw1_side, &Engine::set_fc_dw1_side)
+      .def_property("w1t_pingpong", &Engine::w1t_pingpong, &Engine::set_w1t_pingpong)
       .def("fault_hold", &Engine::fault_hold)
       .def("fault_release", [](Engine& e, uintptr_t stream) { e.fault_release(S(stream)); })
       .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())
@@ -372,10 +375,6 @@ PYBIND11_MODULE(_C, m) {
       .def("reset_counters", &Engine::reset_counters, py::call_guard<py::gil_scoped_release>())
       .def("probe_stream_handoff", &Engine::probe_stream_handoff, py::arg("timeout_s") = 2.0,
            py::call_guard<py::gil_scoped_release>())
-      .def("set_conv2_stream", [](Engine& e, uintptr_t stream, double timeout_s) {
-             return e.set_conv2_stream(S(stream), timeout_s);
-           }, py::arg("stream"), py::arg("timeout_s") = 2.0, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("conv2_stream_on", &Engine::conv2_stream_on)
       .def("begin_epoch", &Engine::begin_epoch, py::arg("seed"), py::arg("rng_base"), py::arg("step0") = 0, py::arg("flags") = 0)
       .def("train_steps", &Engine::train_steps, py::call_guard<py::gil_scoped_release>())
       .def("capture_train", &Engine::capture_train)

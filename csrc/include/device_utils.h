@@ -156,10 +156,29 @@ __device__ __forceinline__ float normalize_u8_alu(uint32_t v) {
   return ((float)v / 255.0f - MNIST_MEAN) / MNIST_STD;
 }
 
-// One Adadelta element update (torch/optim/adadelta.py, foreach order: mul_, addcmul_, add+sqrt,
-// add+sqrt, div_, mul_, mul_, addcmul_, add_), every operation individually rounded (FMA
-// contraction off), so the result is a pure function of the inputs - bitwise identical in every
-// kernel that applies it (the optimizer kernels and the fused fc-backward epilogue).
+// ---- race-window widening (debug build `_C_rw`, -DMNIST_RACE_WIDEN=<us>; docs/DEBUGGING.md) ----
+// Every kernel's workgroups sleep a pseudo-random 0..MNIST_RACE_WIDEN us before their first global
+// read (RW_ENTRY, placed after a kernel's start signal), and every stream hand-off signal - start
+// signals, signal launches, held completions - is preceded by such a sleep (RW_SIGNAL).  The delays
+// are drawn from the real-time clock per workgroup, so each launch of each step explores another
+// interleaving of the compute and comm streams: a buffer that a hand-off does not actually protect
+// is read or overwritten out of order in some step, and the schedule stops being bitwise equal to
+// SERIAL.  Compiled out of the product build (no cost there).
+#ifdef MNIST_RACE_WIDEN
+__device__ __forceinline__ void race_widen_sleep(uint32_t tag) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();               // 100 MHz
+  uint32_t h = (uint32_t)t0 * 0x9e3779b9u ^ (blockIdx.x + 0x7f4a7c15u * tag);
+  h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12; h *= 0x297a2d39u; h ^= h >> 15;
+  const uint64_t ticks = h % (uint32_t)(MNIST_RACE_WIDEN * 100);
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+#define RW_ENTRY() ::mnist::race_widen_sleep(__LINE__)
+#define RW_SIGNAL() ::mnist::race_widen_sleep(__LINE__ * 7u + 1u)
+#else
+#define RW_ENTRY() ((void)0)
+#define RW_SIGNAL() ((void)0)
+#endif
+
 // Spin (one lane) until *a >= target: relaxed agent-scope polls with s_sleep; after ~60 s sets *err
 // and gives up (a protocol bug must not hang the GPU).  Used by the schedule-3 stream hand-offs.
 __device__ __forceinline__ void spin_until_geq(const int* a, int target, int* err) {
@@ -172,8 +191,14 @@ __device__ __forceinline__ void spin_until_geq(const int* a, int target, int* er
       return;
     }
   }
+  RW_SIGNAL();   // (debug build: the held kernel's completion - its hand-off - comes later)
 }
 
+
+// One Adadelta element update (torch/optim/adadelta.py, foreach order: mul_, addcmul_, add+sqrt,
+// add+sqrt, div_, mul_, mul_, addcmul_, add_), every operation individually rounded (FMA
+// contraction off), so the result is a pure function of the inputs - bitwise identical in every
+// kernel that applies it (the optimizer kernels and the fused fc-backward epilogue).
 struct Ada {
   float rho, eps, wd, lr;
   __device__ __forceinline__ float step(float& p, float g, float& sq, float& acc) const {

@@ -107,7 +107,8 @@ __global__ __launch_bounds__(256) void adadelta_kernel(AdadeltaArgs a, int regio
   int bid = blockIdx.x;
   if (a.state_inc && !a.hold_a && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   if (a.signal_start && bid == 0 && threadIdx.x == 0)      // the previous launch on the stream is done
-    __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   bool done = false;
   if (region == ADA_FC && gridDim.x < FC1_TILES + 1) {
     // fc bucket on fewer workgroups than tiles (grid-stride): the overlapped single-GPU / RCCL update
@@ -153,7 +154,8 @@ __global__ __launch_bounds__(256) void adadelta_reduce_kernel(AdadeltaArgs a, Co
   int bid = blockIdx.x;
   if (a.state_inc && !a.hold_a && bid == 0 && threadIdx.x == 0) a.state_inc->step += 1;
   if (a.signal_start && bid == 0 && threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   if (!conv_only) {
     const Ada ad{a.rho, a.eps, a.weight_decay, *a.lr};
     if (bid < FC1_TILES) { fc1_tile<true>(a, ad, bid, ts); return; }

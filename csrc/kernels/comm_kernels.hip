@@ -1,6 +1,7 @@
 // Small kernels of the DDP gradient reducer (runtime/bucket_reducer.cpp): the copy of one
 // parameter's gradient into its bucket view, pre-scaled by 1/world_size (torch DDP's
 // "divide before all-reduce", reducer.hpp copy_grad_to_bucket), 16 B per lane where aligned.
+#include "../include/device_utils.h"
 #include "../include/kernels.h"
 #include "../include/timeline.h"
 
@@ -8,6 +9,7 @@ namespace mnist {
 
 __global__ __launch_bounds__(256) void scale_copy_kernel(float* __restrict__ dst, const float* __restrict__ src,
                                                           int64_t n, float s) {
+  RW_ENTRY();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool vec = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
@@ -45,11 +47,12 @@ namespace mnist {
 // is set every later wait returns immediately and Engine::synchronize() raises.
 __global__ void stream_signal_kernel(int* ctr) {
   TL_SCOPE(TL_SIGNAL);
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) (RW_SIGNAL(), __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 __global__ void stream_wait_kernel(const int* a, const int* b, int delta, int* err, uint64_t timeout_ticks) {
   TL_SCOPE(TL_WAIT);
+  RW_ENTRY();
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
@@ -69,7 +72,7 @@ __global__ void stream_signal_wait_kernel(int* sig, const int* a, const int* b, 
                                           uint64_t timeout_ticks) {
   TL_SCOPE(TL_WAIT);
   if (threadIdx.x != 0) return;
-  __hip_atomic_fetch_add(sig, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  (RW_SIGNAL(), __hip_atomic_fetch_add(sig, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int target = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + delta;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -111,6 +114,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
                                                           const int32_t* __restrict__ idx, int64_t start,
                                                           int64_t n, uint8_t* __restrict__ dst_u8,
                                                           int32_t* __restrict__ dst_labels) {
+  RW_ENTRY();
   TL_SCOPE(TL_GATHER);
   constexpr int CH = 784 / 16;
   const int lane = threadIdx.x & 63;

@@ -433,7 +433,8 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_persist_kernel(ConvBwdArgs
   const int tid = threadIdx.x, n = 4 * B, G = gridDim.x;
   int it = blockIdx.x;
   if (a.signal_ctr && it == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   const StepState* st = a.state ? a.state : &g_zero_state;
   const int step = st->step;
   uint4 w[9];
@@ -674,7 +675,8 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lean_kernel(ConvBwdArg
   const int nt0 = (ng < 2) ? 5 * ng : 10 + 4 * (ng - 2), nn = (ng < 2) ? 5 : 4;
   const int G = gridDim.x, g = blockIdx.x;
   if (a.signal_ctr && g == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   const int rows = H2 * B;
   const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
   const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
@@ -755,7 +757,8 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
   const int mt0 = 2 * (hw & 1), nt0 = 9 * (hw >> 1);
   const int G = gridDim.x, g = blockIdx.x;
   if (a.signal_ctr && g == 0 && tid == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   const int rows = H2 * B;
   const int r0 = (int)((int64_t)g * rows / G), r1 = (int)((int64_t)(g + 1) * rows / G);
   const int nchunks = (r1 - r0 + WG_CH - 1) / WG_CH;
@@ -839,6 +842,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv2_wgrad_lstag_kernel(ConvBwdAr
 // Stand-alone reduce (the DDP schedule all-reduces the conv bucket between it and the update).
 __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(ConvBwdArgs a, int B, int bid0) {
   TL_SCOPE(TL_CONV_REDUCE);
+  RW_ENTRY();
   __shared__ float4 red[256];
   float* grad = a.grad;
   reduce_conv_grads(a, B, blockIdx.x + bid0, red, [grad](int64_t e, float v) { grad[e] = v; });
@@ -852,6 +856,7 @@ static void launch_c1_prereduce(const ConvBwdArgs& a, int B, hipStream_t s);
 __global__ __launch_bounds__(256) void c1_prereduce_kernel(const float* __restrict__ c1part, int nslab,
                                                            float* __restrict__ c1red) {
   TL_SCOPE(TL_C1_PRE);
+  RW_ENTRY();
   __shared__ float4 sh[240];
   const int j = blockIdx.x, tid = threadIdx.x;
   const int R = (nslab + C1_PRE_SLABS - 1) / C1_PRE_SLABS;

@@ -67,6 +67,7 @@ struct has_put4<P, decltype(void(P::PUT4))> { static constexpr bool value = P::P
 // 16 x 16 MFMA blocks: wider per-wave tiles read fewer LDS operands per MFMA
 template <int BM, int BN, int BK, int WGM, class P>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(P p) {
+  RW_ENTRY();
   constexpr int WN = 4 / WGM, TM = BM / WGM / 16, TN = BN / WN / 16;
   static_assert(WGM * WN == 4 && TM >= 1 && TN >= 1 && TM * WGM * 16 == BM && TN * WN * 16 == BN, "wave tiling");
   constexpr int NA = BM * BK / 4, NB = BN * BK / 4;            // float4s per operand tile
@@ -313,6 +314,7 @@ struct PConv2X {
 // ... and fc1.weight position-major for the fc1 input gradient: w1p[o][pos][c] = w1[o][c * 144 + pos]
 // (threads walk the destination: coalesced 16-B stores, gathered 4-B loads from L2)
 __global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a, int train) {
+  RW_ENTRY();
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t < C2 * K2) {
     const int co = t / K2, r = t - co * K2, ci = r / 9, tap = r - 9 * ci;   // torch [co][ci][ky][kx]
@@ -334,6 +336,7 @@ __global__ __launch_bounds__(256) void f32_prep_kernel(F32Step a, int train) {
 // instruction writes 8 whole pixels (1 KB contiguous)
 constexpr int C1_PIX_PER_WG = 32, C1_WG_PER_IMG = (NPIX1 + C1_PIX_PER_WG - 1) / C1_PIX_PER_WG;   // 22
 __global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
+  RW_ENTRY();
   __shared__ float img[IMG * IMG];
   const int b = blockIdx.x / C1_WG_PER_IMG, part = blockIdx.x - b * C1_WG_PER_IMG;
   const uint8_t* src = image_row(a, state_of(a)->step, b);
@@ -357,6 +360,7 @@ __global__ __launch_bounds__(256) void f32_conv1_kernel(F32Step a, int B) {
 // flat elements of one channel = one Philox block (the trunk's rule: counter rng_base + 2 step)
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void f32_pool_kernel(F32Step a, int B) {
+  RW_ENTRY();
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)B * C2 * (NPOOL / 16)) return;
   // lanes = channels: each y2 load instruction reads one pixel's 64 channels (256 contiguous bytes;
@@ -415,6 +419,7 @@ __device__ __forceinline__ void log_softmax10_f32(const float* x, float* lp) {
 // loss; eval writes the row's summed-NLL term and whether argmax (first max) == label.
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void f32_head_kernel(F32Step a, int B, int S) {
+  RW_ENTRY();
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (b >= B) return;
   const StepState* st = state_of(a);
@@ -505,6 +510,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // fc2 weight / bias, fc1 bias gradients and the step's mean loss: workgroup o = hidden unit o
 __global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
+  RW_ENTRY();
   __shared__ float red[4];
   const int o = blockIdx.x;
   float acc[NCLS + 1];
@@ -549,6 +555,7 @@ __global__ __launch_bounds__(256) void f32_fc_small_kernel(F32Step a, int B) {
 // part[g][c][0..9].  (One thread per channel doing its own 64-bit index math and 9 IEEE-division
 // normalisations per pixel: 40 us at B = 200.)
 __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G) {
+  RW_ENTRY();
   __shared__ float red[8][C1 * 10];
   __shared__ float img[IMG * IMG];
   const int g = blockIdx.x, tid = threadIdx.x, c = tid & 31, pl = tid >> 5;
@@ -604,6 +611,7 @@ __global__ __launch_bounds__(256) void f32_conv1w_kernel(F32Step a, int B, int G
 constexpr int RED2_BLOCKS = (WG_N + 63) / 64;
 constexpr int RED1_BLOCKS = C1 * 10 / 4;
 __global__ __launch_bounds__(256) void f32_conv_reduce_kernel(F32Step a, int s2, int s1) {
+  RW_ENTRY();
   __shared__ float red[256];
   const int tid = threadIdx.x;
   if (blockIdx.x < RED2_BLOCKS) {

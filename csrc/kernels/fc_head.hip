@@ -77,6 +77,7 @@ template <int MR>
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict__ p,
                                                       const uint16_t* __restrict__ w1,
                                                       float* __restrict__ z1part, int B) {
+  RW_ENTRY();
   TL_SCOPE(TL_FC1);
   fc1_tile<MR>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
 }
@@ -98,6 +99,7 @@ __device__ __forceinline__ int f1b_swz(int row) { return (row >> 1) & 7; }
 __global__ __launch_bounds__(256) void fc1_fwd_big_kernel(const uint16_t* __restrict__ p,
                                                           const uint16_t* __restrict__ w1,
                                                           float* __restrict__ z1part, int B) {
+  RW_ENTRY();
   TL_SCOPE(TL_FC1);
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * F1B_STAGE];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -359,10 +361,12 @@ __device__ __forceinline__ void head_train_row(const HeadArgs& a, int B, int b, 
 template <int KS, bool IDX>
 __global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a, int B) {
   TL_SCOPE(TL_HEAD);
+  RW_ENTRY();
   head_train_row<KS, IDX>(a, B, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
 __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
+  RW_ENTRY();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + wave;
   if (b >= B) return;
@@ -388,6 +392,7 @@ __global__ __launch_bounds__(256) void head_eval_kernel(HeadArgs a, int B) {
 
 // module API forward: log-probs (train: with dropout-2 drawn from StepState exactly as head_train does)
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, int B, int train) {
+  RW_ENTRY();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + wave;
   if (b >= B) return;
@@ -826,7 +831,8 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
   TL_SCOPE(TL_FC_BWD);
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (a.signal_ctr && blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    (RW_SIGNAL(), __hip_atomic_fetch_add(a.signal_ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
+  RW_ENTRY();
   const int S = fc_bwd_splits(B);
   const int nA = S * ROLE_A_WGS;
   int bid = blockIdx.x + bid0;
@@ -849,6 +855,7 @@ __global__ __launch_bounds__(256, BIG ? 2 : 3) void fc_bwd_kernel(FcBwdArgs a, i
 // loops; 12 KB of LDS and <= 80 VGPRs (6 waves per SIMD) so that it fits beside both of them
 // (dgrad: 2 x 70 KB LDS, 2 x 216 VGPRs per SIMD; wgrad: 89 KB, 2 x 208).  Bitwise the same partials.
 __global__ __launch_bounds__(256, 6) void fc_bwd_dw1_kernel(FcBwdArgs a, int B, int Bp) {
+  RW_ENTRY();
   __shared__ __attribute__((aligned(16))) unsigned char smem[12288];
   const int S = fc_bwd_splits(B);
   const int r = blockIdx.x;
@@ -862,6 +869,7 @@ __global__ __launch_bounds__(256, 6) void fc_bwd_dw1_kernel(FcBwdArgs a, int B, 
 // (u.hold_*) is adadelta_kernel's: the conv2 update that follows on the stream starts after dgrad's start.
 __global__ __launch_bounds__(256, 2) void fc_wgrad_update_kernel(FcBwdArgs a, AdadeltaArgs u, int B, int Bp) {
   TL_SCOPE(TL_ADA_FC);
+  RW_ENTRY();
   __shared__ __attribute__((aligned(16))) unsigned char smem[4096 + 32768];
   if (blockIdx.x == 0) fc_bwd_role_c<true>(a, B, Bp, 0, 1, smem, &u);
   else fc_bwd_role_a<true, true>(a, B, Bp, blockIdx.x - 1, 0, 1, smem, &u);
@@ -881,6 +889,7 @@ void launch_fc_wgrad_update(const FcBwdArgs& a, const AdadeltaArgs& u, int B, in
 // plus the mean loss.
 __global__ __launch_bounds__(256) void fc_grad_reduce_kernel(FcBwdArgs a, int B, int S) {
   TL_SCOPE(TL_FC_BWD);
+  RW_ENTRY();
   constexpr int64_t N4 = (OFF_FC2_B + NCLS + 3) / 4;   // float4 columns (the tail pads into fc2.b's pad)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < N4) {

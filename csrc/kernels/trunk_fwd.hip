@@ -95,6 +95,7 @@ enum TrunkX { TX_PRE = 0, TX_IDX = 1, TX_XIN = 2 };
 template <bool TRAIN, int NS, int XM>
 __global__ __launch_bounds__(256 * NS, NS == 1 ? 3 : 1) void trunk_fwd_kernel(TrunkFwdArgs a) {
   TL_SCOPE(TL_TRUNK);
+  RW_ENTRY();
   using K = TrunkCfg<NS>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[K::LDS];
   float* xs = reinterpret_cast<float*>(smem + K::XS_OFF);

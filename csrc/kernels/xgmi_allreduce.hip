@@ -140,6 +140,7 @@ __device__ __forceinline__ void ada_update4(const XgmiArgs& a, const Ada& ad, in
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_TWOSHOT);
+  RW_ENTRY();
   __shared__ int s_epoch, s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiArgs a) {
 template <int W>
 __global__ __launch_bounds__(256) void xgmi_oneshot_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_ONESHOT);
+  RW_ENTRY();
   __shared__ int s_epoch, s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
@@ -398,6 +400,7 @@ __device__ __forceinline__ void fcu_update(const XgmiArgs& a, const Ada& ad, int
 template <int W>
 __global__ __launch_bounds__(256, W >= 4 ? 6 : 1) void xgmi_fc_fused_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_FC);
+  RW_ENTRY();
   constexpr int PG = 1;                                          // phase-2 units in flight per lane
   __shared__ int s_epoch, s_err;
   __shared__ __attribute__((aligned(16))) uint16_t ts[32 * FCU_TS];
@@ -564,8 +567,9 @@ __global__ __launch_bounds__(256) void xgmi_conv_reduce_fused_kernel(XgmiArgs a,
     // XGMI comm chain: "the previous launch on this stream (the fc all-reduce + update) is done",
     // signalled by the first workgroup at its start instead of by a signal launch
     if (b == 0 && a.ada.signal_start)
-      __hip_atomic_fetch_add(a.ada.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      (RW_SIGNAL(), __hip_atomic_fetch_add(a.ada.signal_start, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT));
   }
+  RW_ENTRY();
   // (the reduce's first barrier orders the slot initialisation before any sink write)
   for (int k = 0; k < nvb; ++k) {
     int nv = 0;

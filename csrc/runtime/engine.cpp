@@ -26,7 +26,6 @@ Engine::Engine(const EngineBuffers& buf, int max_batch, int max_test_batch, hipS
   if (max_batch < 1 || max_test_batch < 0) throw std::runtime_error("bad batch sizes");
   HIP_OK(hipEventCreateWithFlags(&ev_fc_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&ev_done2_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   for (SideLauncher& l : side_) HIP_OK(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
   alloc_workspace();
@@ -47,11 +46,9 @@ Engine::~Engine() {
   }
   for (auto g : side_graphs_)
     if (g) hipGraphExecDestroy(g);
-  for (auto g : c2_graphs_)
-    if (g) hipGraphExecDestroy(g);
   for (auto g : graphs_) hipGraphExecDestroy(g);
   for (auto g : graph_defs_) hipGraphDestroy(g);
-  for (hipEvent_t e : {ev_fc_, ev_done_, ev_done2_, ev_fork_})
+  for (hipEvent_t e : {ev_fc_, ev_done_, ev_fork_})
     if (e) hipEventDestroy(e);
   if (ws_) hipFree(ws_);
   if (ws32_) hipFree(ws32_);
@@ -239,11 +236,9 @@ void Engine::enqueue_step(int batch, bool last) {
   const int32_t* labels = pre ? buf_.epoch_labels : buf_.train_labels;
   TrunkFwdArgs tf{data, idxp, stride, buf_.state, P + OFF_CONV1_W, P + OFF_CONV1_B,
                   buf_.w2f, P + OFF_CONV2_B, a1_, p_, pmask_, nullptr};
-  const bool c2s = use_conv2_stream();
   if (side && !side_forked_) {         // once per chunk: order the comm stream after the chunk start
     HIP_OK(hipEventRecord(ev_fc_, compute_));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fc_, 0));
-    if (c2s) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fc_, 0));
     side_forked_ = true;
   }
   // the previous step's fc update (comm stream) must be done before fc1_fwd reads w1: trunk_fwd
@@ -272,15 +267,14 @@ void Engine::enqueue_step(int batch, bool last) {
   // ... and the fc1 weight gradient itself (fc_bwd role A: 145 workgroups per 1024-row split streaming
   // p from HBM) leaves the compute chain for the comm stream, ahead of that reduce, where it runs
   // beside conv2_wgrad / conv2_dgrad.  The next step cannot overwrite p / dz1 before it is done: the
-  // comm stream's later launches (fc update, conv2 update) gate the next trunk_fwd / fc1_fwd.  Not
-  // with the opt-in conv2 stream, whose conv2 update no longer queues behind it.
-  const bool dw1_side = fc_reduce_side && fc_dw1_side_ && !c2s;
+  // comm stream's later launches (fc update, conv2 update) gate the next trunk_fwd / fc1_fwd.
+  const bool dw1_side = fc_reduce_side && fc_dw1_side_;
   // OVERLAP / XGMI chain, B <= 1024: both fc weight gradients (roles C + A, 146 workgroups) leave the
   // compute launch for the comm stream, released by fc_bwd's start (counter [5]: head_train done)
   // instead of by wgrad's start, so the fc update (or fc all-reduce + update) that follows them
   // starts ~wgrad's length earlier and the comm chain - conv2's reduce + update at its end gates the
   // next trunk_fwd - finishes earlier.  The compute chain keeps role B (dy records) only.
-  const bool fcw_side = side && !c2s && !trace_ && (!xg || xgmi_fuse_update_) && fc_bwd_splits(B) == 1 &&
+  const bool fcw_side = side && !trace_ && (!xg || xgmi_fuse_update_) && fc_bwd_splits(B) == 1 &&
                         fc_dw1_side_;
   // [5] counts fc_bwd starts in every schedule that counts wgrad starts in [0] (lockstep with [1])
   if (side || (sched_ == RCCL && two_buckets_)) fb.signal_ctr = sync_ + 5;
@@ -288,7 +282,10 @@ void Engine::enqueue_step(int batch, bool last) {
   // ... so that fc update runs beside role B, which reads w1t: role B reads this step's copy while the
   // update writes the other (ping-pong like w2d below; every element is rewritten each step)
   uint16_t* const w1t_cur = w1t_in_alt_ ? w1t_alt_ : buf_.w1t;
-  uint16_t* const w1t_next = fcw_side ? (w1t_in_alt_ ? buf_.w1t : w1t_alt_) : w1t_cur;
+  // (w1t_pingpong_ off: test hook only - the update overwrites the copy role B reads, the race the
+  // ping-pong exists for; docs/DEBUGGING.md "race-window widening")
+  const bool w1t_pp = fcw_side && w1t_pingpong_;
+  uint16_t* const w1t_next = w1t_pp ? (w1t_in_alt_ ? buf_.w1t : w1t_alt_) : w1t_cur;
   fb.w1t = w1t_cur;
   phase_begin("bwd_fc");
   if (M) launch_fc_bwd(fb, B, Bp, compute_, !fc_reduce_side, roles);
@@ -297,7 +294,7 @@ void Engine::enqueue_step(int batch, bool last) {
   AdadeltaArgs ad{P, buf_.grad, buf_.square_avg, buf_.acc_delta, buf_.lr, rho_, eps_, wd_,
                   buf_.w2f, buf_.w2d, buf_.w1, w1t_next, nullptr};
   ad.wt = B <= WT_MAX_B;                          // write-through stores at small batches (store16)
-  if (fcw_side) w1t_in_alt_ = !w1t_in_alt_;
+  if (w1t_pp) w1t_in_alt_ = !w1t_in_alt_;
   ConvBwdArgs cb{dyc_, a1_, buf_.w2d, P + OFF_CONV1_W, P + OFF_CONV1_B, data,
                  idxp, stride, buf_.state, c1part_, w2part_, buf_.grad, gscale,
                  conv_wgrad_groups(B), nullptr};
@@ -408,8 +405,7 @@ void Engine::enqueue_step(int batch, bool last) {
   // XGMI (fused kernels) runs the same chain: the fc all-reduce + update holds its completion, the
   // conv2 reduce + all-reduce + update signals [1] at its start (world-1 timeline: two hand-off launches
   // a step fewer, conv2's part no longer queued behind them)
-  // With a conv2 stream (OVERLAP) conv2's part leaves the comm stream: no chain, plain waits / signals
-  const bool chain = !trace_ && (!xg || xgmi_fuse_update_) && !c2s;
+  const bool chain = !trace_ && (!xg || xgmi_fuse_update_);
   phase_begin("allreduce_fc+update");
   if (S) {
     int* const rel = fcw_side ? sync_ + 5 : sync_ + 0;   // fc_bwd's start / wgrad's start
@@ -481,9 +477,8 @@ void Engine::enqueue_step(int batch, bool last) {
     u2.state_inc = nullptr;
     u2.w2d = w2d_in_alt_ ? buf_.w2d : w2d_alt_;
     cb.w2d = w2d_cur;
-    // conv stream: the comm stream after the fc update, or (c2s) the conv2 stream beside it
-    hipStream_t s2 = c2s ? conv2_stream_ : comm_stream_;
-    if (c2s ? enq_c2_ : S) {
+    hipStream_t s2 = comm_stream_;
+    if (S) {
       if (!chain) launch_stream_wait(sync_ + 4, sync_ + 3, 1, sync_ + 2, s2);
       if (chain) u2.signal_start = sync_ + 1;     // the fc update (previous launch) is done
       if (xg) {
@@ -539,10 +534,6 @@ void Engine::enqueue_step(int batch, bool last) {
     if (M && !skip_join_) {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(compute_, ev_done_, 0));
-      if (c2s) {
-        HIP_OK(hipEventRecord(ev_done2_, conv2_stream_));
-        HIP_OK(hipStreamWaitEvent(compute_, ev_done2_, 0));
-      }
     }
     side_pending_ = false;
     side_forked_ = false;
@@ -595,6 +586,13 @@ void Engine::enqueue_step_f32(int batch, bool last) {
       launch_f32_conv2x_conv1w(a, batch, compute_);
       launch_stream_wait(sync_ + 3, sync_ + 4, 0, sync_ + 2, compute_);
       launch_f32_conv_reduce(a, batch, compute_);
+    }
+    // the conv bucket's tail (all-reduce + update, compute stream).  RCCL runs one communicator's
+    // collectives in ISSUE order, even across streams, so with RCCL the conv all-reduce is enqueued
+    // after the comm chain's fc all-reduce: compute reaches it only after [3] >= [4], which the comm
+    // chain signals after the fc all-reduce - issued the other way round, the fc all-reduce would queue
+    // behind a conv all-reduce that waits for it (a cycle broken only by the 60 s hand-off timeout)
+    auto conv_tail = [&] {
       AdadeltaArgs ac = ad;
       ac.state_inc = buf_.state;
       if (xg) {
@@ -604,7 +602,8 @@ void Engine::enqueue_step_f32(int batch, bool last) {
         if (rc) comm_->allreduce_sum(buf_.grad + OFF_CONV1_W, PARAM_TOTAL - OFF_CONV1_W, 0, compute_);
         launch_adadelta(ac, ADA_CONV, compute_);
       }
-    }
+    };
+    if (M && !rc) conv_tail();
     if (S) {
       launch_stream_wait(sync_ + 0, sync_ + 1, 1, sync_ + 2, comm_stream_);
       launch_f32_fc1w(a, batch, comm_stream_);
@@ -621,6 +620,7 @@ void Engine::enqueue_step_f32(int batch, bool last) {
       launch_f32_conv2w(a, batch, comm_stream_);
       launch_stream_signal(sync_ + 3, comm_stream_);
     }
+    if (M && rc) conv_tail();
     side_pending_ = true;
     if (last) {
       if (M && !skip_join_) {
@@ -686,13 +686,12 @@ int Engine::capture_train(int n, int batch, int stride) {
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   side_graphs_.push_back(nullptr);
-  c2_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
 }
 
 void Engine::reset_host_state() {
   comm_sig3_pending_ = false;
-  enq_main_ = enq_side_ = enq_c2_ = true;
+  enq_main_ = enq_side_ = true;
   skip_join_ = false;
   side_pending_ = false;
   side_forked_ = false;
@@ -711,9 +710,8 @@ void Engine::reset_host_state() {
 // (comm stream -> compute) become two events at replay.
 int Engine::capture_train_split(int n, int batch) {
   const bool sp = side_pending_, w2 = w2d_in_alt_, w1 = w1t_in_alt_;
-  const bool c2s = use_conv2_stream();        // a third pass: the conv2 stream's chain
-  hipGraph_t gs = nullptr, gm = nullptr, g2 = nullptr;
-  auto pass = [&](hipStream_t s, bool m, bool side, bool c2, hipGraph_t* out) {
+  hipGraph_t gs = nullptr, gm = nullptr;
+  auto pass = [&](hipStream_t s, bool m, bool side, hipGraph_t* out) {
     side_pending_ = sp;
     w2d_in_alt_ = w2;
     w1t_in_alt_ = w1;
@@ -721,41 +719,36 @@ int Engine::capture_train_split(int n, int batch) {
     side_forked_ = true;                   // forks / joins are events at replay, not captured edges
     enq_main_ = m;
     enq_side_ = side;
-    enq_c2_ = c2;
     skip_join_ = true;
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     for (int i = 0; i < n; ++i) enqueue_step(batch, i == n - 1);
     HIP_OK(hipStreamEndCapture(s, out));
   };
   try {
-    pass(comm_stream_, false, true, false, &gs);
-    if (c2s) pass(conv2_stream_, false, false, true, &g2);
-    pass(compute_, true, false, false, &gm);
-    enq_main_ = enq_side_ = enq_c2_ = true;
+    pass(comm_stream_, false, true, &gs);
+    pass(compute_, true, false, &gm);
+    enq_main_ = enq_side_ = true;
     skip_join_ = false;
   } catch (...) {
     reset_host_state();
     hipStreamCaptureStatus st;
-    for (hipStream_t s : {comm_stream_, conv2_stream_, compute_}) {
+    for (hipStream_t s : {comm_stream_, compute_}) {
       hipGraph_t junk = nullptr;
       if (s && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
         hipStreamEndCapture(s, &junk);
       if (junk) hipGraphDestroy(junk);
     }
-    for (hipGraph_t g : {gs, gm, g2})
+    for (hipGraph_t g : {gs, gm})
       if (g) hipGraphDestroy(g);
     throw;
   }
-  hipGraphExec_t xs = nullptr, xm = nullptr, x2 = nullptr;
+  hipGraphExec_t xs = nullptr, xm = nullptr;
   HIP_OK(hipGraphInstantiate(&xs, gs, nullptr, nullptr, 0));
   HIP_OK(hipGraphInstantiate(&xm, gm, nullptr, nullptr, 0));
-  if (g2) HIP_OK(hipGraphInstantiate(&x2, g2, nullptr, nullptr, 0));
   graph_defs_.push_back(gs);
   graph_defs_.push_back(gm);
-  if (g2) graph_defs_.push_back(g2);
   graphs_.push_back(xm);
   side_graphs_.push_back(xs);
-  c2_graphs_.push_back(x2);
   return (int)graphs_.size() - 1;
 }
 
@@ -814,21 +807,14 @@ void Engine::replay(int id) {
     HIP_OK(hipGraphLaunch(graphs_[id], compute_));
     return;
   }
-  hipGraphExec_t c2 = c2_graphs_[id];
-  if (c2 && !conv2_stream_) throw std::runtime_error("replay: graph captured with the conv2 stream, now unset");
-  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chains ordered after earlier compute work
+  HIP_OK(hipEventRecord(ev_fork_, compute_));          // side chain ordered after earlier compute work
   HIP_OK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
-  if (c2) HIP_OK(hipStreamWaitEvent(conv2_stream_, ev_fork_, 0));
   side_start(0, side, comm_stream_);
-  if (c2) side_start(1, c2, conv2_stream_);
   const hipError_t em = hipGraphLaunch(graphs_[id], compute_);
   const hipError_t es = side_wait(0);
-  const hipError_t e2 = c2 ? side_wait(1) : hipSuccess;
   HIP_OK(em);
   HIP_OK(es);
-  HIP_OK(e2);
-  HIP_OK(hipStreamWaitEvent(compute_, side_[0].join, 0));   // chunk end: compute joins the side chains
-  if (c2) HIP_OK(hipStreamWaitEvent(compute_, side_[1].join, 0));
+  HIP_OK(hipStreamWaitEvent(compute_, side_[0].join, 0));   // chunk end: compute joins the side chain
 }
 
 void Engine::enqueue_eval(int n_total, int batch) {
@@ -878,7 +864,6 @@ int Engine::capture_eval(int n_total, int batch) {
   graph_defs_.push_back(g);
   graphs_.push_back(ex);
   side_graphs_.push_back(nullptr);
-  c2_graphs_.push_back(nullptr);
   return (int)graphs_.size() - 1;
 }
 
@@ -911,15 +896,6 @@ bool Engine::probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s) {
 }
 
 bool Engine::probe_stream_handoff(double timeout_s) { return probe_stream_pair(compute_, comm_stream_, timeout_s); }
-
-bool Engine::set_conv2_stream(hipStream_t s, double timeout_s) {
-  sync_streams();
-  // graphs captured for the other stream layout stay valid only in their own (replay refuses a
-  // conv2-stream graph once the stream is unset; graphs captured without it run the 2-stream chain)
-  const bool ok = s && probe_stream_pair(compute_, s, timeout_s) && probe_stream_pair(comm_stream_, s, timeout_s);
-  conv2_stream_ = ok ? s : nullptr;
-  return ok;
-}
 
 // fault injection (tests): the compute stream spins until fault_release (scratch counters
 // [12] released, [13] zero, [14] the hold's own timeout flag - never the engine's error flag [2])
@@ -959,7 +935,6 @@ void Engine::check_errors() const {
 void Engine::sync_streams() {
   HIP_OK(hipStreamSynchronize(compute_));
   HIP_OK(hipStreamSynchronize(comm_stream_));
-  if (conv2_stream_) HIP_OK(hipStreamSynchronize(conv2_stream_));
 }
 
 void Engine::synchronize() {

@@ -96,6 +96,9 @@ class Engine {
   // XGMI schedules (released by fc_bwd's start)
   void set_fc_dw1_side(bool on) { fc_dw1_side_ = on; }
   bool fc_dw1_side() const { return fc_dw1_side_; }
+  // test hook: the second w1t copy (fc update beside fc_bwd role B); off reintroduces the race it fixes
+  void set_w1t_pingpong(bool on) { w1t_pingpong_ = on; }
+  bool w1t_pingpong() const { return w1t_pingpong_; }
   // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
   // hand-off counters and their error flag, so a schedule never inherits another's counts (e.g. an
   // aborted validation).  Detaching the xgmi communicator of the XGMI schedule unsets the schedule.
@@ -111,12 +114,6 @@ class Engine {
   // until fault_release, launched on another stream, lets it go
   void fault_hold(double timeout_s);
   void fault_release(hipStream_t s);
-  // OVERLAP (single GPU): conv2's slab reduce + update on a third stream, released by dgrad's start
-  // and running beside the fc update instead of queued behind it.  Probes `s` against both streams
-  // (three distinct hardware queues needed) and keeps it only if both hand-offs complete; nullptr =
-  // off (conv2's part back on the comm stream, after the fc update).  Call while idle.
-  bool set_conv2_stream(hipStream_t s, double timeout_s);
-  bool conv2_stream_on() const { return conv2_stream_ != nullptr; }
 
   // --- training
   void begin_epoch(uint64_t seed, uint64_t rng_base, int step0, int flags);   // 24-byte H2D, eager
@@ -156,7 +153,6 @@ class Engine {
   void enqueue_step_f32(int batch, bool last);
   F32Step f32_args() const;
   bool side_schedule() const { return sched_ == OVERLAP || sched_ == XGMI; }
-  bool use_conv2_stream() const { return conv2_stream_ && sched_ == OVERLAP && !f32_ && !trace_; }
   bool probe_stream_pair(hipStream_t x, hipStream_t y, double timeout_s);
   int capture_train_split(int n, int batch);
   void reset_host_state();
@@ -173,6 +169,7 @@ class Engine {
   bool two_buckets_ = true;
   bool rccl_handoff_ = false;
   bool fc_dw1_side_ = true;
+  bool w1t_pingpong_ = true;
   int idx_stride_ = 0;
   int sched_ = SERIAL;
   std::shared_ptr<RcclComm> comm_;
@@ -186,15 +183,13 @@ class Engine {
                                     // [3] conv2 updates done, [4] dgrad starts, [5] fc_bwd starts,
                                     // [8..11] probe scratch,
                                     // [12..15] fault-injection hold
-  hipStream_t conv2_stream_ = nullptr;       // set_conv2_stream
-  // split capture: which stream's pass enqueue_step feeds (main = compute, side = comm, c2 = conv2)
-  bool enq_main_ = true, enq_side_ = true, enq_c2_ = true;
+  // split capture: which stream's pass enqueue_step feeds (main = compute, side = comm)
+  bool enq_main_ = true, enq_side_ = true;
   bool skip_join_ = false;                    // split capture: the chunk-end join is a replay event
   std::vector<hipGraphExec_t> side_graphs_;   // per graph id: its side-chain graph (split capture) or null
-  std::vector<hipGraphExec_t> c2_graphs_;     // per graph id: its conv2-stream graph or null
   hipEvent_t ev_fork_ = nullptr;
-  // side-graph launchers: [0] the comm stream's graph, [1] the conv2 stream's, each on its own host
-  // thread, concurrently with the compute graph's launch on the calling thread
+  // side-graph launcher: the comm stream's graph on its own host thread, concurrently with the compute
+  // graph's launch on the calling thread
   struct SideLauncher {
     std::thread thread;
     std::mutex mu;
@@ -205,7 +200,7 @@ class Engine {
     bool done = false, stop = false;
     hipError_t err = hipSuccess;
   };
-  SideLauncher side_[2];
+  SideLauncher side_[1];
   void side_start(int k, hipGraphExec_t g, hipStream_t s);
   hipError_t side_wait(int k);
   bool trace_ = false;              // profile_steps: roctx range + drain per phase
@@ -217,7 +212,7 @@ class Engine {
   uint16_t* w1t_alt_ = nullptr;     // second transposed fc1 shadow (side fc weight gradients: the fc
                                     // update of step k runs beside fc_bwd role B, which reads w1t)
   bool w1t_in_alt_ = false;         // enqueue-time: the current w1t lives in w1t_alt_
-  hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr, ev_done2_ = nullptr;
+  hipEvent_t ev_fc_ = nullptr, ev_done_ = nullptr;
   // workspace
   int64_t ws_bytes_ = 0;
   void* ws_ = nullptr;

@@ -108,7 +108,8 @@ std::vector<uint8_t> RcclComm::unique_id() {
   return std::vector<uint8_t>(id.internal, id.internal + kUniqueIdBytes);
 }
 
-RcclComm::RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device, double init_timeout_s)
+RcclComm::RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device, double init_timeout_s,
+                   bool wait)
     : world_(world_size), rank_(rank) {
   if (!available()) throw std::runtime_error("RCCL symbols not found (import torch first)");
   if (uid.size() != kUniqueIdBytes) throw std::runtime_error("bad ncclUniqueId size");
@@ -127,7 +128,7 @@ RcclComm::RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, in
     if (r != 0 && r != ncclInProgress) check(r, "ncclCommInitRankConfig");
     comm_ = c;
     nonblocking_ = true;
-    finish(r, "ncclCommInitRankConfig", init_timeout_s);
+    if (wait) finish(r, "ncclCommInitRankConfig", init_timeout_s);
   } else {
     check(a.CommInitRank(&c, world_size, id, rank), "ncclCommInitRank");
     comm_ = c;
@@ -135,7 +136,24 @@ RcclComm::RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, in
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) api().CommDestroy((ncclComm_t)comm_);
+  if (!comm_) return;
+  // a communicator whose init failed or is still running is aborted (ncclCommDestroy would wait for it)
+  if (nonblocking_ && init_status() != 0) abort();
+  else api().CommDestroy((ncclComm_t)comm_);
+}
+
+int RcclComm::init_status() const {
+  if (!comm_) return -1;
+  if (!nonblocking_ || !api().CommGetAsyncError) return 0;
+  ncclResult_t st = 0;
+  ncclResult_t r = api().CommGetAsyncError((ncclComm_t)comm_, &st);
+  return r != 0 ? r : st;
+}
+
+std::string RcclComm::error_string(int code) {
+  if (code == -1) return "communicator aborted";
+  const char* s = api().GetErrorString ? api().GetErrorString(code) : nullptr;
+  return s ? s : ("RCCL error " + std::to_string(code));
 }
 
 void RcclComm::finish(int r, const char* what, double timeout_s) {

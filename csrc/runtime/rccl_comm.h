@@ -22,7 +22,11 @@ class RcclComm {
 
   // Non-blocking communicator where the RCCL exports ncclCommInitRankConfig / ncclCommAbort (the
   // init is polled here and aborted after init_timeout_s), else a blocking ncclCommInitRank.
-  RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device, double init_timeout_s = 600.0);
+  // wait = false (non-blocking communicator only): return as soon as the init is under way in RCCL's
+  // own thread; the caller polls init_status() and may abort() it at any time (distributed.py
+  // PendingRcclComm: the init never holds up the trainer, and a failed or unneeded one is dropped)
+  RcclComm(const std::vector<uint8_t>& uid, int world_size, int rank, int device, double init_timeout_s = 600.0,
+           bool wait = true);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -36,6 +40,10 @@ class RcclComm {
   bool aborted() const { return aborted_; }
   bool nonblocking() const { return nonblocking_; }
   int async_error() const;       // ncclCommGetAsyncError (0 = ncclSuccess, 7 = in progress)
+  // init progress of a wait = false communicator: 0 ready, 7 (ncclInProgress) still running, any other
+  // value the RCCL error code (error_string); -1 after abort()
+  int init_status() const;
+  static std::string error_string(int code);
   int world_size() const { return world_; }
   int rank() const { return rank_; }
 

@@ -25,9 +25,18 @@ OBJ_DIR = os.path.join(ROOT, "build", "obj")
 ARCH = "gfx950"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 OUTPUT = os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
-# debug variant with the in-kernel timeline (csrc/include/timeline.h): same module name, own file
-OBJ_DIR_TL = os.path.join(ROOT, "build", "obj_tl")
-OUTPUT_TL = os.path.join(PKG_DIR, "_C_tl" + EXT_SUFFIX)
+# debug variants, same module name (PyInit__C), own file and object directory:
+#   "tl": in-kernel wave timeline (csrc/include/timeline.h; MNIST_AMD_TIMELINE=1 loads it)
+#   "rw": race-window widening, 0..RACE_WIDEN_US us random sleeps before every kernel's first global
+#         read and every stream hand-off signal (device_utils.h; MNIST_AMD_RACE_WIDEN=1 loads it)
+RACE_WIDEN_US = 20
+VARIANTS = {
+    "": (os.path.join(ROOT, "build", "obj"), OUTPUT, []),
+    "tl": (os.path.join(ROOT, "build", "obj_tl"), os.path.join(PKG_DIR, "_C_tl" + EXT_SUFFIX), ["-DMNIST_TIMELINE"]),
+    "rw": (os.path.join(ROOT, "build", "obj_rw"), os.path.join(PKG_DIR, "_C_rw" + EXT_SUFFIX),
+           [f"-DMNIST_RACE_WIDEN={RACE_WIDEN_US}"]),
+}
+OBJ_DIR_TL, OUTPUT_TL = VARIANTS["tl"][0], VARIANTS["tl"][1]
 
 
 def _hipcc() -> str:
@@ -69,9 +78,9 @@ def _headers() -> list[str]:
     return sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True))
 
 
-def _obj_path(src: str, timeline: bool = False) -> str:
+def _obj_path(src: str, variant: str = "") -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
-    return os.path.join(OBJ_DIR_TL if timeline else OBJ_DIR, rel + ".o")
+    return os.path.join(VARIANTS[variant][0], rel + ".o")
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -81,11 +90,10 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def _compile(src: str, kernel: bool, verbose: bool, timeline: bool = False) -> str:
-    obj = _obj_path(src, timeline)
-    cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes()]
-    if timeline:
-        cmd.append("-DMNIST_TIMELINE")
+def _compile(src: str, kernel: bool, verbose: bool, variant: str = "") -> str:
+    obj = _obj_path(src, variant)
+    cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes(),
+           *VARIANTS[variant][2]]
     if kernel:
         cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
     else:
@@ -100,20 +108,24 @@ def _compile(src: str, kernel: bool, verbose: bool, timeline: bool = False) -> s
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False, timeline: bool = False) -> str:
-    """Compile + link the extension if anything changed; return the .so path.  ``timeline``: the
-    debug variant with in-kernel wave timestamps (``_C_tl``, loaded when MNIST_AMD_TIMELINE=1)."""
-    obj_dir, output = (OBJ_DIR_TL, OUTPUT_TL) if timeline else (OBJ_DIR, OUTPUT)
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, timeline: bool = False,
+          variant: str = "") -> str:
+    """Compile + link the extension if anything changed; return the .so path.  ``variant`` (or
+    ``timeline`` = "tl"): a debug build (``VARIANTS``)."""
+    build_datagen(force=force, verbose=verbose)
+    if timeline:
+        variant = "tl"
+    obj_dir, output = VARIANTS[variant][0], VARIANTS[variant][1]
     os.makedirs(obj_dir, exist_ok=True)
     kernels, host = sources()
     headers = _headers()
     todo = [(s, True) for s in kernels] + [(s, False) for s in host]
-    stale = [(s, k) for s, k in todo if force or _stale(_obj_path(s, timeline), [s, *headers])]
+    stale = [(s, k) for s, k in todo if force or _stale(_obj_path(s, variant), [s, *headers])]
     jobs = jobs or min(8, max(1, len(stale)))
     if stale:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            list(ex.map(lambda sk: _compile(sk[0], sk[1], verbose, timeline), stale))
-    objs = [_obj_path(s, timeline) for s, _ in todo]
+            list(ex.map(lambda sk: _compile(sk[0], sk[1], verbose, variant), stale))
+    objs = [_obj_path(s, variant) for s, _ in todo]
     if force or stale or _stale(output, objs):
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", output + ".tmp", "-ldl"]
         tl = _torch_lib_dir()
@@ -128,14 +140,36 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, t
     return output
 
 
+DATAGEN_SRC = os.path.join(CSRC, "data", "synthetic_gen.cpp")
+DATAGEN_OUT = os.path.join(PKG_DIR, "_datagen" + EXT_SUFFIX)
+
+
+def build_datagen(force: bool = False, verbose: bool = False) -> str:
+    """The synthetic-data generator (``_datagen``: pure C++17 + pybind11, no HIP) - host compiler,
+    strict IEEE float evaluation (no contraction) so every build emits the same bytes."""
+    if not force and not _stale(DATAGEN_OUT, [DATAGEN_SRC]):
+        return DATAGEN_OUT
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-ffp-contract=off", "-fno-fast-math",
+           *_includes(), DATAGEN_SRC, "-o", DATAGEN_OUT + ".tmp", "-pthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"datagen build failed\n{r.stdout}\n{r.stderr}")
+    os.replace(DATAGEN_OUT + ".tmp", DATAGEN_OUT)
+    return DATAGEN_OUT
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--timeline", action="store_true", help="debug variant with in-kernel timestamps (_C_tl)")
+    ap.add_argument("--race-widen", action="store_true", help="debug variant with race-window widening (_C_rw)")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, timeline=a.timeline)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, variant="tl" if a.timeline else "rw" if a.race_widen else "")
     print(out)
     return 0
 

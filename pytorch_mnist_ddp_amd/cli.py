@@ -74,9 +74,10 @@ def _framework_flags(parser: argparse.ArgumentParser) -> None:
                    help='DDP gradient bucket cap in MiB (default 25, as torch DDP)')
     g.add_argument('--first-bucket-mb', type=float, default=1.0,
                    help='DDP first-bucket cap in MiB (default 1, as torch DDP)')
-    g.add_argument('--allreduce', choices=['auto', 'rccl', 'xgmi'], default=None,
-                   help='DDP gradient all-reduce of the fused engine: RCCL, the direct xGMI kernel, or auto '
-                        '(default; times both at startup and keeps the faster)')
+    g.add_argument('--allreduce', choices=['auto', 'rccl', 'xgmi', 'fastest'], default=None,
+                   help='DDP gradient all-reduce of the fused engine: RCCL, the direct xGMI kernels, auto '
+                        '(default: xGMI when it validates at startup on one node, RCCL only as the fallback - '
+                        'never waited for otherwise), or fastest (validate and time both, keep the faster)')
     g.add_argument('--dist-backend', dest='pg_backend', choices=['nccl', 'gloo'], default=None,
                    help='torch.distributed backend for bootstrap / construction collectives (default: nccl = '
                         'RCCL on GPU, gloo with --no-cuda); gloo + --allreduce xgmi runs DDP without RCCL')

@@ -87,11 +87,13 @@ def _test_module(model, device, loader):
 
 
 # ----------------------------------------------------------------------------- main flows
-def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int:
+def run(argv=None, ddp_script: bool = True, t_start: float | None = None, holder: dict | None = None) -> int:
     # startup phases inside the reference timer (--json-log "setup_s") + wall-clock marks since the
     # timer's start ("timeline_s": where the rest goes - epochs, evaluation, teardown)
     setup = PhaseTimes(origin=t_start)
     args = cli.parse_args(ddp=ddp_script, argv=argv)
+    if holder is not None:
+        holder["args"] = args
     args._ddp_script = ddp_script
     # is_available() brings the HIP runtime up (~60 ms) and device_count() initialises amdsmi
     # (~53 ms, measured under cProfile on the box), both on the main thread inside the timer; the
@@ -134,14 +136,17 @@ def run(argv=None, ddp_script: bool = True, t_start: float | None = None) -> int
         args._prewarm = None
     if args._prewarm is None and engine == "fused":
         args._prewarm = _start_prewarm(device)
-    # the fused engine's RCCL communicator initialises on a helper thread while data, model and
-    # trainer are built (its bootstrap is the largest N > 1 startup cost inside the timer)
+    # the fused engine's RCCL communicator (PendingRcclComm): with --allreduce rccl / fastest, and
+    # under auto across nodes (no xGMI there), its non-blocking init starts now on a helper thread
+    # while data, model and trainer are built; under auto on one node it is only created - started
+    # by the trainer if the direct xGMI transport cannot be used, never waited for otherwise
     args._pending_comm = None
-    allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
-    if distributed and engine == "fused" and allreduce != "xgmi":
+    allreduce = _allreduce_choice(args)
+    if distributed and engine == "fused" and allreduce != "xgmi" and (world > 1 or allreduce != "auto"):
         from .parallel.distributed import start_rccl_comm
+        eager = allreduce != "auto" or not _one_node_by_env(world)
         with setup.phase("rccl_comm_start"):
-            args._pending_comm = start_rccl_comm(world, rank, gpu)
+            args._pending_comm = start_rccl_comm(world, rank, gpu, start=eager)
 
     setup.mark("pg_init")
     with setup.phase("data"):
@@ -205,6 +210,27 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
         _json_log(args.json_log, rec)
         scheduler.step()
     _save(args, model, distributed, rank, ddp_script)
+
+
+def _allreduce_choice(args) -> str:
+    return getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
+
+
+def _one_node_by_env(world: int) -> bool:
+    """The launcher says every rank is on this node (torchrun / torch.distributed.launch export
+    LOCAL_WORLD_SIZE); unknown (SLURM without a launcher) counts as "maybe not"."""
+    try:
+        return int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world
+    except ValueError:
+        return False
+
+
+def close_pending_comm(args) -> None:
+    """After the reference's timer: end a cancelled / unused RCCL init's helper thread (bounded) so
+    the interpreter never tears down under it."""
+    p = getattr(args, "_pending_comm", None)
+    if p is not None:
+        p.close(30.0)
 
 
 def gpu_present() -> bool:
@@ -316,9 +342,9 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             _prewarm_body(device)
         if distributed:
             torch.cuda.set_device(gpu)       # (deferred by init_distributed_mode: runtime is up now)
-    allreduce = getattr(args, 'allreduce', None) or os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
+    allreduce = _allreduce_choice(args)
     xgmi_pending = streams = None
-    if distributed and world > 1 and allreduce in ("xgmi", "auto"):
+    if distributed and world > 1 and allreduce in ("xgmi", "auto", "fastest"):
         # the trainer's two streams first: the setup thread's self-test streams must not take the
         # hardware queues they would otherwise get (few queues per process in one-GPU rehearsals)
         from .engine.trainer import make_streams
@@ -345,10 +371,6 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         two_buckets = engine_bucket_layout(ddp.bucket_indices)   # raises on a layout the engine cannot run
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("--allreduce xgmi needs the two-bucket layout (default --bucket-cap-mb/--first-bucket-mb)")
-        if args._pending_comm is not None:     # xgmi-only DDP needs no RCCL communicator at all
-            with setup.phase("rccl_comm_wait"):
-                comm = args._pending_comm.result()
-            setup.add_info("rccl_comm_init_thread_s", args._pending_comm.seconds)
     # The optimizer here is the engine's fused Adadelta kernel (state in `ms`); StepLR(step_size=1)
     # (reference mnist_ddp.py:178, :189) reduces to lr <- lr * gamma after every epoch, computed in
     # the same double arithmetic as torch's scheduler and handed to the kernels as a device scalar.
@@ -360,7 +382,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
                            world_size=world, rank=rank, comm=comm, seed=args.seed, graph_steps=graph_steps,
                            allreduce=allreduce, two_buckets=two_buckets,
                            fp32=getattr(args, "dtype", "bf16") == "fp32", xgmi_pending=xgmi_pending,
-                           streams=streams)
+                           streams=streams, rccl_pending=args._pending_comm)
     if xgmi_pending is not None:
         setup.add_info("xgmi_setup_thread_s", xgmi_pending.seconds)
     setup.mark("trainer")
@@ -498,12 +520,15 @@ def main_mnist(argv=None) -> int:
 
 def main_mnist_ddp(argv=None) -> int:
     start = time.time()
+    holder = {}
     try:
-        rc = run(argv, ddp_script=True, t_start=start)
+        rc = run(argv, ddp_script=True, t_start=start, holder=holder)
     except BaseException as e:  # noqa: BLE001
         if getattr(e, "fatal", False):
             _fatal_exit(e)
         raise
     print(total_time_line(time.time() - start))
     sys.stdout.flush()
+    if "args" in holder:
+        close_pending_comm(holder["args"])
     return rc

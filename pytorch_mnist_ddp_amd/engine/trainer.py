@@ -51,14 +51,7 @@ def rccl_watchdog_s() -> float:
 RCCL_DRAIN_S = 90.0
 
 
-def _fault_delay(kind: str, rank: int) -> float:
-    """Seconds to hold rank ``rank`` back at fault point ``kind`` (``MNIST_AMD_FAULT=kind:rank:seconds``,
-    tests only); 0 when not injected."""
-    spec = os.environ.get("MNIST_AMD_FAULT", "")
-    parts = spec.split(":")
-    if len(parts) == 3 and parts[0] == kind and int(parts[1]) == rank:
-        return float(parts[2])
-    return 0.0
+from ..parallel.distributed import _fault_delay  # noqa: E402  (MNIST_AMD_FAULT=kind:rank:seconds, tests)
 
 
 @dataclass
@@ -121,13 +114,17 @@ def make_streams(dev) -> tuple:
 
 
 class FusedTrainer:
-    """``allreduce`` (DDP): "rccl", "xgmi" or "auto" (default).  Every candidate transport is built
-    and its PRODUCTION schedule - the captured chunk graph training replays - is validated and timed
-    on this node before training (``transport_report``); "auto" keeps the faster valid one.
+    """``allreduce`` (DDP): "rccl", "xgmi", "auto" (default) or "fastest".  A candidate transport's
+    PRODUCTION schedule - the captured chunk graph training replays - is validated on this node before
+    training (``transport_report``).  "auto" validates the direct xGMI transport first and keeps it
+    without ever waiting for RCCL (``rccl_pending``, a ``PendingRcclComm``, is cancelled, or - deferred -
+    never started); RCCL is brought up only when xGMI is unavailable or fails.  "fastest" validates and
+    times both and keeps the faster (see ``_setup_ddp``).  ``hooks``: engine variants for A/B runs
+    (``HOOKS``).
     ``overlap`` (single GPU): the OVERLAP schedule (optimizer work on the comm stream) when the two
     streams pass the hand-off probe, else SERIAL.  ``xgmi_fuse``: the xGMI kernels apply Adadelta
     themselves (False = separate launches: the fused kernels' bitwise oracle).  ``probe_world1``
-    (tests): with a communicator at world 1, evaluate the xGMI candidate under "auto" too.
+    (tests, bench --force-comm): at world 1, make the xGMI transport a candidate under "auto" / "fastest" too.
     ``fp32`` (``--dtype fp32``): the fp32 step of ``f32_net.hip`` (f32-input MFMA GEMMs, fp32
     activations and gradient operands) in the OVERLAP (fc update on the comm stream) or SERIAL schedule,
     RCCL or XGMI at world > 1."""
@@ -137,7 +134,7 @@ class FusedTrainer:
                  comm=None, seed: int = 1, graph_steps: int = 10, dropout: bool = True,
                  two_buckets: bool = True, allreduce: str | None = None, overlap: bool = True,
                  xgmi_fuse: bool = True, probe_world1: bool = False, fp32: bool = False, xgmi_pending=None,
-                 streams=None):
+                 streams=None, rccl_pending=None, hooks: dict | None = None):
         C = native.load()
         self.C, self.ms = C, mstate
         # host seconds per setup phase (engine, xgmi_comm, stream_probe, validate.<transport>,
@@ -203,11 +200,7 @@ class FusedTrainer:
                                int(self.compute.cuda_stream), int(self.comm_stream.cuda_stream),
                                world_size, mstate.rho, mstate.eps, mstate.weight_decay, fp32=self.fp32)
         self.engine.set_bucket_split(two_buckets)
-        # B > 1024, side schedules: fc_bwd's fc1 weight gradient on the comm stream beside the conv
-        # backward (MNIST_AMD_FC_DW1_SIDE=0: in the compute-stream fc_bwd launch, for A/B)
-        self.engine.fc_dw1_side = os.environ.get("MNIST_AMD_FC_DW1_SIDE", "1") != "0"
-        if os.environ.get("MNIST_AMD_DGRAD_GRID"):     # A/B only: persistent dgrad grid (0 = 2 x CUs)
-            C.set_dgrad_grid(int(os.environ["MNIST_AMD_DGRAD_GRID"]))
+        self.apply_hooks(hooks or {})
         self._graphs: dict[tuple[int, int], int] = {}        # captured chunks of the selected schedule
         self._graph_sets: dict[str, dict] = {}               # per transport (validation captures)
         self._eval_graph: int | None = None
@@ -218,9 +211,9 @@ class FusedTrainer:
         if comm is not None:
             self.engine.attach_comm(comm)                    # also the parameter broadcast's transport
         if allreduce is None:
-            allreduce = os.environ.get("MNIST_AMD_ALLREDUCE", "auto")
-        if allreduce not in ("rccl", "xgmi", "auto"):
-            raise ValueError(f"allreduce must be 'rccl', 'xgmi' or 'auto', got {allreduce!r}")
+            allreduce = "auto"
+        if allreduce not in ("rccl", "xgmi", "auto", "fastest"):
+            raise ValueError(f"allreduce must be 'rccl', 'xgmi', 'auto' or 'fastest', got {allreduce!r}")
         if allreduce == "xgmi" and not two_buckets:
             raise ValueError("the xGMI all-reduce runs the engine's two-bucket schedule (two_buckets=True)")
         self.xgmi, self.grad_out = None, None
@@ -232,13 +225,41 @@ class FusedTrainer:
         self.xgmi_validation = None
         self.allreduce = None
         import torch.distributed as _dist
-        ddp = comm is not None or world_size > 1 or (allreduce == "xgmi" and _dist.is_initialized())
+        ddp = (comm is not None or rccl_pending is not None or world_size > 1
+               or (allreduce == "xgmi" and _dist.is_initialized()))
         self._xgmi_pending = xgmi_pending        # distributed.PendingXgmiComm started by the caller
+        self._rccl_pending = rccl_pending        # distributed.PendingRcclComm (maybe not started)
         if not ddp:
             self._setup_single_gpu(overlap)
         else:
             self._setup_ddp(comm, allreduce, two_buckets, probe_world1, train)
         self.setup.add("engine", time.perf_counter() - _t_init - self.setup.total())
+
+    # engine variants for A/B measurements and tests (tools/ab_*.sh through bench.py --hook), set before
+    # any graph is captured: name -> (setter, what it changes)
+    HOOKS = {
+        # B > 1024 side schedules: fc_bwd's fc1 weight gradient on the comm stream beside the conv
+        # backward (default 1; 0 = inside the compute-stream fc_bwd launch)
+        "fc_dw1_side": "fc_bwd's weight-gradient roles on the comm stream (1) or in the compute launch (0)",
+        # persistent conv2_dgrad grid (0 = the default sizing; n > 0 workgroups)
+        "dgrad_grid": "persistent conv2_dgrad grid override in workgroups (0 = default)",
+        # the second w1t copy; 0 = the fc update overwrites the w1t fc_bwd role B reads (a known race,
+        # for the race-window widening check only - never a product setting)
+        "w1t_pingpong": "fc update writes the other w1t copy (1) or the one role B reads (0: the old race)",
+    }
+
+    def apply_hooks(self, hooks: dict) -> None:
+        """Engine variants by name (``HOOKS``); unknown names raise.  Process-wide ones
+        (``dgrad_grid``) stay set until changed."""
+        for k, v in hooks.items():
+            if k == "fc_dw1_side":
+                self.engine.fc_dw1_side = bool(int(v))
+            elif k == "dgrad_grid":
+                self.C.set_dgrad_grid(int(v))
+            elif k == "w1t_pingpong":
+                self.engine.w1t_pingpong = bool(int(v))
+            else:
+                raise ValueError(f"unknown engine hook {k!r} (known: {sorted(self.HOOKS)})")
 
     # ------------------------------------------------------------------ schedule selection
     def _probe_streams(self) -> bool:
@@ -255,45 +276,65 @@ class FusedTrainer:
         # conv2's part moved too); SERIAL when the streams share a hardware queue
         self.overlap = bool(overlap) and self._probe_streams()
         self.engine.set_schedule(C.SCHED_OVERLAP if self.overlap else C.SCHED_SERIAL)
-        # opt-in (MNIST_AMD_CONV2_STREAM=1): conv2's slab reduce + update on a third stream, beside the
-        # fc update from dgrad's start on, if it gets its own hardware queue.  Measured slower (600
-        # steps 64.5-64.8 -> 66.0-67.9 us/step for fc-update grids 144-577: dgrad 14.4 -> 17.5 us with
-        # two co-runners; profiles/r5/ab/conv2_stream.txt), so off by default
-        self.conv2_stream = None
-        # (a hand-off completes in microseconds: a short probe, skipped outright with fewer than 4
-        # hardware queues per process, where the third stream would share one)
-        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-        if (self.overlap and not self.fp32 and queues >= 4
-                and os.environ.get("MNIST_AMD_CONV2_STREAM", "0") == "1"):
-            with self.setup.phase("stream_probe"):
-                s = torch.cuda.Stream(device=self.device)
-                if self.engine.set_conv2_stream(int(s.cuda_stream), 1.0):
-                    self.conv2_stream = s
 
     def _use_graph_set(self, name: str) -> None:
         self._graphs = self._graph_sets.setdefault(name, {})
 
+    def _rccl_candidate(self, comm, pending):
+        """The RCCL communicator: ``comm`` as given, else ``pending``'s (started now if it was deferred,
+        then waited for).  Returns (comm or None, why-not): an init that fails or times out drops RCCL,
+        it never ends the run by itself (the caller decides whether any transport is left)."""
+        if comm is not None or pending is None:
+            return comm, None
+        with self.setup.phase("rccl_comm_wait"):
+            try:
+                comm = pending.result()
+            except Exception as e:  # noqa: BLE001 - reported as the candidate's failure
+                comm = None
+                why = f"rank {self.rank}: RCCL communicator init failed ({type(e).__name__}: {e})"
+            else:
+                why = None
+        self.setup.add_info("rccl_comm_init_thread_s", round(pending.seconds or 0.0, 4))
+        # collective: a communicator is usable only when every rank has one
+        from ..parallel.distributed import gather_strings
+        msgs = [m for m in gather_strings(why or "", self.world) if m]
+        if msgs and comm is not None:
+            comm.abort()
+            comm = None
+        return comm, "; ".join(msgs) or None
+
     def _setup_ddp(self, comm, allreduce: str, two_buckets: bool, probe_world1: bool, train) -> None:
-        """Build every candidate transport, validate + time its production schedule, keep the best."""
+        """Build the candidate transports, validate + time their production schedules, keep one.
+
+        * ``xgmi`` / ``rccl``: that transport only (an RCCL communicator that fails to initialise is
+          the run's error).
+        * ``auto`` (default): the direct xGMI kernels first (one node); once their production schedule
+          has validated on every rank they are kept and RCCL is never waited for - a pending RCCL init
+          is cancelled, a deferred one never starts - so RCCL's bootstrap and validation replays never
+          sit inside the reference's timer.  Only when xGMI cannot be built or fails its validation is
+          RCCL brought up and validated (its init error, timeout or stuck replay then fails the run).
+        * ``fastest``: both validated and timed, the faster kept (an RCCL init that fails drops RCCL).
+        """
         from ..parallel.distributed import create_xgmi_comm, release_xgmi_comm
         C = self.C
         self.overlap = False
-        want_x = allreduce == "xgmi" or (allreduce == "auto" and comm is not None and two_buckets
+        pending, self._rccl_pending = self._rccl_pending, None
+        have_r = comm is not None or pending is not None
+        want_x = allreduce == "xgmi" or (allreduce in ("auto", "fastest") and two_buckets
                                          and (self.world > 1 or probe_world1))
-        want_r = comm is not None and allreduce in ("rccl", "auto")
         x = None
-        pending, self._xgmi_pending = self._xgmi_pending, None
-        if pending is not None and not want_x:      # started by the caller, not a candidate after all
+        xpend, self._xgmi_pending = self._xgmi_pending, None
+        if xpend is not None and not want_x:        # started by the caller, not a candidate after all
             with self.setup.phase("xgmi_comm"):
-                x = pending.result()
+                x = xpend.result()
                 if x is not None:
                     release_xgmi_comm(x, self.world)
                 x = None
         if want_x:
             with self.setup.phase("xgmi_comm"):   # (with a pending setup: the wait for its helper thread)
-                if pending is not None:
-                    x = pending.result()
-                    sub = dict(pending.timings, helper_thread_s=round(pending.seconds or 0.0, 4))
+                if xpend is not None:
+                    x = xpend.result()
+                    sub = dict(xpend.timings, helper_thread_s=round(xpend.seconds or 0.0, 4))
                 else:
                     sub = {}
                     x = create_xgmi_comm(self.world, self.rank, self.device, self.ms.grad.numel(), timings=sub)
@@ -302,7 +343,7 @@ class FusedTrainer:
         # XGMI schedule and of the RCCL schedule's fc update need it (one probe, every rank; after
         # the xGMI setup, whose self-test keeps three more streams busy - with few hardware queues per
         # process, as in the one-GPU rehearsals, the two would share queues)
-        handoff = self._probe_streams() if (x is not None or (want_r and two_buckets)) else False
+        handoff = self._probe_streams() if (x is not None or (have_r and two_buckets)) else False
         self.engine.set_rccl_handoff(handoff)
         if want_x:
             if x is not None and not handoff:
@@ -312,15 +353,25 @@ class FusedTrainer:
                 x = None
             if x is None:
                 self.transport_report["xgmi"] = {"ok": False, "validation": "setup, self-test or stream probe failed"}
+        if x is None and allreduce != "xgmi":
+            # no xGMI transport: RCCL is the only candidate left (its init is waited for only now)
+            comm, why = self._rccl_candidate(comm, pending)
+            pending = None
+            if comm is None and have_r:
+                self.transport_report["rccl"] = {"ok": False, "validation": why or "no communicator"}
+            if comm is not None:
+                self.comm = comm
+                self.engine.attach_comm(comm)
         # DDP construction semantics: rank 0's parameters everywhere BEFORE the validations (they
         # compare the ranks' parameters after replaying the same steps)
-        self.broadcast_params(x)
+        if x is not None or self.comm is not None or not self.transport_report:
+            self.broadcast_params(x)
         if x is not None:
             self.engine.attach_xgmi(x)
             self.engine.set_schedule(C.SCHED_XGMI)
             self.xgmi = x
             self._use_graph_set("xgmi")
-            both = want_r                            # two candidates: time each beyond its first replay
+            both = allreduce == "fastest" and have_r   # two candidates: time each beyond its first replay
             ok, why, us = self._validate("xgmi", train, timed=both)
             if not ok and "differ" in why:
                 # wrong sums, no timeout: retry with system-scope release / acquire fences around every
@@ -342,22 +393,47 @@ class FusedTrainer:
             if not ok:
                 release_xgmi_comm(x, self.world)
                 x = self.xgmi = None
+            if ok and allreduce == "auto":
+                # validated on every rank (collective verdict): RCCL is not needed - every rank drops
+                # its (pending or deferred) communicator, nobody's bootstrap waits for a peer
+                if pending is not None:
+                    pending.cancel()
+                    self.transport_report["rccl"] = {"ok": None, "validation": "not needed: the xGMI "
+                                                     f"transport validated first (RCCL init {pending.status})"}
+                    pending = None
+                elif comm is not None:
+                    self.transport_report["rccl"] = {"ok": None, "validation": "not needed: the xGMI "
+                                                     "transport validated first"}
+                comm = None
+            elif allreduce in ("auto", "fastest") and comm is None and pending is not None:
+                comm, why = self._rccl_candidate(None, pending)   # xGMI failed (auto) / both timed
+                pending = None
+                if comm is None:
+                    self.transport_report["rccl"] = {"ok": False, "validation": why or "no communicator"}
+                else:
+                    self.comm = comm
+                    self.engine.attach_comm(comm)
+        want_r = comm is not None and allreduce in ("rccl", "auto", "fastest") and \
+            not (allreduce == "auto" and self.transport_report.get("xgmi", {}).get("ok"))
         if want_r:
             self.engine.set_schedule(C.SCHED_RCCL)
             self._use_graph_set("rccl")
-            ok, why, us = self._validate("rccl", train, timed=want_x)
+            ok, why, us = self._validate("rccl", train, timed=x is not None)
             self.transport_report["rccl"] = {"ok": ok, "validation": why, "us_per_step": us}
         valid = {k: v["us_per_step"] for k, v in self.transport_report.items() if v.get("ok")}
         self.allreduce_timings = {k: round(v["us_per_step"], 2) for k, v in self.transport_report.items()
                                   if v.get("us_per_step") is not None}
         if not valid:
             msg = "; ".join(f"{k}: {v.get('validation')}" for k, v in self.transport_report.items())
-            hint = "" if comm is not None else " (no RCCL communicator: rerun with --allreduce rccl or auto)"
+            hint = "" if have_r else " (no RCCL communicator: rerun with --allreduce rccl or auto)"
             raise StartupValidationError(f"world size {self.world}: no gradient all-reduce passed its startup "
                                          f"validation ({msg or 'no candidate'}){hint}", self.transport_report,
                                          self.setup)
         pick = min(valid, key=valid.get)
         if pick == "xgmi":
+            if self.comm is not None and allreduce != "fastest":
+                self.engine.attach_comm(None)
+                self.comm = None
             self.engine.attach_xgmi(x)
             self.engine.set_schedule(C.SCHED_XGMI)
         else:

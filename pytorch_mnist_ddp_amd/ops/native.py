@@ -21,7 +21,10 @@ def load(build_if_missing: bool = True):
     if _C is not None:
         return _C
     if os.environ.get("MNIST_AMD_TIMELINE") == "1":
-        _C = _load_timeline_variant(build_if_missing)
+        _C = _load_variant("tl", build_if_missing)
+        return _C
+    if os.environ.get("MNIST_AMD_RACE_WIDEN") == "1":
+        _C = _load_variant("rw", build_if_missing)
         return _C
     if os.environ.get("MNIST_AMD_EXT_PATH"):      # A/B runs: another build of the same sources
         _C = _load_from(os.environ["MNIST_AMD_EXT_PATH"])
@@ -39,19 +42,19 @@ def load(build_if_missing: bool = True):
     raise RuntimeError(f"native extension pytorch_mnist_ddp_amd._C is not available: {_err}")
 
 
-def _load_timeline_variant(build_if_missing: bool):
-    """The debug build with in-kernel wave timestamps (``_C_tl``, csrc/include/timeline.h), imported
-    under the module name ``_C`` (its PyInit symbol) so every caller gets it."""
-    import importlib.util
-    import sys
+def _load_variant(variant: str, build_if_missing: bool):
+    """A debug build (``_build.VARIANTS``: "tl" = in-kernel wave timestamps, csrc/include/timeline.h;
+    "rw" = race-window widening, csrc/include/device_utils.h), imported under the module name ``_C``
+    (its PyInit symbol) so every caller gets it."""
     import sysconfig
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "_C_tl" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+                        f"_C_{variant}" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
     if not os.path.exists(path):
         if not build_if_missing:
-            raise RuntimeError(f"timeline build {path} missing (python -m pytorch_mnist_ddp_amd._build --timeline)")
+            raise RuntimeError(f"debug build {path} missing (python -m pytorch_mnist_ddp_amd._build "
+                               f"{'--timeline' if variant == 'tl' else '--race-widen'})")
         from .. import _build
-        _build.build(timeline=True)
+        _build.build(variant=variant)
     return _load_from(path)
 
 

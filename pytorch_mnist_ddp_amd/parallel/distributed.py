@@ -71,6 +71,45 @@ def init_distributed_mode(args) -> None:
 
 _UID_KEY = "pytorch_mnist_ddp_amd/rccl_unique_id"
 _rccl_seq = 0          # communicators created so far (same order on every rank -> unique store keys)
+# ncclCommInitRank's own limit (a peer that never arrives): the communicator is aborted after it
+RCCL_INIT_TIMEOUT_S = float(os.environ.get("MNIST_AMD_RCCL_INIT_TIMEOUT", "300"))
+
+
+def _fault_delay(kind: str, rank: int) -> float:
+    """Seconds to hold rank ``rank`` back at fault point ``kind`` (``MNIST_AMD_FAULT=kind:rank:seconds``,
+    tests only); 0 when not injected."""
+    parts = os.environ.get("MNIST_AMD_FAULT", "").split(":")
+    if len(parts) == 3 and parts[0] == kind and int(parts[1]) == rank:
+        return float(parts[2])
+    return 0.0
+
+
+def _uid(world_size: int, rank: int, tag: str, store=None, cancelled=None):
+    """The communicator's ncclUniqueId: made by rank 0, passed through the store (``store``: the
+    caller's client, else the default one).  ``cancelled()`` is polled while waiting (None = never)."""
+    from ..ops import native
+    C = native.load()
+    if store is None:
+        store = dist.distributed_c10d._get_default_store()
+    key = f"{_UID_KEY}/{tag}"
+    if rank == 0:
+        uid = C.RcclComm.unique_id()
+        store.set(key, uid)
+        return uid
+    deadline = time.monotonic() + RCCL_INIT_TIMEOUT_S
+    while True:
+        try:
+            store.wait([key], timedelta(seconds=0.25))
+            return store.get(key)
+        except RuntimeError:
+            if cancelled is not None and cancelled():
+                raise _Cancelled() from None
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"rank 0's ncclUniqueId did not arrive within {RCCL_INIT_TIMEOUT_S:.0f} s") from None
+
+
+class _Cancelled(Exception):
+    pass
 
 
 def create_rccl_comm(world_size: int, rank: int, device: int, tag: str | None = None):
@@ -83,52 +122,122 @@ def create_rccl_comm(world_size: int, rank: int, device: int, tag: str | None = 
     if tag is None:
         tag = str(_rccl_seq)
     _rccl_seq += 1
-    store = dist.distributed_c10d._get_default_store()
-    key = f"{_UID_KEY}/{tag}"
-    if rank == 0:
-        uid = C.RcclComm.unique_id()
-        store.set(key, uid)
-    else:
-        store.wait([key], timedelta(minutes=5))
-        uid = store.get(key)
-    return C.RcclComm(bytes(uid), world_size, rank, device)
+    uid = _uid(world_size, rank, tag)
+    return C.RcclComm(bytes(uid), world_size, rank, device, RCCL_INIT_TIMEOUT_S)
 
 
 class PendingRcclComm:
-    """:func:`create_rccl_comm` on a helper thread (``ncclCommInitRank`` blocks for its bootstrap -
-    socket rendezvous, topology detection, channel setup - and releases the GIL meanwhile).
-    ``result()`` joins and returns the communicator (or re-raises its error); ``seconds`` is how
-    long the init took on the helper thread."""
+    """The framework's RCCL communicator, initialised off the critical path: a helper thread fetches the
+    ncclUniqueId (its own store client) and starts a NON-BLOCKING ``ncclCommInitRankConfig`` (the
+    bootstrap - socket rendezvous, topology detection, channel setup - runs in RCCL's own thread),
+    then polls it.  Nothing waits for it unless RCCL is actually needed:
 
-    def __init__(self, world_size: int, rank: int, device: int):
+    * ``result(timeout_s)`` joins and returns the communicator, or raises its init error (an init that
+      fails - e.g. two ranks on one GPU - or exceeds ``RCCL_INIT_TIMEOUT_S`` is aborted first);
+    * ``cancel()`` returns at once: the helper aborts the (pending or finished) communicator and exits
+      (``--allreduce auto`` once the xGMI transport has validated on every rank: a collective verdict,
+      so every rank cancels, and no rank's bootstrap is left waiting for a peer);
+    * ``start=False`` defers even the start (``start()``): RCCL is then touched only if the caller asks.
+
+    ``seconds`` is the helper's time; ``status`` one of "not started", "initialising", "ready",
+    "failed: ...", "cancelled".  Fault injection (tests): ``MNIST_AMD_FAULT=rccl_init_delay:R:S`` holds
+    rank R's helper S seconds before its init (cancel-aware)."""
+
+    def __init__(self, world_size: int, rank: int, device: int, start: bool = True):
         global _rccl_seq
         self._tag = str(_rccl_seq)          # claimed now: the store keys follow the callers' order
         _rccl_seq += 1
         self._args = (world_size, rank, device)
         self._comm, self._err, self.seconds = None, None, None
-        self._t = threading.Thread(target=self._run, name="rccl-init", daemon=True)
-        self._t.start()
+        self._cancel = threading.Event()
+        self._t = None
+        self._taken = False                 # result() handed the communicator out: cancel() leaves it
+        self.status = "not started"
+        if start:
+            self.start()
+
+    @property
+    def started(self) -> bool:
+        return self._t is not None
+
+    def start(self) -> "PendingRcclComm":
+        if self._t is None:
+            from .hostcomm import own_store_client
+            self._store = own_store_client()             # its own socket (None: share the default)
+            self.status = "initialising"
+            self._t = threading.Thread(target=self._run, name="rccl-init", daemon=True)
+            self._t.start()
+        return self
 
     def _run(self):
+        from ..ops import native
         t0 = time.perf_counter()
+        world, rank, device = self._args
+        comm = None
         try:
-            torch.cuda.set_device(self._args[2])
-            self._comm = create_rccl_comm(*self._args, tag=self._tag)
+            if self._cancel.wait(_fault_delay("rccl_init_delay", rank)):
+                raise _Cancelled()
+            C = native.load()
+            if not C.RcclComm.available():
+                raise RuntimeError("RCCL not found in this process")
+            torch.cuda.set_device(device)
+            uid = _uid(world, rank, self._tag, self._store, self._cancel.is_set)
+            comm = C.RcclComm(bytes(uid), world, rank, device, RCCL_INIT_TIMEOUT_S, False)
+            deadline = time.monotonic() + RCCL_INIT_TIMEOUT_S
+            while True:
+                st = comm.init_status()
+                if st == 0:
+                    break
+                if st != 7:                 # ncclInProgress
+                    raise RuntimeError(f"ncclCommInitRankConfig failed: {C.RcclComm.error_string(st)}")
+                if self._cancel.wait(0.002):
+                    raise _Cancelled()
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"ncclCommInitRankConfig did not complete within {RCCL_INIT_TIMEOUT_S:.0f} s")
+            if self._cancel.is_set():
+                raise _Cancelled()
+            self._comm, self.status = comm, "ready"
+        except _Cancelled:
+            if comm is not None:
+                comm.abort()
+            self._err, self.status = RuntimeError("RCCL communicator init cancelled"), "cancelled"
         except BaseException as e:  # noqa: BLE001 - re-raised in result()
-            self._err = e
+            if comm is not None:
+                comm.abort()
+            self._err, self.status = e, f"failed: {e}"
         self.seconds = time.perf_counter() - t0
 
-    def result(self, timeout_s: float = 600.0):
+    def result(self, timeout_s: float = RCCL_INIT_TIMEOUT_S + 30.0):
+        self.start()
         self._t.join(timeout_s)
         if self._t.is_alive():
-            raise RuntimeError(f"RCCL communicator init did not finish within {timeout_s:.0f} s")
+            self.cancel()
+            raise RuntimeError(f"RCCL communicator init did not finish within {timeout_s:.0f} s (cancelled)")
         if self._err is not None:
             raise self._err
+        self._taken = True
         return self._comm
 
+    def cancel(self) -> None:
+        """Drop the communicator unless ``result()`` handed it out (non-blocking: the helper thread
+        aborts a pending init; a finished, unused one is aborted here)."""
+        if self._taken:
+            return
+        self._cancel.set()
+        c, self._comm = self._comm, None
+        if c is not None:
+            c.abort()
+            self.status = "cancelled"
 
-def start_rccl_comm(world_size: int, rank: int, device: int) -> PendingRcclComm:
-    return PendingRcclComm(world_size, rank, device)
+    def close(self, timeout_s: float = 10.0) -> None:
+        """Cancel and wait (bounded) for the helper thread: call after training, outside any timer."""
+        self.cancel()
+        if self._t is not None:
+            self._t.join(timeout_s)
+
+
+def start_rccl_comm(world_size: int, rank: int, device: int, start: bool = True) -> PendingRcclComm:
+    return PendingRcclComm(world_size, rank, device, start=start)
 
 
 def get_rank() -> int:
@@ -144,7 +253,6 @@ def barrier(world: int | None = None) -> None:
     get_hostcomm(world).barrier()
 
 
-_XGMI_KEY = "pytorch_mnist_ddp_amd/xgmi_record"
 # stage-wait timeout of the startup self-test / schedule validation: long enough that a peer delayed
 # by the GPU's queue scheduling (many processes on one GPU in rehearsals) is not mistaken for a hang
 STARTUP_TIMEOUT_S = float(os.environ.get("MNIST_AMD_STARTUP_TIMEOUT", "15"))
@@ -216,16 +324,34 @@ def _device_identity(device) -> str:
     return native.load().device_identity(torch.device(device).index or 0)
 
 
-def ranks_per_device(device, world: int | None = None) -> int:
-    """Largest number of ranks of the default process group that drive one physical GPU (1 in the
-    production layout; > 1 in the one-GPU multi-process rehearsal).  The xGMI kernels wait per
-    workgroup on their peers, so the residency planner (``xgmi_plan_grids``) sizes their grids for
-    this many ranks' spinning workgroups on one GPU."""
+def _node_identity() -> str:
+    """This host (hostname + kernel boot id): ranks whose identities differ cannot share IPC memory."""
+    import socket
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+def device_topology(device, world: int | None = None) -> tuple[int, int]:
+    """(largest number of ranks of the default process group that drive one physical GPU, number of
+    nodes): one host collective.  Ranks per GPU is 1 in the production layout and > 1 in the one-GPU
+    multi-process rehearsal; the xGMI kernels wait per workgroup on their peers, so the residency
+    planner (``xgmi_plan_grids``) sizes their grids for that many ranks' spinning workgroups on one
+    GPU.  The direct xGMI transport needs one node (IPC-mapped peer memory)."""
     hc = get_hostcomm(world)
     if hc.world == 1:
-        return 1
-    ids = hc.gather_strings(_device_identity(device))
-    return max(ids.count(i) for i in ids)
+        return 1, 1
+    ids = [s.split("|", 1) for s in hc.gather_strings(_node_identity() + "|" + _device_identity(device))]
+    devs = [d for _, d in ids]
+    return max(devs.count(d) for d in devs), len({n for n, _ in ids})
+
+
+def ranks_per_device(device, world: int | None = None) -> int:
+    """Largest number of ranks of the default process group that drive one physical GPU."""
+    return device_topology(device, world)[0]
 
 
 def ranks_share_a_device(device) -> bool:
@@ -235,7 +361,7 @@ def ranks_share_a_device(device) -> bool:
 
 def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | None = None, channels: int = 3,
                      verify: bool = True, oneshot_max: int = 32768, co_ranks: int | None = None,
-                     timings: dict | None = None, store=None):
+                     timings: dict | None = None):
     """Direct xGMI all-reduce communicator over ``numel`` floats (csrc/runtime/xgmi_comm.h).
 
     The communicator owns its input / output buffers (``x.grad_in`` / ``x.grad_out``: zero-copy fp32
@@ -246,8 +372,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
     to map its peers or to verify (callers then keep the RCCL all-reduce).  ``co_ranks`` (default:
     measured with :func:`ranks_per_device`) sizes the kernel grids so every rank's spinning
     workgroups are resident.  ``timings`` (optional dict) receives host seconds per sub-step
-    (co_ranks, alloc, exchange, connect, verify): the N > 1 startup budget.  ``store``: the client
-    for the record exchange (default: the default process group's)."""
+    (co_ranks, alloc, exchange, connect, verify): the N > 1 startup budget.  The records travel as a
+    host collective (the calling thread's channel, see ``hostcomm.use_channel``)."""
     from torch.utils.dlpack import from_dlpack
 
     from ..ops import native
@@ -267,7 +393,12 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
         t = now
 
     if co_ranks is None:
-        co_ranks = ranks_per_device(dev, world_size)
+        co_ranks, nodes = device_topology(dev, world_size)
+        if nodes > 1:                 # (every rank saw the same gather: all return None together)
+            if rank == 0:
+                print(f"[xgmi] {nodes} nodes: no direct xGMI transport across nodes", flush=True)
+            tm["multi_node"] = nodes
+            return None
     lap("co_ranks")
     x = None
     try:
@@ -276,12 +407,8 @@ def create_xgmi_comm(world_size: int, rank: int, device, numel: int, tag: str | 
         x.grad_out = from_dlpack(x.dlpack("out"))
         lap("alloc")
         if world_size > 1:
-            if store is None:
-                store = dist.distributed_c10d._get_default_store()
-            store.set(f"{_XGMI_KEY}/{tag}/{rank}", x.record())
-            keys = [f"{_XGMI_KEY}/{tag}/{q}" for q in range(world_size)]
-            store.wait(keys, timedelta(minutes=5))
-            recs = [store.get(k) for k in keys]
+            # (a host collective: a peer's abort ends the wait at once instead of after its timeout)
+            recs = get_hostcomm(world_size).all_gather_bytes(x.record())
             lap("exchange")
             x.connect(recs)
             lap("connect")
@@ -328,7 +455,7 @@ class PendingXgmiComm:
             world, rank, dev, numel = self._args
             torch.cuda.set_device(dev)
             with use_channel(self._hc):
-                self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings, store=self._store)
+                self._comm = create_xgmi_comm(world, rank, dev, numel, timings=self.timings)
         except BaseException as e:  # noqa: BLE001 - re-raised in result()
             import traceback
             self._err = e

@@ -107,30 +107,35 @@ _default_pg = None
 _tls = threading.local()
 
 
+_channels: dict[str, int] = {}
+
+
 def channel(name: str, store=None) -> HostComm:
     """A separate sequence of host collectives (own key prefix) for a helper thread whose collectives
     run concurrently with the main thread's: every rank issues each channel's collectives in the same
     order, but the interleaving ACROSS channels differs between ranks, so the two must never share
-    one sequence counter.  ``store``: the channel's own client (see :func:`own_store_client`), else
+    one sequence counter.  Every channel of one name gets a fresh prefix (``name/k``: k-th channel of
+    that name in this process, the same on every rank), so a later channel never reads an earlier
+    one's leftover keys.  ``store``: the channel's own client (see :func:`own_store_client`), else
     the default store."""
     if store is None:
         store = dist.distributed_c10d._get_default_store()
-    return HostComm(store, dist.get_rank(), dist.get_world_size(), prefix=f"{_PREFIX}/{name}")
+    k = _channels.get(name, 0)
+    _channels[name] = k + 1
+    return HostComm(store, dist.get_rank(), dist.get_world_size(), prefix=f"{_PREFIX}/{name}/{k}")
 
 
-def own_store_client(timeout_s: float = 300.0):
-    """A second TCPStore client connection to the rendezvous server (MASTER_ADDR / MASTER_PORT) for a
-    helper thread.  One client serialises its calls on one socket, so a helper's blocking waits on
-    the default client stall the main thread's collectives (measured: the DDP wrap's one shape check
-    took 1.1 s behind the xGMI setup thread's record exchange).  None when the env does not name the
-    server (tcp:// or store= initialisation): callers then share the default client."""
-    addr, port = os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")
-    if not addr or not port:
-        return None
+def own_store_client():
+    """A second client connection to the rendezvous store for a helper thread: ``clone()`` of the
+    default store opens a new socket to the same server under the SAME key prefixes (torchelastic's
+    ``/worker/attempt_N`` etc.), so a helper's keys and the abort key are in the namespace every other
+    channel uses.  One client serialises its calls on one socket, so a helper's blocking waits on the
+    default client stall the main thread's collectives (measured: the DDP wrap's one shape check took
+    1.1 s behind the xGMI setup thread's record exchange).  None when the store cannot be cloned:
+    callers then share the default client (same namespace either way, so ranks that differ here still
+    meet)."""
     try:
-        c = dist.TCPStore(addr, int(port), is_master=False, wait_for_workers=False,
-                          timeout=timedelta(seconds=timeout_s))
-        return dist.PrefixStore("pytorch_mnist_ddp_amd/own", c)
+        return dist.distributed_c10d._get_default_store().clone()
     except Exception:  # noqa: BLE001 - fall back to the shared client
         return None
 

@@ -67,3 +67,44 @@ def test_normalize_matches_torchvision_formula():
 
 def test_split_sizes_match_mnist():
     assert synthetic.TRAIN_SIZE == 60000 and synthetic.TEST_SIZE == 10000
+
+
+def test_native_generator_v3_thread_invariant_and_balanced(monkeypatch):
+    """Generator v3 (csrc/data/synthetic_gen.cpp): every sample is a pure function of (seed, index),
+    so 1 and 7 threads give the same bytes, a prefix of a larger split equals the smaller split, the
+    classes are balanced, ~1 % of the train labels are flipped, and train / test streams differ."""
+    import torch
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    a_img, a_lab = synthetic.generate_native(3000, seed=11, label_noise=0.0)
+    monkeypatch.setenv("OMP_NUM_THREADS", "7")
+    b_img, b_lab = synthetic.generate_native(3000, seed=11, label_noise=0.0)
+    assert a_img.dtype == torch.uint8 and a_img.shape == (3000, 28, 28) and a_lab.dtype == torch.int64
+    assert torch.equal(a_img, b_img) and torch.equal(a_lab, b_lab)
+    c_img, c_lab = synthetic.generate_native(1000, seed=11, label_noise=0.0)
+    assert torch.equal(c_img, a_img[:1000]) and torch.equal(c_lab, a_lab[:1000])
+    counts = torch.bincount(a_lab, minlength=10)
+    assert counts.min() > 240 and counts.max() < 360
+    n_img, n_lab = synthetic.generate_native(20000, seed=11, label_noise=0.01)
+    assert torch.equal(n_img[:3000], a_img)                     # label noise leaves the images alone
+    flipped = (n_lab[:3000] != a_lab).float().mean().item()
+    assert flipped < 0.02
+    assert 0.003 < (n_lab != synthetic.generate_native(20000, seed=11)[1]).float().mean().item() < 0.02
+    d_img, _ = synthetic.generate_native(1000, seed=12)
+    assert not torch.equal(d_img, c_img)
+    assert 30 < a_img.float().mean().item() < 80                # strokes + speckle, not blank / saturated
+
+
+def test_synthetic_split_is_generated_not_cached(tmp_path):
+    """load_mnist(synthetic) builds the split in-process every run (no disk cache, so no cold / warm
+    difference inside the reference's timer) and gives the same bytes each time."""
+    import os
+    from pytorch_mnist_ddp_amd.data.datasets import load_mnist
+    a = load_mnist(str(tmp_path), train=False, synthetic_data=True, synthetic_size=500, verbose=False)
+    b = load_mnist(str(tmp_path), train=False, synthetic_data=True, synthetic_size=500, verbose=False)
+    assert torch_equal(a.images, b.images) and torch_equal(a.targets, b.targets)
+    assert not os.path.exists(os.path.join(str(tmp_path), "synthetic_cache"))
+
+
+def torch_equal(x, y):
+    import torch
+    return torch.equal(x, y)

@@ -211,3 +211,66 @@ def test_bench_fp32_xgmi_rehearsal(gpu_box, tmp_path, W):
     assert j["n_gpus"] == W and j["dtype"] == "fp32" and j["params_in_sync"] is True
     assert j["config"]["allreduce"] == "xgmi" and j["config"]["schedule"] == "xgmi"
     assert j["config"]["xgmi_validation"].startswith("ok (graph replay")
+
+
+def _driver_cmd(W, tmp_path, *extra, n_train=8000, B=200, epochs=2):
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+            "--nnodes", "1", "--nproc-per-node", str(W), os.path.join(ROOT, "mnist_ddp.py"),
+            "--batch-size", str(B), "--epochs", str(epochs), "--synthetic", "--synthetic-train-size", str(n_train),
+            "--synthetic-test-size", "1000", "--json-log", str(tmp_path / "log.jsonl"), *extra]
+
+
+def _setups(tmp_path):
+    return [x for x in (json.loads(ln) for ln in open(tmp_path / "log.jsonl")) if "setup_s" in x]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W", [2, 4])
+def test_production_command_trains_on_xgmi_rccl_never_waited(gpu_box, tmp_path, W):
+    """The driver's PRODUCTION command - default ``nccl`` process group, default ``--allreduce auto``, no
+    transport flag - with W ranks sharing GPU 0 (where RCCL could not initialise: two ranks on one
+    GPU): the xGMI transport validates first, RCCL is never started or waited for (no rccl phase
+    inside the reference timer), the run trains and exits 0 (VERDICT r5 #1)."""
+    r = subprocess.run(_driver_cmd(W, tmp_path), capture_output=True, text=True, timeout=280, cwd=tmp_path,
+                       env=_env())
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert len(re.findall(r"Total cost time:[0-9.]+ ms", r.stdout)) == W
+    assert len(re.findall(r"Test set: Average loss", r.stdout)) == 2
+    setups = _setups(tmp_path)
+    assert len(setups) == W
+    for x in setups:
+        assert x["allreduce"] == "xgmi", x["transport_report"]
+        rep = x["transport_report"]
+        assert rep["xgmi"]["ok"] and rep["rccl"]["ok"] is None, rep
+        assert rep["rccl"]["validation"].startswith("not needed") and "not started" in rep["rccl"]["validation"]
+        assert not any(k.startswith("trainer.rccl") or k.startswith("rccl_comm_wait") for k in x["setup_s"]), x["setup_s"]
+
+
+@pytest.mark.timeout(300)
+def test_fastest_drops_failed_rccl_init_and_keeps_xgmi(gpu_box, tmp_path):
+    """``--allreduce fastest`` starts RCCL's non-blocking init at once; with two ranks on one GPU it
+    fails (or is cut off by its init timeout): the failure drops the RCCL candidate on every rank
+    (collective) instead of ending the run, the validated xGMI schedule trains, and the transport
+    report names the init failure."""
+    r = subprocess.run(_driver_cmd(2, tmp_path, "--allreduce", "fastest"), capture_output=True, text=True,
+                       timeout=280, cwd=tmp_path, env=_env(MNIST_AMD_RCCL_INIT_TIMEOUT="40"))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    for x in _setups(tmp_path):
+        rep = x["transport_report"]
+        assert x["allreduce"] == "xgmi" and rep["xgmi"]["ok"], rep
+        assert rep["rccl"]["ok"] is False and "RCCL communicator init failed" in rep["rccl"]["validation"], rep
+
+
+@pytest.mark.timeout(300)
+def test_auto_falls_back_to_rccl_when_xgmi_fails(gpu_box, tmp_path):
+    """``--allreduce auto`` where the xGMI validation fails (rank 1 held back past the stage timeout):
+    only then is RCCL brought up - here it cannot initialise (two ranks on one GPU) - and the run stops
+    with ONE error naming both candidates' failures instead of hanging."""
+    env = _env(MNIST_AMD_FAULT="validate_delay:1:6", MNIST_AMD_STARTUP_TIMEOUT="2", MNIST_AMD_RCCL_INIT_TIMEOUT="40")
+    r = subprocess.run(_driver_cmd(2, tmp_path, epochs=1), capture_output=True, text=True, timeout=280,
+                       cwd=tmp_path, env=env)
+    err = r.stdout + r.stderr
+    assert r.returncode != 0, err[-3000:]
+    assert "no gradient all-reduce passed its startup validation" in err, err[-3000:]
+    assert "xgmi:" in err and "rccl:" in err and "RCCL communicator init failed" in err, err[-3000:]
+    assert "Train Epoch" not in r.stdout

@@ -65,7 +65,7 @@ def test_fp32_xgmi_schedule_world1_matches_single_gpu(cuda_device):
 
 
 def test_transport_choice_by_schedule_replay_world1(cuda_device):
-    """--allreduce auto picks the transport by replaying each candidate's PRODUCTION schedule: at
+    """--allreduce fastest picks the transport by replaying each candidate's PRODUCTION schedule: at
     world 1 with an RCCL communicator and the xGMI candidate forced in (probe_world1), both captured
     chunk graphs are validated and timed (us per step in transport_report), the faster is kept, and
     training on it is bitwise the single-transport runs (RCCL schedule; xGMI schedule) - the
@@ -79,10 +79,10 @@ def test_transport_choice_by_schedule_replay_world1(cuda_device):
         comm = create_rccl_comm(1, 0, 0)
         idx = torch.randperm(2000, generator=torch.Generator().manual_seed(4))
         res = {}
-        for name, kw in (("auto", dict(allreduce="auto", probe_world1=True)), ("rccl", dict(allreduce="rccl")),
+        for name, kw in (("fastest", dict(allreduce="fastest", probe_world1=True)), ("rccl", dict(allreduce="rccl")),
                          ("xgmi", dict(allreduce="xgmi"))):
             ms, t = _world1_trainer(cuda_device, comm, **kw)
-            if name == "auto":
+            if name == "fastest":
                 rep = t.transport_report
                 assert set(rep) == {"xgmi", "rccl"}, rep
                 assert all(r["ok"] and r["us_per_step"] > 0 for r in rep.values()), rep
@@ -97,7 +97,7 @@ def test_transport_choice_by_schedule_replay_world1(cuda_device):
             t.synchronize()
             res[name] = (ms.param.clone(), t.loss_log.clone())
         for name in ("rccl", "xgmi"):
-            assert torch.equal(res[name][0], res["auto"][0]) and torch.equal(res[name][1], res["auto"][1]), name
+            assert torch.equal(res[name][0], res["fastest"][0]) and torch.equal(res[name][1], res["fastest"][1]), name
     finally:
         dist.destroy_process_group()
 
@@ -144,7 +144,7 @@ def test_world_gt1_without_transport_refuses(cuda_device, monkeypatch):
 
 
 def test_stuck_rccl_candidate_is_aborted_and_xgmi_kept(cuda_device, monkeypatch):
-    """--allreduce auto where the RCCL candidate's validation replay never completes (an injected
+    """--allreduce fastest where the RCCL candidate's validation replay never completes (an injected
     device-side stall in front of it, MNIST_AMD_FAULT=rccl_stall): the host watchdog fires, the RCCL
     communicator is aborted (ncclCommAbort) and dropped, the streams drain, and training continues on
     the already-validated xGMI schedule - bitwise equal to --allreduce xgmi, no fatal exit."""
@@ -159,7 +159,7 @@ def test_stuck_rccl_candidate_is_aborted_and_xgmi_kept(cuda_device, monkeypatch)
         monkeypatch.setenv("MNIST_AMD_RCCL_WATCHDOG", "3")
         comm = create_rccl_comm(1, 0, 0)
         assert comm.nonblocking                      # ncclCommInitRankConfig(blocking = 0)
-        ms, t = _world1_trainer(cuda_device, comm, allreduce="auto", probe_world1=True)
+        ms, t = _world1_trainer(cuda_device, comm, allreduce="fastest", probe_world1=True)
         rep = t.transport_report
         assert rep["xgmi"]["ok"] and not rep["rccl"]["ok"], rep
         assert "communicator aborted after" in rep["rccl"]["validation"], rep
