@@ -624,9 +624,11 @@ __device__ __forceinline__ void fc_bwd_role_a(const FcBwdArgs& a, int B, int Bp,
 
 // B: gradient into the conv trunk.  WG = 16 batch rows x 4 consecutive pooled positions x 64 channels
 // (N = 256 columns of dz1 . w1).  The epilogue applies dropout-1 scale/keep and the ReLU (pooled > 0)
-// and writes the *compact* un-pooled gradient: one 192-B record per (image, pooled position) =
-// 64 bf16 pooled gradients + 64 argmax codes (DYC_* in kernels.h).  The conv backward kernels expand
-// it into the dense NHWC tile while staging, so the 75 %-zero dense map never touches HBM.
+// and writes the *compact* un-pooled gradient: one DYC_REC (144-B) record per (image, pooled
+// position) = 64 bf16 pooled gradients (DYC_ROUTE = 128 B) + the 2-bit argmax codes as two bit planes
+// per 8-channel chunk (16 B; layout in kernels.h next to DYC_REC / DYC_ROUTE).  The conv backward
+// kernels expand it into the dense NHWC tile while staging, so the 75 %-zero dense map never touches
+// HBM.
 template <bool CACHE_W>
 __device__ __forceinline__ void fc_bwd_role_b(const FcBwdArgs& a, int B, int Bp, int rb, int MR,
                                               unsigned char* smem) {

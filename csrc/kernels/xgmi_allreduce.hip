@@ -398,7 +398,10 @@ __device__ __forceinline__ void fcu_update(const XgmiArgs& a, const Ada& ad, int
 }  // namespace
 
 template <int W>
-__global__ __launch_bounds__(256, W >= 4 ? 6 : 1) void xgmi_fc_fused_kernel(XgmiArgs a) {
+#ifndef XGMI_FC_W1_MINBLOCKS   // A/B builds only (-DXGMI_FC_W1_MINBLOCKS=6: the VGPR-capped form at W < 4)
+#define XGMI_FC_W1_MINBLOCKS 1
+#endif
+__global__ __launch_bounds__(256, W >= 4 ? 6 : XGMI_FC_W1_MINBLOCKS) void xgmi_fc_fused_kernel(XgmiArgs a) {
   TL_SCOPE(TL_XGMI_FC);
   RW_ENTRY();
   constexpr int PG = 1;                                          // phase-2 units in flight per lane

@@ -168,8 +168,19 @@ def main(argv=None) -> int:
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--timeline", action="store_true", help="debug variant with in-kernel timestamps (_C_tl)")
     ap.add_argument("--race-widen", action="store_true", help="debug variant with race-window widening (_C_rw)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], metavar="NAME[=VALUE]",
+                    help="A/B build: extra preprocessor define (with --out; loaded via MNIST_AMD_EXT_PATH)")
+    ap.add_argument("--out", default=None, help="A/B build: output .so path (own object directory)")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, variant="tl" if a.timeline else "rw" if a.race_widen else "")
+    if a.out:
+        flags = ["-D" + d for d in a.defines] + (["-DMNIST_TIMELINE"] if a.timeline else [])
+        name = "ab_" + "_".join(d.replace("=", "-") for d in a.defines + (["tl"] if a.timeline else []))
+        VARIANTS[name] = (os.path.join(ROOT, "build", "obj_" + name), os.path.abspath(a.out), flags)
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, variant=name)
+    else:
+        out = build(force=a.force, jobs=a.jobs, verbose=a.verbose,
+                    variant="tl" if a.timeline else "rw" if a.race_widen else "")
     print(out)
     return 0
 

@@ -20,14 +20,14 @@ def load(build_if_missing: bool = True):
     global _C, _err
     if _C is not None:
         return _C
+    if os.environ.get("MNIST_AMD_EXT_PATH"):      # A/B runs: another build of the same sources
+        _C = _load_from(os.environ["MNIST_AMD_EXT_PATH"])
+        return _C
     if os.environ.get("MNIST_AMD_TIMELINE") == "1":
         _C = _load_variant("tl", build_if_missing)
         return _C
     if os.environ.get("MNIST_AMD_RACE_WIDEN") == "1":
         _C = _load_variant("rw", build_if_missing)
-        return _C
-    if os.environ.get("MNIST_AMD_EXT_PATH"):      # A/B runs: another build of the same sources
-        _C = _load_from(os.environ["MNIST_AMD_EXT_PATH"])
         return _C
     try:
         _C = importlib.import_module("pytorch_mnist_ddp_amd._C")

@@ -42,13 +42,16 @@ def trainer(dev, B=200, n=2000, graph_steps=3, **kw):
 
 
 def run(ms, t, n, epochs=2):
+    """The trained state: fp32 master weights, optimizer state, logged losses, and (bf16 step) the
+    bf16 weight shadows the next step reads (the fp32 step reads none: its xGMI update does not
+    maintain the fc1 shadows at all, the single-GPU one does - not part of the comparison)."""
     import torch
     idx = torch.randperm(n, generator=torch.Generator().manual_seed(5))
     for ep in range(1, epochs + 1):
         t.train_epoch(ep, idx)
     t.synchronize()
-    return {k: getattr(ms, k).clone() for k in ("param", "square_avg", "acc_delta", "w1", "w1t", "w2f", "w2d")} | \
-        {"loss_log": t.loss_log.clone()}
+    keys = ("param", "square_avg", "acc_delta") + (() if t.fp32 else ("w1", "w1t", "w2f", "w2d"))
+    return {k: getattr(ms, k).clone() for k in keys} | {"loss_log": t.loss_log.clone()}
 
 
 def diff(a, b) -> list[str]:

@@ -97,8 +97,9 @@ def measure(args):
         if args.sched == "rccl":
             comm = create_rccl_comm(1, 0, 0)
         kw = dict(comm=comm, allreduce=args.sched)
+    hooks = dict(h.split("=", 1) for h in args.hook)
     tr = FusedTrainer(ms, train, None, B, 1000, num_samples=max(total * B, 60000), seed=1,
-                      graph_steps=args.graph_steps, **kw)
+                      graph_steps=args.graph_steps, hooks=hooks, **kw)
     tr.start_stream(stream, gather=True)
     tr.precapture(args.warmup)
     tr.precapture(args.steps)
@@ -175,6 +176,8 @@ def product_period(args) -> float | None:
     """The same command's period with the product build (bench.py, host-timed)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup", str(args.warmup),
            "--batch-size", str(args.batch), "--graph-steps", str(args.graph_steps), "--no-full-run"]
+    for h in args.hook:
+        cmd += ["--hook", h]
     if args.sched != "overlap":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes",
                "1", "--nproc-per-node", "1"] + cmd[1:] + ["--force-comm", "--allreduce", args.sched]
@@ -196,6 +199,8 @@ def main() -> int:
     ap.add_argument("--sched", choices=["overlap", "xgmi", "rccl"], default="overlap",
                     help="overlap: single GPU; xgmi / rccl: the world-1 DDP production schedule")
     ap.add_argument("--no-product", action="store_true")
+    ap.add_argument("--hook", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine variant (FusedTrainer.HOOKS), for the timeline and the product run")
     args = ap.parse_args()
     recs, sched = measure(args)
     table, span = analyse(recs, args.steps)
