@@ -569,6 +569,11 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
             "params_in_sync": in_sync,
             "desync_epoch": desync_epoch,
             "total_cost_time_s": script.get("total_cost_time_s") if script else None,
+            # the synthetic split is generated in-process by every run (native generator v3, no disk
+            # cache), so the reference-timer run above IS the cold start; its data phase is reported
+            "total_cost_time_cold_s": script.get("total_cost_time_s") if script else None,
+            "synthetic_data": {"generator": "v3 native (csrc/data/synthetic_gen.cpp)", "disk_cache": None,
+                               "child_data_phase_s": ((script or {}).get("setup_phases_s") or {}).get("data")},
             "reference_script": script,
             "wallclock_20ep_s": round(wall, 3) if wall is not None else None,
             "wallclock_20ep_note": "in-process 20 epochs on the built trainer (state reset): excludes PG init, "

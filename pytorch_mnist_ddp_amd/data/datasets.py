@@ -71,6 +71,5 @@ def load_mnist(root: str = "./data", train: bool = True, synthetic_data: bool | 
             _warned.add(train)
             print(f"[mnist-amd] MNIST {'train' if train else 'test'} IDX files not found under "
                   f"{root}; using deterministic synthetic 28x28 data", file=sys.stderr)
-    cache = os.path.join(root, "synthetic_cache") if root else None
-    images, labels = synthetic.synthetic_mnist(train, synthetic_size, cache_dir=cache)
+    images, labels = synthetic.synthetic_mnist(train, synthetic_size)     # (native, in-process: no cache)
     return MNISTData(images, labels, train, "synthetic")

@@ -155,10 +155,9 @@ def generate_native(n: int, seed: int, label_noise: float = 0.0,
     return images, labels
 
 
-def synthetic_mnist(train: bool, size: int | None = None, cache_dir: str | None = None
-                    ) -> tuple[torch.Tensor, torch.Tensor]:
-    """The synthetic split (generator v3, native: ~20-60 ms for 60k + 10k images, so there is no disk
-    cache - every run generates its data the same way, cold or warm).  ``cache_dir`` is accepted for
-    compatibility and ignored."""
+def synthetic_mnist(train: bool, size: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """The synthetic split (generator v3, native: 40 ms for 60k + 10k images on the GPU box's 16-CPU
+    share, profiles/r6/check1/datagen.txt), so there is no disk cache - every run generates its data
+    the same way, cold or warm."""
     n = size if size is not None else (TRAIN_SIZE if train else TEST_SIZE)
     return generate_native(n, seed=(1 if train else 2) * 7919 + 17, label_noise=LABEL_NOISE if train else 0.0)

@@ -82,6 +82,29 @@ def _hc_worker(rank, world, port, q, mode):
             t.join(60)
             q.put((rank, (main, side.get("h"))))
             time.sleep(2.0)
+        elif mode == "clone":
+            # helper-thread clients are clones of the default store (same key namespace); two channels
+            # of one name never see each other's keys; a default-store abort reaches a clone-channel wait
+            from pytorch_mnist_ddp_amd.parallel.hostcomm import channel, own_store_client
+            c1 = own_store_client()
+            assert c1 is not None
+            a = channel("setup", c1)
+            first = a.gather_strings(f"a{rank}")
+            b = channel("setup", own_store_client())   # a later channel of the same name
+            second = b.gather_strings(f"b{rank}")
+            assert a.prefix != b.prefix
+            if rank == 1:
+                time.sleep(1.0)
+                hc.abort("rank 1 failed in xgmi setup")
+                q.put((rank, (first, second, "aborted")))
+            else:
+                t0 = time.perf_counter()
+                try:
+                    b.barrier(timeout_s=120)
+                    q.put((rank, (first, second, "no error")))
+                except RuntimeError as e:
+                    q.put((rank, (first, second, f"{time.perf_counter() - t0:.1f}|{e}")))
+            time.sleep(3.0)
         else:                                         # rank 1 fails, the others wait in a collective
             if rank == 1:
                 time.sleep(1.0)
@@ -137,3 +160,17 @@ def test_host_collective_channels_are_independent():
         main, helper = res[r]
         assert main == [[f"m{i}r{q}" for q in range(3)] for i in range(8)]
         assert helper == [[f"h{i}r{q}" for q in range(3)] for i in range(8)]
+
+
+def test_helper_channels_share_the_default_namespace_and_abort():
+    """helper-thread store clients are clones of the default store, so their keys
+    and the abort key live in the default store's namespace; every channel instance has its own key
+    prefix (a later channel of the same name never reads an earlier one's leftovers)."""
+    res = _run(3, "clone")
+    for r in range(3):
+        first, second, tail = res[r]
+        assert first == ["a0", "a1", "a2"] and second == ["b0", "b1", "b2"]
+    assert res[1][2] == "aborted"
+    for r in (0, 2):
+        dt, msg = res[r][2].split("|", 1)
+        assert "job aborted by a peer: rank 1 failed in xgmi setup" in msg and float(dt) < 20.0

@@ -7,7 +7,8 @@ Runs ``mnist_ddp.py --batch-size 200 --epochs 20 --synthetic --json-log`` under 
 (``--one-gpu``: every rank on GPU 0 - gloo process group + the xGMI kernels, 2 hardware queues per
 process, as the one-GPU rehearsals; ``--production``: every rank on GPU 0 but the driver's production
 command - default ``nccl`` process group, ``--allreduce auto``, no transport flag - where RCCL cannot
-initialise, two ranks sharing a GPU; ``--cold``: an empty synthetic-data cache per run) and prints, per run, every rank's setup phases (host seconds on
+initialise, two ranks sharing a GPU).  Every run generates its synthetic data in-process (native
+generator, no cache), so each row is a cold start. and prints, per run, every rank's setup phases (host seconds on
 its main thread, in order), their sum (``setup_total_s`` is the max of these over ranks), the xGMI
 communicator's sub-steps and the helper-thread timings, plus the script's ``Total cost time``.
 """
@@ -24,8 +25,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(world: int, one_gpu: bool, extra: list[str], production: bool = False,
-        cold: bool = False) -> tuple[list[dict], float | None, str]:
+def run(world: int, one_gpu: bool, extra: list[str], production: bool = False) -> tuple[list[dict], float | None, str]:
     jlog = tempfile.NamedTemporaryFile(prefix="startup_", suffix=".jsonl", delete=False).name
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes",
            "1", "--nproc-per-node", str(world), os.path.join(ROOT, "mnist_ddp.py"), "--batch-size", "200",
@@ -35,14 +35,7 @@ def run(world: int, one_gpu: bool, extra: list[str], production: bool = False,
         env.update(MNIST_AMD_ONE_GPU="1", GPU_MAX_HW_QUEUES="2")
     if one_gpu and not production:
         cmd += ["--dist-backend", "gloo", "--allreduce", "xgmi"]
-    tmp = None
-    if cold:
-        tmp = tempfile.mkdtemp(prefix="startup_cache_")
-        env["MNIST_AMD_CACHE_DIR"] = tmp
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
-    if tmp:
-        import shutil
-        shutil.rmtree(tmp, ignore_errors=True)
     if r.returncode != 0:
         raise SystemExit(f"world {world}: rc {r.returncode}\n{r.stderr[-3000:]}")
     times = [float(x) for x in re.findall(r"Total cost time:([0-9.eE+-]+) ms", r.stdout)]
@@ -74,14 +67,13 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--one-gpu", action="store_true")
     ap.add_argument("--production", action="store_true")
-    ap.add_argument("--cold", action="store_true")
     ap.add_argument("--out", default=None)
     ap.add_argument("extra", nargs="*")
     args = ap.parse_args()
     lines = ["# Startup inside the reference timer, per phase and rank", ""]
     for w in args.world:
         for rep in range(args.reps):
-            setups, total, cmd = run(w, args.one_gpu, args.extra, args.production, args.cold)
+            setups, total, cmd = run(w, args.one_gpu, args.extra, args.production)
             lines.append(f"`{cmd}` (rep {rep + 1})")
             lines.append("")
             lines += table(w, setups, total)
