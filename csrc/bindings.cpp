@@ -466,6 +466,11 @@ PYBIND11_MODULE(_C, m) {
     }
     return std::string(bus) + "|" + u;
   });
+  m.def("synth_render", [](uintptr_t plan, uintptr_t templates, int64_t n, uintptr_t out, uintptr_t stream) {
+    launch_synth_render(P<const void>(plan), P<const float>(templates), n, P<uint8_t>(out), S(stream));
+    check_launch();
+  }, py::arg("plan"), py::arg("templates"), py::arg("n"), py::arg("out"), py::arg("stream"),
+     "render n synthetic images [n, 784] on the device from a host-made plan (generator v3)");
   m.def("memset_sync", [](uintptr_t ptr, int value, int64_t nbytes) {
     // setup-time buffer initialisation without a torch fill kernel (whose code object would load on
     // first launch inside the reference timer); synchronous

@@ -199,6 +199,9 @@ void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 void launch_set_step(StepState* st, int step, hipStream_t s);
 void launch_set_state(StepState* st, const StepState& v, hipStream_t s);
 // epoch pre-gather: dst rows [start, start+n) = src rows idx[start..start+n) (+ labels)
+// synthetic data generator v3 (csrc/kernels/datagen.hip): render n images [n, 784] from a host plan
+// (n x 96-B synth::Sample records, csrc/data/synth_render.h) and the zero-bordered templates
+void launch_synth_render(const void* plan, const float* templates, int64_t n, uint8_t* out, hipStream_t s);
 void launch_gather_rows(const uint8_t* src_u8, const int32_t* src_labels, const int32_t* idx, int64_t start,
                         int64_t n, uint8_t* dst_u8, int32_t* dst_labels, hipStream_t s);
 // device-counter stream hand-offs (engine DDP schedule 3)

@@ -147,7 +147,7 @@ DATAGEN_OUT = os.path.join(PKG_DIR, "_datagen" + EXT_SUFFIX)
 def build_datagen(force: bool = False, verbose: bool = False) -> str:
     """The synthetic-data generator (``_datagen``: pure C++17 + pybind11, no HIP) - host compiler,
     strict IEEE float evaluation (no contraction) so every build emits the same bytes."""
-    if not force and not _stale(DATAGEN_OUT, [DATAGEN_SRC]):
+    if not force and not _stale(DATAGEN_OUT, [DATAGEN_SRC, os.path.join(CSRC, "data", "synth_render.h")]):
         return DATAGEN_OUT
     cxx = os.environ.get("CXX", "g++")
     cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-ffp-contract=off", "-fno-fast-math",

@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import os
 import sys
-from dataclasses import dataclass
 
 import torch
 
@@ -21,12 +20,25 @@ MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
 
 
-@dataclass
 class MNISTData:
-    images: torch.Tensor   # uint8 [N, 28, 28]
-    targets: torch.Tensor  # int64 [N]
-    train: bool
-    source: str            # "idx:<root>" or "synthetic"
+    """uint8 images [N, 28, 28] + int64 targets [N].  A synthetic split holds its generator plan
+    instead and renders the images on first use (``images``: on the host), or straight into device
+    memory (``device_images``: the fused engine's HBM-resident copy, no host image tensor at all)."""
+
+    def __init__(self, images: torch.Tensor | None, targets: torch.Tensor, train: bool, source: str, plan=None):
+        self._images, self.targets, self.train, self.source, self.plan = images, targets, train, source, plan
+
+    @property
+    def images(self) -> torch.Tensor:
+        if self._images is None:
+            self._images = self.plan.render_cpu()
+        return self._images
+
+    def device_images(self, device) -> torch.Tensor:
+        """uint8 [N, 784] on ``device`` (a synthetic split is rendered there by the generator kernel)."""
+        if self._images is None and self.plan is not None:
+            return self.plan.render_device(device)
+        return self.images.reshape(len(self), -1).contiguous().to(device)
 
     def __len__(self) -> int:
         return int(self.targets.shape[0])
@@ -71,5 +83,5 @@ def load_mnist(root: str = "./data", train: bool = True, synthetic_data: bool | 
             _warned.add(train)
             print(f"[mnist-amd] MNIST {'train' if train else 'test'} IDX files not found under "
                   f"{root}; using deterministic synthetic 28x28 data", file=sys.stderr)
-    images, labels = synthetic.synthetic_mnist(train, synthetic_size)     # (native, in-process: no cache)
-    return MNISTData(images, labels, train, "synthetic")
+    plan = synthetic.synthetic_plan(train, synthetic_size)     # (native, in-process: no cache)
+    return MNISTData(None, plan.labels, train, "synthetic", plan=plan)

@@ -115,21 +115,35 @@ def generate(n: int, seed: int, templates: torch.Tensor | None = None, chunk: in
 
 GENERATOR_VERSION = 3
 
+# difficulty knobs of the v3 recipe (csrc/data/synthetic_gen.cpp: Params)
+DEFAULT_PARAMS = {
+    "jitter": 1.6, "sigma0": 0.9, "sigma1": 0.7,        # templates: control-point jitter, stroke sigma
+    "rot_deg": 12.0, "scale": 0.3, "shear": 0.3,         # warps
+    "overlay": 0.6,                                      # other-class stroke strength (x u^2)
+    "gain0": 0.6, "gain1": 0.4,                          # gain
+    "nthr": 0.55, "namp": 0.25,                          # speckle
+}
+
 
 def _threads() -> int:
     """Generator threads: this process's CPU share (OMP_NUM_THREADS when the launcher set one - the
-    GPU box's 16 - else the affinity mask), at most 16."""
+    GPU box's 16 - else the affinity mask, at most 16) split among the node's ranks (LOCAL_WORLD_SIZE):
+    the ranks generate concurrently and would otherwise oversubscribe the share."""
     import os
     try:
         n = int(os.environ.get("OMP_NUM_THREADS", "0"))
     except ValueError:
         n = 0
-    if n <= 0:
+    if n <= 1:
         try:
             n = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
             n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+    try:
+        local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    except ValueError:
+        local = 1
+    return max(1, min(n, 16) // local)
 
 
 def _datagen():
@@ -143,21 +157,68 @@ def _datagen():
         return importlib.import_module("pytorch_mnist_ddp_amd._datagen")
 
 
-def generate_native(n: int, seed: int, label_noise: float = 0.0,
-                    template_seed: int = TEMPLATE_SEED) -> tuple[torch.Tensor, torch.Tensor]:
-    """Generator v3: (uint8 [n,28,28], int64 [n]) from the native multi-threaded generator - every
-    sample a pure function of (seed, index), so any thread count gives the same bytes."""
-    images = torch.empty(n, IMG, IMG, dtype=torch.uint8)
-    labels = torch.empty(n, dtype=torch.int64)
-    if n:
-        _datagen().generate(n, seed, template_seed, float(label_noise), images.data_ptr(), labels.data_ptr(),
-                            _threads())
-    return images, labels
+class SynthPlan:
+    """Generator v3 split: the per-sample plan (uint8 [n, 96]: warps, strengths, template indices,
+    crop, noise key - csrc/data/synth_render.h ``synth::Sample``), the labels and the zero-bordered
+    templates.  ``render_cpu()`` / ``render_device()`` turn it into the uint8 images, with the same
+    bytes on the host and on the GPU."""
+
+    def __init__(self, n: int, seed: int, label_noise: float = 0.0, template_seed: int = TEMPLATE_SEED,
+                 params: dict | None = None):
+        D = _datagen()
+        p = dict(DEFAULT_PARAMS, **(params or {}))
+        self.n = int(n)
+        self.templates = torch.empty(D.TEMPLATE_FLOATS, dtype=torch.float32)
+        D.templates(template_seed, p, self.templates.data_ptr())
+        self.plan = torch.empty(self.n, D.SAMPLE_BYTES, dtype=torch.uint8)
+        self.labels = torch.empty(self.n, dtype=torch.int64)
+        if self.n:
+            D.plan(self.n, seed, float(label_noise), p, self.plan.data_ptr(), self.labels.data_ptr(), _threads())
+
+    def render_cpu(self) -> torch.Tensor:
+        """uint8 [n, 28, 28] on the host (threads)."""
+        images = torch.empty(self.n, IMG, IMG, dtype=torch.uint8)
+        if self.n:
+            _datagen().render(self.plan.data_ptr(), self.templates.data_ptr(), self.n, images.data_ptr(),
+                              _threads())
+        return images
+
+    def render_device(self, device) -> torch.Tensor:
+        """uint8 [n, 784] rendered on ``device`` by csrc/kernels/datagen.hip (the plan and templates
+        go up: 7.7 MB instead of the 55 MB of images), ordered on the current stream."""
+        from ..ops import native
+        C = native.load()
+        out = torch.empty(self.n, IMG * IMG, dtype=torch.uint8, device=device)
+        if self.n:
+            plan = self.plan.to(device, non_blocking=False)
+            tmpl = self.templates.to(device, non_blocking=False)
+            C.synth_render(plan.data_ptr(), tmpl.data_ptr(), self.n, out.data_ptr(),
+                           torch.cuda.current_stream(device).cuda_stream)
+            torch.cuda.current_stream(device).synchronize()     # (plan / tmpl are freed on return)
+        return out
+
+
+def generate_native(n: int, seed: int, label_noise: float = 0.0, template_seed: int = TEMPLATE_SEED,
+                    params: dict | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """Generator v3 on the host: (uint8 [n,28,28], int64 [n]) - every sample a pure function of
+    (seed, index), so any thread count gives the same bytes."""
+    pl = SynthPlan(n, seed, label_noise, template_seed, params)
+    return pl.render_cpu(), pl.labels
+
+
+def split_seed(train: bool) -> int:
+    return (1 if train else 2) * 7919 + 17
+
+
+def synthetic_plan(train: bool, size: int | None = None, params: dict | None = None) -> SynthPlan:
+    """The synthetic split's plan (generator v3): the labels at once, the images rendered on demand -
+    on the host, or by the fused engine straight into HBM.  Every run generates its data the same way
+    (no disk cache), cold or warm."""
+    n = size if size is not None else (TRAIN_SIZE if train else TEST_SIZE)
+    return SynthPlan(n, split_seed(train), LABEL_NOISE if train else 0.0, params=params)
 
 
 def synthetic_mnist(train: bool, size: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-    """The synthetic split (generator v3, native: 40 ms for 60k + 10k images on the GPU box's 16-CPU
-    share, profiles/r6/check1/datagen.txt), so there is no disk cache - every run generates its data
-    the same way, cold or warm."""
-    n = size if size is not None else (TRAIN_SIZE if train else TEST_SIZE)
-    return generate_native(n, seed=(1 if train else 2) * 7919 + 17, label_noise=LABEL_NOISE if train else 0.0)
+    """The synthetic split rendered on the host: (uint8 [n,28,28], int64 [n])."""
+    pl = synthetic_plan(train, size)
+    return pl.render_cpu(), pl.labels

@@ -155,7 +155,7 @@ class FusedTrainer:
         # thread's self-test - so these two are the process's first and keep their own hardware queues)
         self.compute, self.comm_stream = streams if streams is not None else make_streams(dev)
         # ---- device-resident data
-        self.train_u8 = train.images.reshape(len(train), -1).contiguous().to(dev)
+        self.train_u8 = train.device_images(dev)              # (synthetic: rendered on the device)
         self.train_labels = train.targets.to(torch.int32).to(dev)
         z = native.zeros                                     # hipMemset: no torch fill kernel
         self.train_idx = z(self.steps_per_epoch * self.B, torch.int32, dev)
@@ -165,7 +165,7 @@ class FusedTrainer:
         self.loss_log = z(max(self.steps_per_epoch, 1), torch.float32, dev)
         self.n_test = len(test) if test is not None else 0
         if test is not None:
-            self.test_u8 = test.images.reshape(self.n_test, -1).contiguous().to(dev)
+            self.test_u8 = test.device_images(dev)
             self.test_labels = test.targets.to(torch.int32).to(dev)
             self.test_idx = torch.arange(self.n_test, dtype=torch.int32).to(dev)
             self.test_loss_rows = z(self.n_test, torch.float32, dev)
