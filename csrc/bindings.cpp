@@ -466,6 +466,26 @@ PYBIND11_MODULE(_C, m) {
     }
     return std::string(bus) + "|" + u;
   });
+  // raw HIP streams for the engine: "dedicated" = hipExtStreamCreateWithCUMask over every CU (the
+  // runtime gives a CU-masked stream a hardware queue of its own instead of sharing a pooled one),
+  // else hipStreamCreateWithPriority(non-blocking, priority)
+  m.def("create_stream", [](int device, bool dedicated, int priority) {
+    if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("create_stream: hipSetDevice failed");
+    hipStream_t st = nullptr;
+    if (dedicated) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        throw std::runtime_error("create_stream: CU count");
+      std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+      if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        throw std::runtime_error("hipExtStreamCreateWithCUMask failed");
+    } else if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, priority) != hipSuccess) {
+      throw std::runtime_error("hipStreamCreateWithPriority failed");
+    }
+    return reinterpret_cast<uintptr_t>(st);
+  }, py::arg("device"), py::arg("dedicated") = true, py::arg("priority") = 0);
+  m.def("destroy_stream", [](uintptr_t s) { (void)hipStreamDestroy(S(s)); });
   m.def("synth_render", [](uintptr_t plan, uintptr_t templates, int64_t n, uintptr_t out, uintptr_t stream) {
     launch_synth_render(P<const void>(plan), P<const float>(templates), n, P<uint8_t>(out), S(stream));
     check_launch();

@@ -119,7 +119,10 @@ GENERATOR_VERSION = 3
 DEFAULT_PARAMS = {
     "jitter": 1.6, "sigma0": 0.9, "sigma1": 0.7,        # templates: control-point jitter, stroke sigma
     "rot_deg": 12.0, "scale": 0.3, "shear": 0.3,         # warps
-    "overlay": 0.6,                                      # other-class stroke strength (x u^2)
+    # other-class stroke strength (x u^2): 0.85 puts a converged CNN at 99.34 % test accuracy after
+    # the README's 20 epochs, v2's regime (0.6: 99.97 %, 0.9: 98.93 %; tools/synth_difficulty.py,
+    # profiles/r6/difficulty/)
+    "overlay": 0.85,
     "gain0": 0.6, "gain1": 0.4,                          # gain
     "nthr": 0.55, "namp": 0.25,                          # speckle
 }

@@ -454,9 +454,14 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
         setup.mark(f"epoch{epoch}_train")
         if epoch == 1:                     # the trainer's phases include epoch 1's graph captures
             setup.update(trainer.setup, prefix="trainer.")
+            # (t_start_unix / trainer_ready_unix: the node's wall clock at the timer's start and when the
+            # trainer was ready, so a multi-rank table can separate the launcher's start skew between
+            # ranks - which the first collective absorbs - from the startup's own critical path)
             _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
                                       "setup_info": setup.info, "allreduce": trainer.allreduce if distributed else None,
-                                      "transport_report": trainer.transport_report or None})
+                                      "transport_report": trainer.transport_report or None,
+                                      "t_start_unix": setup.origin,
+                                      "trainer_ready_unix": setup.origin + setup.marks.get("trainer", 0.0)})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,
                "img_per_s": st.samples / max(st.train_seconds, 1e-9)}
         handle = None

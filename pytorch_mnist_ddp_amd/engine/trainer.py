@@ -107,10 +107,28 @@ class StartupValidationError(RuntimeError):
         self.setup = setup
 
 
+_ENGINE_STREAMS: dict[int, tuple] = {}
+
+
 def make_streams(dev) -> tuple:
-    """The trainer's compute and (high-priority) comm streams."""
-    # (comm at normal priority, or compute raised instead: 600 steps within noise, profiles/r5/ab/stream_priority.txt)
-    return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev, priority=-1)
+    """The trainers' compute and comm streams: one process-wide pair per device, each on a HARDWARE
+    QUEUE OF ITS OWN (``_C.create_stream``: a CU-masked stream over every CU, which the HIP runtime
+    never shares with another stream).  Streams from torch's pool or plain ``hipStreamCreate`` land
+    on a pooled queue (GPU_MAX_HW_QUEUES per process, 4 by default); once a process holds more streams
+    than that, a new stream shares a queue with an older one, and a trainer whose streams share queues
+    ran its step 4.6x slower (63 -> 290 us at B = 200: ``tools/queue_mapping.py``,
+    profiles/r6/queues/) - the bimodal slow mode seen in round 5 (docs/DEBUGGING.md).  Trainers of one
+    process run one after another on the same pair (each chunk ends joined, so nothing of one trainer
+    is left in flight when the next one enqueues)."""
+    dev = torch.device(dev)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    pair = _ENGINE_STREAMS.get(key)
+    if pair is None:
+        C = native.load()
+        pair = tuple(torch.cuda.ExternalStream(C.create_stream(key, True, 0), device=torch.device("cuda", key))
+                     for _ in range(2))
+        _ENGINE_STREAMS[key] = pair
+    return pair
 
 
 class FusedTrainer:

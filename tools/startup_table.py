@@ -44,10 +44,24 @@ def run(world: int, one_gpu: bool, extra: list[str], production: bool = False) -
     return [x for x in recs if "setup_s" in x], max(times) if times else None, " ".join(cmd[3:])
 
 
+def critical(setups: list[dict]) -> tuple[float | None, float | None]:
+    """(launch skew = last rank's timer start - first rank's, startup critical path = last rank ready -
+    last rank's start): the first collective makes every earlier-started rank wait out the skew, which
+    the launcher (process start, `import torch`), not the startup, decides."""
+    if not all("t_start_unix" in x and "trainer_ready_unix" in x for x in setups):
+        return None, None
+    t0 = [x["t_start_unix"] for x in setups]
+    t1 = [x["trainer_ready_unix"] for x in setups]
+    return max(t0) - min(t0), max(t1) - max(t0)
+
+
 def table(world: int, setups: list[dict], total: float | None) -> list[str]:
     keys = list(dict.fromkeys(k for x in setups for k in x["setup_s"]))
+    skew, crit = critical(setups)
+    extra = (f"; launch skew {skew:.3f} s, critical path from the last rank's start {crit:.3f} s"
+             if skew is not None else "")
     out = [f"### world {world}: Total cost time {total:.3f} s, setup_total_s (max over ranks) "
-           f"{max(sum(x['setup_s'].values()) for x in setups):.3f} s", "",
+           f"{max(sum(x['setup_s'].values()) for x in setups):.3f} s{extra}", "",
            "| phase | " + " | ".join(f"rank {i}" for i in range(len(setups))) + " |",
            "|---|" + "---|" * len(setups)]
     for k in keys:
