@@ -336,12 +336,24 @@ __device__ __forceinline__ void dgrad_compute_p(const ConvBwdArgs& a, int strip,
   if constexpr (!PRE) dgrad_mask_load(a, strip, b, wave, own);
   const DgMask& mk = PRE ? pre : own;
   prefetch();
+#ifdef DG_UB_AREUSE   // A/B upper bound only (wrong results): one A read per tap row, reused for c = 1, 2
+  bf16x8 Arow[2][MT];
+#endif
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) {
     const int t = ks >> 1, h = ks & 1, d = t / 3, c = t % 3;
     bf16x8 A[MT], Bf[2];
+#ifdef DG_UB_AREUSE
+    if (c == 0 && (DG_UB_AREUSE == 1 || t == 0)) {   // (=2: one A read for the whole loop)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) Arow[h][i] = ld16(abase[i][c][h ^ (d & 1)] + (2 - d) * DG_PITCH * C2);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) A[i] = Arow[h][i];
+#else
 #pragma unroll
     for (int i = 0; i < MT; ++i) A[i] = ld16(abase[i][c][h ^ (d & 1)] + (2 - d) * DG_PITCH * C2);
+#endif
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) Bf[nt] = ld16(bbase[h] + (t * C1 + nt * 16) * C2);
 #pragma unroll

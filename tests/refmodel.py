@@ -28,10 +28,12 @@ def reference_forward(net, x, mask1=None, mask2=None, train=True):
     return F.log_softmax(x, dim=1)
 
 
-def reference_step(net, images_u8, labels, mask1=None, mask2=None):
-    net = copy.deepcopy(net).cpu().float()
+def reference_step(net, images_u8, labels, mask1=None, mask2=None, dtype=torch.float32):
+    net = copy.deepcopy(net).cpu().to(dtype)
     net.zero_grad(set_to_none=True)
-    x = normalize_u8(images_u8)
+    x = normalize_u8(images_u8).to(dtype)
+    mask1 = mask1.to(dtype) if mask1 is not None else None
+    mask2 = mask2.to(dtype) if mask2 is not None else None
     out = reference_forward(net, x, mask1, mask2)
     loss = F.nll_loss(out, labels.long())
     loss.backward()

@@ -3,8 +3,9 @@
 The reference trains in fp32 (mnist_ddp.py:49-73); this engine keeps every activation, gradient
 operand and parameter in fp32 and runs the GEMM-shaped work on gfx950's f32-input MFMA
 (v_mfma_f32_16x16x4_f32, exact fp32 products).  Against torch's fp32 CPU ops the only differences
-are summation orders (and the max-pool routing of near ties), so the tolerances here are 3e-4
-relative (conv1.weight at B = 1100 sums 743,600 products per element: 1.07e-4 measured) - two orders of magnitude tighter than the bf16 engine's tests (test_gpu_numerics.py).
+are summation orders (and the max-pool routing of near ties), so the gradients are held to the float64
+gradient within 3e-4 relative, or within 3x torch fp32's own error where cancellation makes that
+larger (conv1.bias: 6.7e-4 against torch fp32 on the round-6 synthetic data) - two orders of magnitude tighter than the bf16 engine's tests (test_gpu_numerics.py).
 """
 import copy
 import os
@@ -64,10 +65,14 @@ def test_fp32_step_gradients_match_torch_fp32(cuda_device, B, dropout):
         m1 = _keep_mask(t.seed, 0, B * 9216, 192).view(B, 64, 12, 12)
         m2 = _keep_mask(t.seed, 1, B * 128, 128).view(B, 128)
     loss_ref, _, g_ref = reference_step(ref, imgs, labels, m1, m2)
+    _, _, g64 = reference_step(ref, imgs, labels, m1, m2, dtype=torch.float64)
     grads = ms.views(ms.grad)
     for n, g in g_ref.items():
-        e = rel_err(grads[n], g)
-        assert e < 3e-4, (n, e)
+        # against the float64 gradient: as accurate as torch's own fp32 CPU step (a gradient that
+        # is a small sum of many cancelling terms - conv1.bias - has a large relative error in
+        # either), and within 3e-4 of it otherwise
+        e, e_torch = rel_err(grads[n], g64[n]), rel_err(g, g64[n])
+        assert e < max(3e-4, 3.0 * e_torch), (n, e, e_torch)
     assert abs(t.loss_log[0].item() - loss_ref.item()) < 1e-5 * max(1.0, abs(loss_ref.item()))
     assert ms.get_step() == 1 and all(torch.isfinite(v).all() for v in ms.views(ms.param).values())
 
