@@ -368,6 +368,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_rccl_handoff", &Engine::set_rccl_handoff)
       .def_property("fc_dw1_side", &Engine::fc_dw1_side, &Engine::set_fc_dw1_side)
       .def_property("w1t_pingpong", &Engine::w1t_pingpong, &Engine::set_w1t_pingpong)
+      .def_property("c1_lanes", &Engine::c1_lanes, &Engine::set_c1_lanes)
       .def("fault_hold", &Engine::fault_hold)
       .def("fault_release", [](Engine& e, uintptr_t stream) { e.fault_release(S(stream)); })
       .def("set_schedule", &Engine::set_schedule, py::call_guard<py::gil_scoped_release>())

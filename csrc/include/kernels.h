@@ -192,6 +192,9 @@ void launch_adadelta(const AdadeltaArgs& a, int region, hipStream_t s, int grid 
 void launch_adadelta_reduce(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 // conv-only form restricted to reduce parts [lo, hi) (conv_grad_reduce.h partition)
 void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, int lo, int hi, hipStream_t s);
+// the conv1 parts [RED_W2_PARTS, RED_ALL_PARTS) of that launch, bitwise equal, on 80 one-wave workgroups
+// (one float4 column each, the slice tree on cross-lane moves)
+void launch_adadelta_c1(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s);
 // Refresh bf16 shadows from fp32 params without an update (after load_state_dict / broadcast).
 void launch_refresh_shadows(const AdadeltaArgs& a, hipStream_t s);
 

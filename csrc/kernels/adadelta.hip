@@ -187,6 +187,85 @@ void launch_adadelta_reduce_parts(const AdadeltaArgs& a, const ConvBwdArgs& c, i
   hipLaunchKernelGGL(adadelta_reduce_kernel, dim3(hi - lo), dim3(256), 0, s, a, c, B, 1, lo);
 }
 
+// conv1's reduce + update (the conv1 parts of adadelta_reduce_kernel, bitwise equal) on 80 one-wave
+// workgroups: workgroup = one float4 column of the 320 conv1 gradient values, lane = slab slice.  Each
+// lane sums rows slice, slice + 64, ... as the 256-thread parts do, and the fixed tree over the 64
+// slices (slice s += slice s + w, w = 32 .. 1) runs on cross-lane moves instead of LDS round trips
+// and barriers; the step's last compute launch at small batches, so its 20 x 4 KB-per-CU load bursts
+// became 80 x 1 KB and its six barriers none.
+__global__ __launch_bounds__(64) void adadelta_c1_kernel(AdadeltaArgs a, ConvBwdArgs c) {
+  TL_SCOPE(TL_RED_CONV1);
+  const int col = blockIdx.x, sl = threadIdx.x;
+  if (a.state_inc && !a.hold_a && col == 0 && sl == 0) a.state_inc->step += 1;
+  RW_ENTRY();
+  const int nslab = c.c1red ? C1_PRE_SLABS : c.c1_rows;
+  const float4* src = reinterpret_cast<const float4*>(c.c1red ? c.c1red : c.c1part) + col;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 t = z4;
+  int64_t e[4];
+  float pp[4], ps[4], pa[4], lr = 0.f;
+  bool first = true;
+  auto pre = [&] {                        // the update's operands, in flight with the slab loads
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 4 * col + r, ci = j / 10, kk = j - ci * 10;
+      e[r] = kk < 9 ? (int64_t)OFF_CONV1_W + ci * 9 + kk : (int64_t)OFF_CONV1_B + ci;
+      pp[r] = a.param[e[r]];
+      ps[r] = a.square_avg[e[r]];
+      pa[r] = a.acc_delta[e[r]];
+    }
+    lr = *a.lr;
+  };
+  for (int k0 = sl; k0 < nslab; k0 += 64 * 16) {
+    float4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int r = k0 + 64 * k;
+      v[k] = src[(int64_t)(r < nslab ? r : 0) * 80];
+    }
+    if (first) pre();
+    first = false;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k0 + 64 * k >= nslab) v[k] = z4;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w; }
+  }
+  if (first) pre();
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {     // lanes >= w compute values nobody reads
+    t.x += __shfl_down(t.x, w, 64);
+    t.y += __shfl_down(t.y, w, 64);
+    t.z += __shfl_down(t.z, w, 64);
+    t.w += __shfl_down(t.w, w, 64);
+  }
+  if (sl == 0) {
+    const float sc = c.grad_scale;
+    const float o[4] = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
+    const Ada ad{a.rho, a.eps, a.weight_decay, lr};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float p = pp[r], sq = ps[r], acc = pa[r];
+      c.grad[e[r]] = o[r];                // the flat gradient buffer stays complete (p.grad views)
+      ad.step(p, o[r], sq, acc);
+      a.param[e[r]] = p;
+      a.square_avg[e[r]] = sq;
+      a.acc_delta[e[r]] = acc;
+    }
+  }
+  // as adadelta_reduce_kernel: the launch completes only once the comm stream has published this
+  // step's conv2 update, then the step index advances
+  if (a.hold_a && col == gridDim.x - 1 && sl == 0) {
+    spin_until_geq(a.hold_a, __hip_atomic_load(a.hold_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hold_err);
+    if (a.state_inc) a.state_inc->step += 1;
+  }
+}
+
+void launch_adadelta_c1(const AdadeltaArgs& a, const ConvBwdArgs& c, int B, hipStream_t s) {
+  (void)B;
+  hipLaunchKernelGGL(adadelta_c1_kernel, dim3(80), dim3(64), 0, s, a, c);
+}
+
 static int adadelta_grid(int region) {
   if (region == ADA_FC) return FC1_TILES + 1;
   if (region == ADA_CONV) return CONV_WGS;

@@ -513,7 +513,10 @@ void Engine::enqueue_step(int batch, bool last) {
       u1.hold_a = sync_ + 3;
       u1.hold_b = sync_ + 4;
       u1.hold_err = sync_ + 2;
-      launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
+      if (c1_lanes_)
+        launch_adadelta_c1(u1, cb, B, compute_);
+      else
+        launch_adadelta_reduce_parts(u1, cb, B, RED_W2_PARTS, RED_ALL_PARTS, compute_);
     }
     phase_end();
     w2d_in_alt_ = !w2d_in_alt_;

@@ -99,6 +99,10 @@ class Engine {
   // test hook: the second w1t copy (fc update beside fc_bwd role B); off reintroduces the race it fixes
   void set_w1t_pingpong(bool on) { w1t_pingpong_ = on; }
   bool w1t_pingpong() const { return w1t_pingpong_; }
+  // single-GPU OVERLAP step tail: conv1's reduce + update on 80 one-wave workgroups (1) or as the 20
+  // conv1 parts of the 256-thread reduce launch (0); bitwise equal (A/B hook)
+  void set_c1_lanes(bool on) { c1_lanes_ = on; }
+  bool c1_lanes() const { return c1_lanes_; }
   // Selects the schedule (checks its transport is attached), waits for all streams and zeroes the
   // hand-off counters and their error flag, so a schedule never inherits another's counts (e.g. an
   // aborted validation).  Detaching the xgmi communicator of the XGMI schedule unsets the schedule.
@@ -170,6 +174,7 @@ class Engine {
   bool rccl_handoff_ = false;
   bool fc_dw1_side_ = true;
   bool w1t_pingpong_ = true;
+  bool c1_lanes_ = true;
   int idx_stride_ = 0;
   int sched_ = SERIAL;
   std::shared_ptr<RcclComm> comm_;

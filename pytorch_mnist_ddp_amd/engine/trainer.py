@@ -264,6 +264,9 @@ class FusedTrainer:
         # the second w1t copy; 0 = the fc update overwrites the w1t fc_bwd role B reads (a known race,
         # for the race-window widening check only - never a product setting)
         "w1t_pingpong": "fc update writes the other w1t copy (1) or the one role B reads (0: the old race)",
+        # single-GPU OVERLAP step tail: conv1's reduce + update on 80 one-wave workgroups (1) or the
+        # 20 conv1 parts of the 256-thread reduce launch (0); bitwise equal either way
+        "c1_lanes": "conv1 reduce + update on one-wave workgroups (1) or the 256-thread parts (0)",
     }
 
     def apply_hooks(self, hooks: dict) -> None:
@@ -276,6 +279,8 @@ class FusedTrainer:
                 self.C.set_dgrad_grid(int(v))
             elif k == "w1t_pingpong":
                 self.engine.w1t_pingpong = bool(int(v))
+            elif k == "c1_lanes":
+                self.engine.c1_lanes = bool(int(v))
             else:
                 raise ValueError(f"unknown engine hook {k!r} (known: {sorted(self.HOOKS)})")
 
