@@ -59,7 +59,7 @@ if ROOT not in sys.path:
 from pytorch_mnist_ddp_amd.data.datasets import load_mnist  # noqa: E402
 from pytorch_mnist_ddp_amd.data.samplers import DistributedIndexStream  # noqa: E402
 from pytorch_mnist_ddp_amd.engine.state import ModelState  # noqa: E402
-from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer  # noqa: E402
+from pytorch_mnist_ddp_amd.engine.trainer import FusedTrainer, stream_kind  # noqa: E402
 from pytorch_mnist_ddp_amd.models.net import Net  # noqa: E402
 from pytorch_mnist_ddp_amd.parallel.distributed import (_max_over_ranks, barrier,  # noqa: E402
                                                         params_fingerprint_equal, start_rccl_comm)
@@ -447,7 +447,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                  "xgmi_ordering": tr.xgmi.ordering if tr.xgmi is not None else None,
                  "xgmi_grids": ({k: v for k, v in tr.xgmi.grids.items() if not k.startswith("cap")}
                                 if tr.xgmi is not None else None),
-                 "schedule": ["serial", "overlap", "rccl", "xgmi"][tr.engine.schedule]}
+                 "schedule": ["serial", "overlap", "rccl", "xgmi"][tr.engine.schedule],
+                 "streams": stream_kind()}
     phases.update(tr.setup, prefix="trainer.")
     # bimodal-slowdown guard (docs/DEBUGGING.md): the timed window against the same schedule's startup
     # validation replay (max over ranks, dropout off); > 1.25x flags a slow mode loudly

@@ -110,6 +110,19 @@ class StartupValidationError(RuntimeError):
 _ENGINE_STREAMS: dict[int, tuple] = {}
 
 
+def under_profiler() -> bool:
+    """The process runs under rocprofv3 (its ``ROCPROF_*`` environment).  rocprofv3 segfaults in its
+    exit-time teardown (``__cxa_finalize``, after every kernel ran and the bench line was printed, so
+    the trace is lost) in a process that created CU-masked streams (profiles/r6/final/prof_b200_cumask.log);
+    profiled runs therefore use plain non-blocking streams, which get queues of their own anyway while
+    the process holds fewer streams than GPU_MAX_HW_QUEUES (one trainer: two)."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def stream_kind() -> str:
+    return "plain (rocprofv3)" if under_profiler() else "cu_masked"
+
+
 def make_streams(dev) -> tuple:
     """The trainers' compute and comm streams: one process-wide pair per device, each on a HARDWARE
     QUEUE OF ITS OWN (``_C.create_stream``: a CU-masked stream over every CU, which the HIP runtime
@@ -125,7 +138,8 @@ def make_streams(dev) -> tuple:
     pair = _ENGINE_STREAMS.get(key)
     if pair is None:
         C = native.load()
-        pair = tuple(torch.cuda.ExternalStream(C.create_stream(key, True, 0), device=torch.device("cuda", key))
+        dedicated = not under_profiler()
+        pair = tuple(torch.cuda.ExternalStream(C.create_stream(key, dedicated, 0), device=torch.device("cuda", key))
                      for _ in range(2))
         _ENGINE_STREAMS[key] = pair
     return pair
