@@ -119,8 +119,13 @@ def under_profiler() -> bool:
     return any(k.startswith("ROCPROF") for k in os.environ)
 
 
+_STREAM_FALLBACK: list[str] = []
+
+
 def stream_kind() -> str:
-    return "plain (rocprofv3)" if under_profiler() else "cu_masked"
+    if under_profiler():
+        return "plain (rocprofv3)"
+    return f"plain (CU-masked stream failed: {_STREAM_FALLBACK[0]})" if _STREAM_FALLBACK else "cu_masked"
 
 
 def make_streams(dev) -> tuple:
@@ -139,8 +144,16 @@ def make_streams(dev) -> tuple:
     if pair is None:
         C = native.load()
         dedicated = not under_profiler()
-        pair = tuple(torch.cuda.ExternalStream(C.create_stream(key, dedicated, 0), device=torch.device("cuda", key))
-                     for _ in range(2))
+
+        def one():
+            try:
+                return C.create_stream(key, dedicated, 0)
+            except RuntimeError as e:              # (a runtime without CU-masked queues: plain stream)
+                if not dedicated:
+                    raise
+                _STREAM_FALLBACK.append(str(e))
+                return C.create_stream(key, False, 0)
+        pair = tuple(torch.cuda.ExternalStream(one(), device=torch.device("cuda", key)) for _ in range(2))
         _ENGINE_STREAMS[key] = pair
     return pair
 
