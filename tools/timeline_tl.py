@@ -35,7 +35,8 @@ COMM = {"ada_fc", "conv2 reduce+update", "stream_wait", "stream_signal", "xgmi_f
 
 
 def clusters(recs):
-    """Wave records [(kid, t0, t1)] -> per kid a list of launches (start, end, waves)."""
+    """Wave records [(kid, t0, t1)] -> per kid a list of launches (start, end, waves, wave durations,
+    wave start offsets)."""
     by = {}
     for kid, t0, t1 in recs:
         by.setdefault(kid, []).append((t0, t1))
@@ -48,10 +49,12 @@ def clusters(recs):
             if cur is None or t0 > cur[1]:
                 if cur is not None:
                     res.append(cur)
-                cur = [t0, t1, 1]
+                cur = [t0, t1, 1, [], []]
             else:
                 cur[1] = max(cur[1], t1)
                 cur[2] += 1
+            cur[3].append(t1 - t0)                       # wave durations
+            cur[4].append(t0 - cur[0])                   # wave start offsets in the launch
         res.append(cur)
         out[kid] = res
     return out
@@ -123,21 +126,29 @@ def analyse(recs, steps):
         raise SystemExit(f"expected {steps} trunk_fwd launches, got {len(trunk)}")
     starts = [c[0] for c in trunk]
     period = (starts[-1] - starts[0]) / (len(starts) - 1) / 100.0      # ticks of 10 ns -> us
-    rows = {}
+    rows, wstat = {}, {}
     for kid, launches in cl.items():
-        for s, e, w in launches:
+        for s, e, w, wd, ws in launches:
             i = max(j for j in range(len(starts)) if starts[j] <= s) if s >= starts[0] else -1
             if i < 1:                                    # skip the first step (ramp from idle)
                 continue
             rows.setdefault(kid, []).append(((s - starts[i]) / 100.0, (e - starts[i]) / 100.0, w))
+            d = wstat.setdefault(kid, ([], []))
+            d[0].extend(wd)
+            d[1].append(sorted(ws)[int(0.9 * (len(ws) - 1))])
     table = []
     for kid, v in sorted(rows.items(), key=lambda kv: sum(x[0] for x in kv[1]) / len(kv[1])):
         n = len(v)
         st = sum(x[0] for x in v) / n
         en = sum(x[1] for x in v) / n
+        wd, ws = wstat[kid]
+        wd = sorted(wd)
         table.append({"kernel": NAMES[kid] if kid < len(NAMES) else str(kid), "launches": n,
                       "start_us": round(st, 2), "end_us": round(en, 2), "dur_us": round(en - st, 2),
-                      "waves": round(sum(x[2] for x in v) / n, 1)})
+                      "waves": round(sum(x[2] for x in v) / n, 1),
+                      "wave_p50_us": round(wd[len(wd) // 2] / 100.0, 2),
+                      "wave_p90_us": round(wd[int(0.9 * (len(wd) - 1))] / 100.0, 2),
+                      "start_p90_us": round(sum(ws) / len(ws) / 100.0, 2)})
     span = {"period_us": round(period, 2), "steps": len(starts),
             "step_periods_us": [round((b - a) / 100.0, 1) for a, b in zip(starts, starts[1:])]}
     ends = [c[1] for launches in cl.values() for c in launches]
@@ -146,7 +157,7 @@ def analyse(recs, steps):
     # starts before the second trunk_fwd, relative to the first trunk_fwd start
     first = []
     for kid, launches in cl.items():
-        for s, e, w in launches:
+        for s, e, w, _, _ in launches:
             if s < starts[1]:
                 first.append((round((s - starts[0]) / 100.0, 2), round((e - starts[0]) / 100.0, 2),
                               NAMES[kid] if kid < len(NAMES) else str(kid)))
@@ -211,10 +222,12 @@ def main() -> int:
              f"(timeline build); product build, same command: {round(prod, 2) if prod else 'n/a'} us/step", "",
              f"device window (first trunk_fwd start to last kernel end): {span['window_us']} us for "
              f"{span['steps']} steps; step periods: {span['step_periods_us']}", "",
-             "| kernel | stream | launches | start us | end us | duration us | waves |", "|---|---|---|---|---|---|---|"]
+             "| kernel | stream | launches | start us | end us | duration us | waves | wave p50 / p90 us | "
+             "90 % of waves started by us |", "|---|---|---|---|---|---|---|---|---|"]
     for r in table:
         lines.append(f"| {r['kernel']} | {'comm' if r['kernel'] in COMM else 'compute'} | {r['launches']} | "
-                     f"{r['start_us']} | {r['end_us']} | {r['dur_us']} | {r['waves']} |")
+                     f"{r['start_us']} | {r['end_us']} | {r['dur_us']} | {r['waves']} | "
+                     f"{r['wave_p50_us']} / {r['wave_p90_us']} | {r['start_p90_us']} |")
     lines += ["", "Offsets are relative to the step's trunk_fwd start (first step excluded); every wave records"
               " its start / end with s_memrealtime (10 ns), a launch = the union of its waves.", ""]
     lines += ["First replayed step (launches starting before the second trunk_fwd; us from the first trunk_fwd start):",
