@@ -109,6 +109,25 @@ def test_overlap_schedule_bitwise_equals_serial(cuda_device, graph_steps):
     assert lo == ls and co == cs
 
 
+@pytest.mark.parametrize("B", [200, 1500])
+def test_one_wave_conv1_tail_bitwise_equals_reduce_parts(cuda_device, B):
+    """The OVERLAP step tail's conv1 reduce + update on 80 one-wave workgroups (adadelta_c1_kernel,
+    the slice tree on cross-lane moves; B = 1500 reads the group sums c1red) == the same work as the
+    20 conv1 parts of the 256-thread reduce launch (hook c1_lanes=0), bit for bit, gradients included."""
+    n = 2000 if B == 200 else 3000
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(13))
+    _, ms_a, ta = _trainer(cuda_device, graph_steps=3, n_train=n, B=B, overlap=True)
+    _, ms_b, tb = _trainer(cuda_device, graph_steps=3, n_train=n, B=B, overlap=True, hooks={"c1_lanes": 0})
+    assert ta.engine.c1_lanes and not tb.engine.c1_lanes
+    for ep in (1, 2):
+        ta.train_epoch(ep, idx)
+        tb.train_epoch(ep, idx)
+    torch.cuda.synchronize()
+    for name in ("param", "square_avg", "acc_delta", "grad"):
+        assert torch.equal(getattr(ms_a, name), getattr(ms_b, name)), name
+    assert torch.equal(ta.loss_log, tb.loss_log)
+
+
 @pytest.mark.parametrize("graph_steps", [0, 2])
 def test_overlap_schedule_large_batch_bitwise_equals_serial(cuda_device, graph_steps):
     """B > 1024: fc_bwd's split partials are summed on the comm stream (ahead of the fc update) in
