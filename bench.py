@@ -210,6 +210,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu", action="store_true", help="reference CPU config (mnist.py --no-cuda, batch 64)")
     ap.add_argument("--no-script-run", dest="script_run", action="store_false",
                     help="skip the mnist_ddp.py child job (total_cost_time_s)")
+    ap.add_argument("--script-last", dest="script_first", action="store_false",
+                    help="run the mnist_ddp.py child job after this process's own run, beside its idle GPU "
+                         "contexts (default: first, before any rank of this job touches a GPU - as a user "
+                         "runs the command)")
     ap.add_argument("--no-warm-replay", dest="warm_replay", action="store_false",
                     help="do not replay the timed region's graphs (state restored) before the warmup")
     ap.add_argument("--warm-replay-steps", type=int, default=int(os.environ.get("MNIST_AMD_WARM_STEPS", "500")),
@@ -333,6 +337,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     t_setup = time.perf_counter()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    from pytorch_mnist_ddp_amd.engine.trainer import make_streams
+    make_streams(dev)          # the engine's stream pair first: hardware queues of their own
     use_pg = world > 1 or (args.force_comm and "MASTER_ADDR" in os.environ)
     pending = None
     if use_pg:
@@ -340,7 +346,8 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
         with phases.phase("pg_init"):
             # lazy (no device_id): ProcessGroupNCCL never builds a communicator - the engine's all-reduce
             # runs on its own RCCL communicator or the xGMI kernels, verdicts over the TCPStore
-            dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank)
+            if not dist.is_initialized():       # (the reference-first child job initialised it)
+                dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank)
         if args.allreduce != "xgmi":
             # the RCCL communicator (as the driver): rccl / fastest start its non-blocking init now, while
             # data and model build; auto on one node defers it - the trainer starts it only if xGMI fails
@@ -520,22 +527,15 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
                     break
 
     # ---- the reference's own metric, measured the reference's way (child job at the same N)
-    script = None
-    if args.full_run and args.script_run:
+    script = getattr(args, "_script_first", None)
+    if args.full_run and args.script_run and not args.script_first:
         diag.phase = "reference_script"
         torch.cuda.synchronize()
         if use_pg:
             barrier()
         if rank == 0:
             try:
-                extra = []     # non-default transport choices carry over to the child job
-                if args.dist_backend != "nccl":
-                    extra += ["--dist-backend", args.dist_backend]
-                if args.allreduce != "auto":
-                    extra += ["--allreduce", args.allreduce]
-                if args.dtype != "bf16":
-                    extra += ["--dtype", args.dtype]
-                script = run_reference_script(world, B, args.epochs, extra=extra)
+                script = run_reference_script(world, B, args.epochs, extra=_script_extra(args))
             except Exception as e:  # noqa: BLE001 - reported in the JSON
                 script = {"error": f"{type(e).__name__}: {e}"}
         if use_pg:   # the other ranks wait on the store (host-side), leaving their GPUs to the child job
@@ -598,6 +598,41 @@ def run_rank(args, world: int, rank: int, local: int, diag: Diag) -> dict | None
     return out
 
 
+def _script_extra(args) -> list[str]:
+    extra = []     # non-default transport choices carry over to the child job
+    if args.dist_backend != "nccl":
+        extra += ["--dist-backend", args.dist_backend]
+    if args.allreduce != "auto":
+        extra += ["--allreduce", args.allreduce]
+    if args.dtype != "bf16":
+        extra += ["--dtype", args.dtype]
+    return extra
+
+
+def reference_first(args, world: int, rank: int, use_pg: bool) -> dict | None:
+    """The reference-timer child job before this job touches a GPU: the ranks meet on the process
+    group's store (no device work: the nccl group is lazy), rank 0 runs ``mnist_ddp.py`` at this N, the
+    others wait host-side.  Measured like a user's run on idle GPUs - run after the bench, beside its
+    processes' idle HIP contexts, the child's runtime bring-up took 0.12 s instead of 0.06
+    (``--script-last``)."""
+    if use_pg and not dist.is_initialized():
+        dist.init_process_group(args.dist_backend, init_method="env://", world_size=world, rank=rank)
+    script = None
+    if rank == 0:
+        try:
+            script = run_reference_script(world, args.batch_size, args.epochs, extra=_script_extra(args))
+        except Exception as e:  # noqa: BLE001 - reported in the JSON
+            script = {"error": f"{type(e).__name__}: {e}"}
+        script["order"] = "first"
+    if use_pg:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("bench/script_first_done", "1")
+        else:
+            store.wait(["bench/script_first_done"], timedelta(seconds=1200))
+    return script
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
@@ -620,6 +655,9 @@ def main(argv=None) -> int:
     diag = Diag(rank, world)
     rc = 0
     try:
+        if args.full_run and args.script_run and args.script_first:
+            diag.phase = "reference_script"
+            args._script_first = reference_first(args, world, rank, use_pg)
         out = run_rank(args, world, rank, local, diag)
         if out is not None:
             print(json.dumps(out), flush=True)

@@ -487,6 +487,26 @@ PYBIND11_MODULE(_C, m) {
     return reinterpret_cast<uintptr_t>(st);
   }, py::arg("device"), py::arg("dedicated") = true, py::arg("priority") = 0);
   m.def("destroy_stream", [](uintptr_t s) { (void)hipStreamDestroy(S(s)); });
+  // do two streams hand off through device counters (x waits for y's signal, then y for x's)?  False
+  // when they share a hardware queue: the first wait times out (timeout_s) before the signal queued
+  // behind it runs.  Engine-independent form of Engine::probe_stream_handoff (make_streams).
+  m.def("probe_streams", [](uintptr_t xs, uintptr_t ys, double timeout_s) {
+    hipStream_t x = S(xs), y = S(ys);
+    int* c = nullptr;
+    if (hipMalloc(&c, 4 * sizeof(int)) != hipSuccess) throw std::runtime_error("probe_streams: hipMalloc failed");
+    launch_fill(c, 4 * sizeof(int), 0, x);
+    bool ok = hipStreamSynchronize(x) == hipSuccess;
+    launch_stream_wait(c + 0, c + 2, 1, c + 3, x, timeout_s);
+    launch_stream_signal(c + 0, y);
+    launch_stream_wait(c + 1, c + 2, 1, c + 3, y, timeout_s);
+    launch_stream_signal(c + 1, x);
+    ok = ok && hipStreamSynchronize(x) == hipSuccess && hipStreamSynchronize(y) == hipSuccess;
+    int err = 1;
+    if (ok) ok = hipMemcpyAsync(&err, c + 3, sizeof(int), hipMemcpyDeviceToHost, x) == hipSuccess &&
+                 hipStreamSynchronize(x) == hipSuccess;
+    (void)hipFree(c);
+    return ok && err == 0;
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("x"), py::arg("y"), py::arg("timeout_s") = 0.5);
   m.def("synth_render", [](uintptr_t plan, uintptr_t templates, int64_t n, uintptr_t out, uintptr_t stream) {
     launch_synth_render(P<const void>(plan), P<const float>(templates), n, P<uint8_t>(out), S(stream));
     check_launch();

@@ -266,6 +266,12 @@ def _prewarm_body(device, steps: dict | None = None) -> None:
     from .ops import native
     C = native.load()                        # the _C extension (dlopen; no device work)
     lap("native_load")
+    # the engine's stream pair before any other stream of the process - the default stream included -
+    # so that each has a hardware queue of its own (engine/trainer.py make_streams; brings the
+    # runtime and the context up)
+    from .engine.trainer import make_streams
+    make_streams(device)
+    lap("engine_streams")
     # GIL released: the HIP runtime + context, then every kernel TU's code object
     t_rt, t_co, t_cp, t_ms, t_h2d, t_d2h = C.hip_prewarm(device.index if device.index is not None else 0)
     steps["hip_runtime_context"], steps["code_objects"] = round(t_rt, 4), round(t_co, 4)
@@ -460,6 +466,8 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
                                       "setup_info": setup.info, "allreduce": trainer.allreduce if distributed else None,
                                       "transport_report": trainer.transport_report or None,
+                                      "schedule": ["serial", "overlap", "rccl", "xgmi"][trainer.engine.schedule],
+                                      "graph_steps": trainer.graph_steps if trainer.use_graphs else 0,
                                       "t_start_unix": setup.origin,
                                       "trainer_ready_unix": setup.origin + setup.marks.get("trainer", 0.0)})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,

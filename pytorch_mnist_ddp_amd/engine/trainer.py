@@ -110,51 +110,52 @@ class StartupValidationError(RuntimeError):
 _ENGINE_STREAMS: dict[int, tuple] = {}
 
 
-def under_profiler() -> bool:
-    """The process runs under rocprofv3 (its ``ROCPROF_*`` environment).  rocprofv3 segfaults in its
-    exit-time teardown (``__cxa_finalize``, after every kernel ran and the bench line was printed, so
-    the trace is lost) in a process that created CU-masked streams (profiles/r6/final/prof_b200_cumask.log);
-    profiled runs therefore use plain non-blocking streams, which get queues of their own anyway while
-    the process holds fewer streams than GPU_MAX_HW_QUEUES (one trainer: two)."""
-    return any(k.startswith("ROCPROF") for k in os.environ)
+_STREAM_KIND: dict[int, str] = {}
 
 
-_STREAM_FALLBACK: list[str] = []
-
-
-def stream_kind() -> str:
-    if under_profiler():
-        return "plain (rocprofv3)"
-    return f"plain (CU-masked stream failed: {_STREAM_FALLBACK[0]})" if _STREAM_FALLBACK else "cu_masked"
+def stream_kind(device: int | None = None) -> str:
+    if not _STREAM_KIND:
+        return "not created"
+    return _STREAM_KIND.get(device, next(iter(_STREAM_KIND.values())))
 
 
 def make_streams(dev) -> tuple:
-    """The trainers' compute and comm streams: one process-wide pair per device, each on a HARDWARE
-    QUEUE OF ITS OWN (``_C.create_stream``: a CU-masked stream over every CU, which the HIP runtime
-    never shares with another stream).  Streams from torch's pool or plain ``hipStreamCreate`` land
-    on a pooled queue (GPU_MAX_HW_QUEUES per process, 4 by default); once a process holds more streams
-    than that, a new stream shares a queue with an older one, and a trainer whose streams share queues
-    ran its step 4.6x slower (63 -> 290 us at B = 200: ``tools/queue_mapping.py``,
-    profiles/r6/queues/) - the bimodal slow mode seen in round 5 (docs/DEBUGGING.md).  Trainers of one
-    process run one after another on the same pair (each chunk ends joined, so nothing of one trainer
-    is left in flight when the next one enqueues)."""
+    """The trainers' compute and comm streams: one process-wide pair per device of NON-BLOCKING
+    streams, created before any other stream of the process (the driver's prewarm thread and bench.py
+    call this right after the HIP context exists), so each lands on a hardware queue of its own.
+
+    Why both properties (profiles/r6/queues/, profiles/r6/ab/stream_kind/):
+    * hardware queues: the HIP runtime maps streams onto a pool of GPU_MAX_HW_QUEUES queues per
+      process (4); a stream created after the pool is used up shares a queue with an older one, and a
+      trainer whose streams landed on shared queues ran its device-counter-chained step 4.6x slower
+      (63 -> 290 us at B = 200, ``tools/queue_mapping.py``) - round 5's bimodal slow mode.  Two
+      streams created first (the legacy default stream being the only older one) get queues of their
+      own, and every trainer of the process reuses them;
+    * non-blocking: CU-masked streams (``_C.create_stream(dedicated=True)``, which the runtime never
+      puts on a shared queue) are BLOCKING streams - they synchronise with the legacy default stream,
+      which torch uses for its host reads (``.item()`` of a logged loss) and small fills.  With them
+      the reference's 20-epoch run (``mnist_ddp.py``) trained at 72.5-73.2 us/step instead of the
+      62.1-62.3 it reaches on non-blocking streams (Total cost time 0.66-0.76 -> 0.59-0.60 s), although
+      bench.py's timed window, which touches no default-stream op, read 61.2 with either.
+    The pair is probed at once (``_C.probe_streams``: device-counter hand-offs both ways, 0.5 s timeout);
+    if the two non-blocking streams share a queue anyway - a process with a smaller queue pool
+    (GPU_MAX_HW_QUEUES=2 in the one-GPU multi-rank rehearsals) or streams made before them - the pair
+    becomes two CU-masked streams instead: dedicated queues, blocking semantics (``stream_kind``)."""
     dev = torch.device(dev)
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     pair = _ENGINE_STREAMS.get(key)
     if pair is None:
         C = native.load()
-        dedicated = not under_profiler()
-
-        def one():
-            try:
-                return C.create_stream(key, dedicated, 0)
-            except RuntimeError as e:              # (a runtime without CU-masked queues: plain stream)
-                if not dedicated:
-                    raise
-                _STREAM_FALLBACK.append(str(e))
-                return C.create_stream(key, False, 0)
-        pair = tuple(torch.cuda.ExternalStream(one(), device=torch.device("cuda", key)) for _ in range(2))
+        raw = [C.create_stream(key, False, 0) for _ in range(2)]
+        kind = "non-blocking, created first (own hardware queues)"
+        if not C.probe_streams(raw[0], raw[1]):
+            for r in raw:
+                C.destroy_stream(r)
+            raw = [C.create_stream(key, True, 0) for _ in range(2)]
+            kind = "cu_masked (the non-blocking pair shared a hardware queue)"
+        pair = tuple(torch.cuda.ExternalStream(r, device=torch.device("cuda", key)) for r in raw)
         _ENGINE_STREAMS[key] = pair
+        _STREAM_KIND[key] = kind
     return pair
 
 
