@@ -212,6 +212,11 @@ def _run_module(args, model, device, train_data, test_data, train_stream, test_s
     _save(args, model, distributed, rank, ddp_script)
 
 
+def _stream_kind() -> str:
+    from .engine.trainer import stream_kind
+    return stream_kind()
+
+
 def _schedule_name(trainer) -> str | None:
     eng = getattr(trainer, "engine", None)
     return ["serial", "overlap", "rccl", "xgmi"][eng.schedule] if eng is not None else None
@@ -471,7 +476,7 @@ def _run_fused(args, model, device, train_data, test_data, train_stream, test_st
             _json_log(args.json_log, {"setup_s": setup.rounded(), "setup_total_s": round(setup.total(), 4),
                                       "setup_info": setup.info, "allreduce": trainer.allreduce if distributed else None,
                                       "transport_report": trainer.transport_report or None,
-                                      "schedule": _schedule_name(trainer),
+                                      "schedule": _schedule_name(trainer), "streams": _stream_kind(),
                                       "t_start_unix": setup.origin,
                                       "trainer_ready_unix": setup.origin + setup.marks.get("trainer", 0.0)})
         rec = {"epoch": epoch, "train_s": st.train_seconds, "steps": st.steps,

@@ -137,7 +137,7 @@ def make_streams(dev) -> tuple:
       the reference's 20-epoch run (``mnist_ddp.py``) trained at 72.5-73.2 us/step instead of the
       62.1-62.3 it reaches on non-blocking streams (Total cost time 0.66-0.76 -> 0.59-0.60 s), although
       bench.py's timed window, which touches no default-stream op, read 61.2 with either.
-    The pair is probed at once (``_C.probe_streams``: device-counter hand-offs both ways, 0.5 s timeout);
+    The pair is probed at once (``_C.probe_streams``: device-counter hand-offs both ways, 50 ms timeout);
     if the two non-blocking streams share a queue anyway - a process with a smaller queue pool
     (GPU_MAX_HW_QUEUES=2 in the one-GPU multi-rank rehearsals) or streams made before them - the pair
     becomes two CU-masked streams instead: dedicated queues, blocking semantics (``stream_kind``)."""
