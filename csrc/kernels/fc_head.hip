@@ -24,16 +24,15 @@ namespace mnist {
 // One fc1 workgroup (row tile x K-chunk) of the R x 32 grid, linear id `lin`.
 template <int MR>
 __device__ __forceinline__ void fc1_tile(const uint16_t* __restrict__ p, const uint16_t* __restrict__ w1,
-                                        float* __restrict__ z1part, int B, int R, int lin) {
+                                        float* __restrict__ z1part, int B, int R, int xcd, int j, int wave) {
   constexpr int KC = NFLAT / FC1_KSPLIT;   // 288
   constexpr int KS = KC / 32;              // 9
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const int m = lane & 15, kg = lane >> 4;
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (linear id mod 8), so
   // give every XCD 4 whole K-chunks (all row tiles of each): a chunk's 74 KB w1 slice is then
   // fetched into ONE XCD's L2 instead of all eight (grid = R x 32, R*32 divisible by 8)
   static_assert(FC1_KSPLIT == 32, "4 K-chunks per XCD");
-  const int xcd = lin & 7, j = lin >> 3;
   const int chunk = 4 * xcd + j / R;
   const int tile = j - (j / R) * R;
   const uint16_t* pb = w1 + (int64_t)(32 * wave + m) * NFLAT + chunk * KC + 8 * kg;
@@ -79,7 +78,8 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const uint16_t* __restrict
                                                       float* __restrict__ z1part, int B) {
   RW_ENTRY();
   TL_SCOPE(TL_FC1);
-  fc1_tile<MR>(p, w1, z1part, B, gridDim.x, blockIdx.x + gridDim.x * blockIdx.y);
+  const int lin = blockIdx.x + gridDim.x * blockIdx.y;
+  fc1_tile<MR>(p, w1, z1part, B, gridDim.x, lin & 7, lin >> 3, threadIdx.x >> 6);
 }
 
 // Large batches: 64 rows x 128 columns per workgroup, K split 4 ways (2304 = 36 stages of 64),
@@ -415,10 +415,13 @@ void launch_head_fwd(const HeadArgs& a, int B, bool train, hipStream_t s) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, B, train ? 1 : 0);
 }
 
-// 4 rows (waves) per workgroup: measured at B = 200 1 row per workgroup (224 WGs) 82.9 us/step,
-// 2 rows 82.1, 4 rows 82.2 - the head is bound by its per-row dependent latency chain
+// One row (wave) per workgroup: the 224 one-wave workgroups spread the rows' partial-sum loads
+// (16 KB each) over 224 CUs instead of 4 rows on each of 56 - the head is a per-row latency chain,
+// and its load phase shortened: B = 200, 600 steps, same box interleaved 61.04-61.47 -> 60.37-60.89
+// us/step over 5 rounds (profiles/r6/ab/head_rows/; round 2's 1 / 2 / 4 rows per workgroup read
+// 82.9 / 82.1 / 82.2 on that step).  Same rows, same math: bitwise the same results.
 void launch_head_train(const HeadArgs& a, int B, int Bp, hipStream_t s) {
-  const dim3 g(Bp / 4), t(256);   // (Bp is a multiple of 32)
+  const dim3 g(Bp), t(64);   // (Bp is a multiple of 32)
   if (fc1_ksplit(B) == FC1_KSPLIT) {
     if (a.idx) hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, true>), g, t, 0, s, a, B);
     else hipLaunchKernelGGL((head_train_kernel<FC1_KSPLIT, false>), g, t, 0, s, a, B);
