@@ -26,7 +26,7 @@ from .data import (DistributedIndexStream, HostLoader, RandomIndexStream, Sequen
 from .models.net import Net
 from .optim import Adadelta, StepLR
 from .utils.checkpoint import load_state_dict, save_state_dict
-from .utils.logging import test_line, total_time_line, train_line
+from .utils.logging import print_line, test_line, total_time_line, train_line
 from .utils.profiling import PhaseTimes
 
 
@@ -549,7 +549,7 @@ def main_mnist_ddp(argv=None) -> int:
         if getattr(e, "fatal", False):
             _fatal_exit(e)
         raise
-    print(total_time_line(time.time() - start))
+    print_line(total_time_line(time.time() - start))
     sys.stdout.flush()
     if "args" in holder:
         close_pending_comm(holder["args"])

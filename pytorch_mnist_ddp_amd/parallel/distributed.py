@@ -63,8 +63,9 @@ def init_distributed_mode(args) -> None:
         args.dist_backend = getattr(args, "pg_backend", None) or "nccl"
     else:
         args.dist_backend = "gloo"
-    print(f"| distributed init (rank {args.rank}): {args.dist_url}, local rank:{args.gpu}, "
-          f"world size:{args.world_size}", flush=True)
+    from ..utils.logging import print_line
+    print_line(f"| distributed init (rank {args.rank}): {args.dist_url}, local rank:{args.gpu}, "
+               f"world size:{args.world_size}")
     dist.init_process_group(backend=args.dist_backend, init_method=args.dist_url, world_size=args.world_size,
                             rank=args.rank, timeout=timedelta(minutes=10))
 

@@ -17,3 +17,12 @@ def test_line(test_loss: float, correct: int, total: int) -> str:
 def total_time_line(seconds: float) -> str:
     # mnist_ddp.py:203 (value is seconds although labelled "ms"; preserved)
     return f'Total cost time:{seconds} ms'
+
+
+def print_line(line: str) -> None:
+    """One whole line in ONE write: lines every rank prints (the distributed-init and Total-cost-time
+    lines) stay whole in a shared pipe even with an unbuffered stdout, where ``print`` writes the text
+    and the newline separately and two ranks' lines can interleave."""
+    import sys
+    sys.stdout.write(line + "\n")
+    sys.stdout.flush()
