@@ -506,7 +506,7 @@ PYBIND11_MODULE(_C, m) {
                  hipStreamSynchronize(x) == hipSuccess;
     (void)hipFree(c);
     return ok && err == 0;
-  }, py::call_guard<py::gil_scoped_release>(), py::arg("x"), py::arg("y"), py::arg("timeout_s") = 0.05);
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("x"), py::arg("y"), py::arg("timeout_s") = 0.5);
   m.def("synth_render", [](uintptr_t plan, uintptr_t templates, int64_t n, uintptr_t out, uintptr_t stream) {
     launch_synth_render(P<const void>(plan), P<const float>(templates), n, P<uint8_t>(out), S(stream));
     check_launch();

@@ -113,6 +113,11 @@ _ENGINE_STREAMS: dict[int, tuple] = {}
 _STREAM_KIND: dict[int, str] = {}
 
 
+def under_profiler() -> bool:
+    """The process runs under rocprofv3 (its ``ROCPROF_*`` environment)."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def stream_kind(device: int | None = None) -> str:
     if not _STREAM_KIND:
         return "not created"
@@ -137,10 +142,13 @@ def make_streams(dev) -> tuple:
       the reference's 20-epoch run (``mnist_ddp.py``) trained at 72.5-73.2 us/step instead of the
       62.1-62.3 it reaches on non-blocking streams (Total cost time 0.66-0.76 -> 0.59-0.60 s), although
       bench.py's timed window, which touches no default-stream op, read 61.2 with either.
-    The pair is probed at once (``_C.probe_streams``: device-counter hand-offs both ways, 50 ms timeout);
+    The pair is probed at once (``_C.probe_streams``: device-counter hand-offs both ways, 0.5 s timeout);
     if the two non-blocking streams share a queue anyway - a process with a smaller queue pool
     (GPU_MAX_HW_QUEUES=2 in the one-GPU multi-rank rehearsals) or streams made before them - the pair
-    becomes two CU-masked streams instead: dedicated queues, blocking semantics (``stream_kind``)."""
+    becomes two CU-masked streams instead: dedicated queues, blocking semantics (``stream_kind``) -
+    except under rocprofv3, whose exit-time teardown segfaults in a process with CU-masked streams
+    (profiles/r6/final/prof_b200_cumask.log): there the pair stays as it is and the trainer's own
+    stream probe picks OVERLAP or SERIAL."""
     dev = torch.device(dev)
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     pair = _ENGINE_STREAMS.get(key)
@@ -148,7 +156,7 @@ def make_streams(dev) -> tuple:
         C = native.load()
         raw = [C.create_stream(key, False, 0) for _ in range(2)]
         kind = "non-blocking, created first (own hardware queues)"
-        if not C.probe_streams(raw[0], raw[1]):
+        if not C.probe_streams(raw[0], raw[1]) and not under_profiler():
             for r in raw:
                 C.destroy_stream(r)
             raw = [C.create_stream(key, True, 0) for _ in range(2)]

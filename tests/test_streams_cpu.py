@@ -50,6 +50,30 @@ def test_make_streams_falls_back_to_dedicated_queues_when_the_pair_shares_one(mo
     monkeypatch.setattr(torch.cuda, "ExternalStream", lambda ptr, device=None: ("stream", ptr))
     monkeypatch.setattr(trainer, "_ENGINE_STREAMS", {})
     monkeypatch.setattr(trainer, "_STREAM_KIND", {})
+    for k in [k for k in list(__import__("os").environ) if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
     pair = trainer.make_streams("cuda:0")
     assert calls == [False, False, True, True] and destroyed == [2001, 2002]
     assert [p[1] for p in pair] == [2003, 2004] and trainer.stream_kind(0).startswith("cu_masked")
+
+
+def test_make_streams_keeps_the_plain_pair_under_rocprofv3(monkeypatch):
+    calls = []
+
+    class FakeC:
+        @staticmethod
+        def create_stream(device, dedicated, priority):
+            calls.append(dedicated)
+            return 3000 + len(calls)
+
+        @staticmethod
+        def probe_streams(x, y, timeout_s=0.5):
+            return False
+
+    monkeypatch.setattr(trainer.native, "load", lambda: FakeC)
+    monkeypatch.setattr(torch.cuda, "ExternalStream", lambda ptr, device=None: ("stream", ptr))
+    monkeypatch.setattr(trainer, "_ENGINE_STREAMS", {})
+    monkeypatch.setattr(trainer, "_STREAM_KIND", {})
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    trainer.make_streams("cuda:0")
+    assert calls == [False, False]                   # no CU-masked streams under the profiler
