@@ -25,12 +25,15 @@ namespace mnist {
 // Phase timing (tools/phase_timing.hip compiles this file with MNIST_PHASE_TIMING): thread 0 of
 // every workgroup records s_memtime at each phase boundary.
 #ifdef MNIST_PHASE_TIMING
-constexpr int kPhaseMaxWG = 4096;
-__device__ uint64_t g_phase_times[kPhaseMaxWG * 8];
-#define PHASE_MARK(i)                                                                          \
-  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < kPhaseMaxWG)                   \
-    g_phase_times[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime();
+// PHASE_MARK_BY(t, i): the same by thread t (tools/exp/trunk_pipe_exp.hip marks a second role).
+constexpr int kPhaseMaxWG = 4096, kPhaseSlots = 16;
+__device__ uint64_t g_phase_times[kPhaseMaxWG * kPhaseSlots];
+#define PHASE_MARK_BY(t, i)                                                                    \
+  if (threadIdx.x == (t) && blockIdx.y * gridDim.x + blockIdx.x < kPhaseMaxWG)                 \
+    g_phase_times[(blockIdx.y * gridDim.x + blockIdx.x) * kPhaseSlots + (i)] = __builtin_amdgcn_s_memtime();
+#define PHASE_MARK(i) PHASE_MARK_BY(0, i)
 #else
+#define PHASE_MARK_BY(t, i)
 #define PHASE_MARK(i)
 #endif
 

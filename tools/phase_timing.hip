@@ -52,13 +52,14 @@ int main(int argc, char** argv) {
   float ms = 0; CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= kReps;
   const int nwg = 3 * B / trunk_strips_per_wg(B);
-  std::vector<uint64_t> t((size_t)nwg * 8);
+  constexpr int S = kPhaseSlots;
+  std::vector<uint64_t> t((size_t)nwg * S);
   CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_phase_times), t.size() * 8));
   const char* names[6] = {"0 loads+W2/x staging", "1 conv1 (VALU)", "1b W2 tail", "2 conv2 MFMA",
                           "3 pool epilogue", "4 dropout+stores"};
   printf("B=%d  kernel %.2f us (events, mean of 50 back-to-back), %d WGs; s_memtime ticks are per-XCD shader clocks\n", B, ms * 1000, nwg);
   std::vector<double> tot;
-  for (int w = 0; w < nwg; ++w) tot.push_back((double)(t[w * 8 + 6] - t[w * 8]));
+  for (int w = 0; w < nwg; ++w) tot.push_back((double)(t[w * S + 6] - t[w * S]));
   std::sort(tot.begin(), tot.end());
   printf("  WG lifetime ticks: median %.0f  p10 %.0f  p90 %.0f\n", tot[nwg / 2], tot[nwg / 10], tot[nwg * 9 / 10]);
   {  // per-XCD (WG id % 8 shares a clock) dispatch spread and span
@@ -66,7 +67,7 @@ int main(int argc, char** argv) {
     for (int x = 0; x < 8; ++x) {
       uint64_t lo = ~0ull, hi = 0, last_start = 0;
       for (int w = x; w < nwg; w += 8) {
-        lo = std::min(lo, t[w * 8]); hi = std::max(hi, t[w * 8 + 6]); last_start = std::max(last_start, t[w * 8]);
+        lo = std::min(lo, t[w * S]); hi = std::max(hi, t[w * S + 6]); last_start = std::max(last_start, t[w * S]);
       }
       st.push_back((double)(last_start - lo)); sp.push_back((double)(hi - lo));
     }
@@ -76,7 +77,7 @@ int main(int argc, char** argv) {
   }
   for (int ph = 0; ph < 6; ++ph) {
     std::vector<double> d;
-    for (int w = 0; w < nwg; ++w) d.push_back((double)(t[w * 8 + ph + 1] - t[w * 8 + ph]));
+    for (int w = 0; w < nwg; ++w) d.push_back((double)(t[w * S + ph + 1] - t[w * S + ph]));
     std::sort(d.begin(), d.end());
     printf("  phase %-22s median %7.0f  p90 %7.0f ticks\n", names[ph], d[nwg / 2], d[nwg * 9 / 10]);
   }
